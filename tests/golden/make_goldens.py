@@ -1,0 +1,118 @@
+#!/usr/bin/env python3
+"""Generate the golden vectors under tests/golden/ from the REFERENCE itself.
+
+Runs oracle/_ref/ref_driver -- the reference's unchanged src/TRPO_FVP.c,
+src/TRPO_CG.c and src/TRPO_Util.c compiled by oracle/Makefile (needs
+/root/reference; only ever run in the build container, never on the GPU box).
+
+Every case is described in manifest.json so that tests can rebuild the exact
+inputs: fixture cases read the reference's own ArmTest*.txt files (copied here
+as data), synthetic cases regenerate inputs with trpo_amd.synth (bit-exact).
+Outputs are written with %.17g, so they round-trip exactly.
+
+    python tests/golden/make_goldens.py
+"""
+from __future__ import annotations
+
+import json
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "trpo-robot-control_amd"))
+from trpo_amd import synth  # noqa: E402
+
+DRIVER = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
+ARM = [15, 16, 16, 3]
+SIGMA3 = [0.6065306597126334, 0.8, 1.3]     # exp(-0.5) and two more, as exact literals
+
+CASES = [
+    # --- reference fixtures (build/ArmTest*.txt) ---
+    dict(name="fix_fvp_n3150", kind="fvp", src="fixture", n=3150, vin="fvp_col1"),
+    dict(name="fix_fvp_n2400", kind="fvp", src="fixture", n=2400, vin="fvp_col1"),
+    dict(name="fix_cg_n3150_th1e-10", kind="cg", src="fixture", n=3150, vin="cg_col1", maxiter=10, resth=1e-10),
+    dict(name="fix_cg_n3150_th0", kind="cg", src="fixture", n=3150, vin="cg_col1", maxiter=10, resth=0.0),
+    dict(name="fix_cg_n2400_th1e-10", kind="cg", src="fixture", n=2400, vin="cg_col1", maxiter=10, resth=1e-10),
+    dict(name="fix_fvp_n1", kind="fvp", src="fixture", n=1, vin="fvp_col1"),
+    dict(name="fix_fvp_n17", kind="fvp", src="fixture", n=17, vin="fvp_col1"),
+    # --- synthetic (trpo_amd.synth, seed 20261015) ---
+    dict(name="syn_sigma_fvp", kind="fvp", src="synth", layers=ARM, acfunc="lttl", n=1000, std=SIGMA3, vin="v"),
+    dict(name="syn_sigma_cg", kind="cg", src="synth", layers=ARM, acfunc="lttl", n=1000, std=SIGMA3, vin="b",
+         maxiter=10, resth=0.0),
+    dict(name="syn_acts_fvp", kind="fvp", src="synth", layers=ARM, acfunc="lsto", n=777, std=SIGMA3, vin="v"),
+    dict(name="syn_deep_fvp", kind="fvp", src="synth", layers=[15, 32, 16, 8, 3], acfunc="lotsl", n=1000,
+         std=[1.0, 1.0, 1.0], vin="v"),
+    dict(name="syn_wide_in_fvp", kind="fvp", src="synth", layers=[376, 64, 64, 17], acfunc="lttl", n=600,
+         std=[1.0] * 17, vin="v"),
+    dict(name="syn_2x64_fvp_n4096", kind="fvp", src="synth", layers=[15, 64, 64, 3], acfunc="lttl", n=4096,
+         std=[1.0, 1.0, 1.0], vin="v"),
+    dict(name="syn_arm_cg_n50000", kind="cg", src="synth", layers=ARM, acfunc="lttl", n=50000,
+         std=[1.0, 1.0, 1.0], vin="b", maxiter=10, resth=0.0),
+    dict(name="syn_2x64_cg_n50000", kind="cg", src="synth", layers=[15, 64, 64, 3], acfunc="lttl", n=50000,
+         std=[1.0, 1.0, 1.0], vin="b", maxiter=10, resth=0.0),
+]
+
+
+def build_inputs(case, tmp):
+    """Returns (model_path, data_path, layers, acfunc, vin_vector)."""
+    if case["src"] == "fixture":
+        layers, acfunc = ARM, "lttl"
+        model, data = os.path.join(HERE, "ArmTestModel.txt"), os.path.join(HERE, "ArmTestData.txt")
+        P = synth.num_params(layers)
+        fname = "ArmTestFVP.txt" if case["vin"] == "fvp_col1" else "ArmTestCG.txt"
+        vin = np.loadtxt(os.path.join(HERE, fname))[:P, 0]
+        return model, data, layers, acfunc, vin
+    layers, acfunc = case["layers"], case["acfunc"]
+    P = synth.num_params(layers)
+    theta = synth.make_theta(layers)
+    obs = synth.make_obs(case["n"], layers[0])
+    model, data = os.path.join(tmp, case["name"] + ".model"), os.path.join(tmp, case["name"] + ".data")
+    synth.write_model_file(model, theta)
+    synth.write_data_file(data, obs, np.asarray(case["std"], dtype=np.float64))
+    vin = synth.make_v(P) if case["vin"] == "v" else synth.make_b(P)
+    return model, data, layers, acfunc, vin
+
+
+def run_case(case, tmp):
+    model, data, layers, acfunc, vin = build_inputs(case, tmp)
+    vpath = os.path.join(tmp, case["name"] + ".in")
+    synth.write_vector_file(vpath, vin)
+    out = os.path.join(HERE, case["name"] + ".txt")
+    lay = ",".join(str(x) for x in layers)
+    if case["kind"] == "fvp":
+        cmd = [DRIVER, "fvp", model, data, str(case["n"]), lay, acfunc, "0.1", vpath, out, "1"]
+    else:
+        cmd = [DRIVER, "cg", model, data, str(case["n"]), lay, acfunc, "0.1", vpath, str(case["maxiter"]),
+               repr(case["resth"]), out, "1"]
+    res = subprocess.run(cmd, capture_output=True, text=True, check=True)
+    rec = dict(case)
+    rec.update(layers=layers, acfunc=acfunc, damping=0.1, expected=os.path.basename(out))
+    if case["kind"] == "cg":
+        hist = re.findall(r"CG Iter\[(\d+)\] Residual Norm=(\S+), Soln Norm=(\S+)", res.stdout)
+        rec["rdotr"] = [float(h[1]) for h in hist]
+        rec["xnorm"] = [float(h[2]) for h in hist]
+        rec["iters"] = len(hist) - 1
+    y = np.loadtxt(out)
+    rec["norm"] = float(np.linalg.norm(y))
+    print("%-24s P=%-5d |out|=%.15g" % (case["name"], len(y), rec["norm"]), flush=True)
+    return rec
+
+
+def main():
+    if not os.path.exists(DRIVER):
+        sys.exit("build the reference first: make -C oracle ref")
+    with tempfile.TemporaryDirectory() as tmp:
+        recs = [run_case(c, tmp) for c in CASES]
+    with open(os.path.join(HERE, "manifest.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_goldens.py", "driver": "oracle/_ref/ref_driver",
+                   "seed": synth.SEED, "cases": recs}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,103 @@
+"""Seeded synthetic TRPO inputs, bit-identical on every host.
+
+The generator uses only integer arithmetic (splitmix64) and exact fp64
+operations -- no transcendental functions -- so the CPU oracle, the reference
+build and the MI355X path all see bit-identical inputs, here and on the GPU box.
+
+Distributions:
+  * observations ~ U[-0.17, 0.19]    (the ArmTestData.txt range)
+  * W ~ N(0, 1/fan_in)   via Irwin-Hall(12) - 6, b = 0, logstd = 0
+  * v ~ U[0, 1)          (as ArmTestFVP.txt column 1)
+  * CG right-hand side b ~ N(0, 1e-2^2)
+"""
+from __future__ import annotations
+
+import numpy as np
+
+SEED = 20261015
+_GOLDEN = np.uint64(0x9E3779B97F4A7C15)
+_M1 = np.uint64(0xBF58476D1CE4E5B9)
+_M2 = np.uint64(0x94D049BB133111EB)
+
+# stream ids keep the different inputs independent
+STREAM_OBS, STREAM_W, STREAM_V, STREAM_B = 1, 2, 3, 4
+
+
+def _splitmix(seed: int, stream: int, count: int, offset: int = 0) -> np.ndarray:
+    base = np.uint64((seed * 0x100000001B3 + stream * 0x9E3779B1) & 0xFFFFFFFFFFFFFFFF)
+    with np.errstate(over="ignore"):
+        i = np.arange(offset + 1, offset + count + 1, dtype=np.uint64)
+        z = base + i * _GOLDEN
+        z = (z ^ (z >> np.uint64(30))) * _M1
+        z = (z ^ (z >> np.uint64(27))) * _M2
+        z = z ^ (z >> np.uint64(31))
+    return z
+
+
+def uniform(seed: int, stream: int, count: int, lo: float = 0.0, hi: float = 1.0,
+            offset: int = 0) -> np.ndarray:
+    u = (_splitmix(seed, stream, count, offset) >> np.uint64(11)).astype(np.float64) * (2.0 ** -53)
+    return lo + (hi - lo) * u
+
+
+def normal(seed: int, stream: int, count: int, sigma: float = 1.0) -> np.ndarray:
+    """Irwin-Hall(12) approximation of N(0, sigma^2): exact arithmetic only."""
+    u = uniform(seed, stream, 12 * count).reshape(count, 12)
+    acc = np.zeros(count)
+    for j in range(12):          # fixed summation order
+        acc = acc + u[:, j]
+    return (acc - 6.0) * sigma
+
+
+def num_params(layers) -> int:
+    """src/TRPO_Util.c:7-17."""
+    p = 0
+    for i in range(len(layers) - 1):
+        p += layers[i] * layers[i + 1] + layers[i + 1]
+    return p + layers[-1]
+
+
+def make_theta(layers, seed: int = SEED, logstd: float = 0.0) -> np.ndarray:
+    """Flat parameters in the reference layout: W[i] [in][out], B[i], ..., LogStd."""
+    parts = []
+    for i in range(len(layers) - 1):
+        fan_in, out = layers[i], layers[i + 1]
+        w = normal(seed + 1000 * i, STREAM_W, fan_in * out, sigma=1.0 / np.sqrt(float(fan_in)))
+        parts += [w, np.zeros(out)]
+    parts.append(np.full(layers[-1], logstd))
+    return np.concatenate(parts)
+
+
+def make_obs(n: int, obs_dim: int, seed: int = SEED) -> np.ndarray:
+    return uniform(seed, STREAM_OBS, n * obs_dim, -0.17, 0.19).reshape(n, obs_dim)
+
+
+def make_v(P: int, seed: int = SEED) -> np.ndarray:
+    return uniform(seed, STREAM_V, P)
+
+
+def make_b(P: int, seed: int = SEED) -> np.ndarray:
+    return normal(seed, STREAM_B, P, sigma=1e-2)
+
+
+def write_model_file(path: str, theta: np.ndarray) -> None:
+    """One value per line (src/TRPO_FVP.c:670-699)."""
+    with open(path, "w") as f:
+        f.write("\n".join("%.17g" % x for x in theta))
+        f.write("\n")
+
+
+def write_data_file(path: str, obs: np.ndarray, std: np.ndarray, mean: np.ndarray | None = None) -> None:
+    """Per sample: Mean[A] Std[A] Obs[O] Action[A] Adv (src/TRPO_FVP.c:731-762).
+    Action and Advantage are zero: the FVP/CG path never reads them."""
+    n, _ = obs.shape
+    A = len(std)
+    if mean is None:
+        mean = np.zeros((n, A))
+    zeros = np.zeros((n, A + 1))
+    table = np.concatenate([mean, np.broadcast_to(std, (n, A)), obs, zeros], axis=1)
+    np.savetxt(path, table, fmt="%.17g")
+
+
+def write_vector_file(path: str, v: np.ndarray) -> None:
+    np.savetxt(path, np.asarray(v, dtype=np.float64), fmt="%.17g")
