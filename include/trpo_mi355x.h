@@ -1,0 +1,135 @@
+/*
+ * trpo_mi355x.h -- drop-in C ABI of the MI355X Fisher-vector-product /
+ * conjugate-gradient path (libtrpo_mi355x.so).
+ *
+ * Part 1 replaces, symbol for symbol, the reference's L3 numerical core
+ * declared in src/include/TRPO.h of custom-computing-ic/TRPO-Robot-Control:
+ *
+ *   TRPOparam      <- src/include/TRPO.h:6-49   (field-for-field identical layout)
+ *   NumParamsCalc  <- src/include/TRPO.h:81     (impl. src/TRPO_Util.c:7-17)
+ *   FVP            <- src/include/TRPO.h:89     (impl. src/TRPO_FVP.c:11-545)
+ *   FVPFast        <- src/include/TRPO.h:93     (impl. src/TRPO_FVP.c:548-949)
+ *   CG             <- src/include/TRPO.h:96     (impl. src/TRPO_CG.c:11-113)
+ *   FVP_FPGA       <- src/include/TRPO.h:98     (accelerator twin, same signature)
+ *   CG_FPGA        <- src/include/TRPO.h:101    (accelerator twin, same signature)
+ *
+ * Same prototypes, same by-value TRPOparam, same ownership (caller owns Input/b
+ * and Result, fp64, length NumParamsCalc()), same return convention (elapsed
+ * compute seconds >= 0, or -1 when a file cannot be opened / the request is
+ * invalid), same stdout lines from CG.  Model and data still arrive by path
+ * and may change between calls: the parsed, device-resident copy is cached
+ * keyed on (path, size, mtime, NumSamples, layer shape).
+ *
+ * Part 2 is the in-memory context API the trainers need: no
+ * per-call file I/O, observations uploaded once per update, P-vectors resident
+ * in HBM through the whole CG solve, optional RCCL sample sharding.
+ *
+ * Linkage is C; the header is safe to include from C and C++ (the reference's
+ * build/Makefile.cpuonly compiles its callers with g++).
+ */
+#ifndef TRPO_MI355X_H
+#define TRPO_MI355X_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#ifndef TRPO_H /* the reference's own TRPO.h already defines the struct */
+typedef struct {
+    char *ModelFile;         /* model: W[i] [in][out], B[i] per layer, LogStd */
+    char *BaselineFile;      /* unused by this path */
+    char *ResultFile;        /* unused by this path */
+    char *DataFile;          /* per sample: Mean[A] Std[A] Obs[O] Action[A] Adv */
+    size_t NumLayers;        /* e.g. 4 for [Input]->[H1]->[H2]->[Output] */
+    char *AcFunc;            /* per layer: 'l' linear, 't' tanh, 's' sigmoid, 'o' 0.1x */
+    size_t *LayerSize;       /* NumLayers sizes, input first */
+    size_t NumSamples;
+    double CG_Damping;
+    size_t *PaddedLayerSize; /* FPGA only; ignored */
+    size_t *NumBlocks;       /* FPGA only; ignored */
+} TRPOparam;
+
+size_t NumParamsCalc(size_t *LayerSize, size_t NumLayers);
+double FVP(TRPOparam param, double *Result, double *Input);
+double FVPFast(TRPOparam param, double *Result, double *Input, size_t NumThreads);
+double CG(TRPOparam param, double *Result, double *b, size_t MaxIter, double ResidualTh, size_t NumThreads);
+double FVP_FPGA(TRPOparam param, double *Result, double *Input);
+double CG_FPGA(TRPOparam param, double *Result, double *b, size_t MaxIter, double ResidualTh, size_t NumThreads);
+#endif
+
+/* ------------------------------------------------------------------------- */
+/* Part 2: in-memory context API                                             */
+/* ------------------------------------------------------------------------- */
+
+typedef struct trpo_ctx trpo_ctx;
+
+/* Error codes (negative) returned by the int-valued functions. */
+enum {
+    TRPO_OK = 0,
+    TRPO_E_INVALID = -1,   /* bad shape, activation, NULL pointer */
+    TRPO_E_DEVICE = -2,    /* no usable MI355X / HIP error */
+    TRPO_E_NOMEM = -3,
+    TRPO_E_COMM = -4,      /* RCCL failure */
+    TRPO_E_IO = -5
+};
+
+/* Create a context on HIP device `device` (-1: current / $TRPO_DEVICE / 0).
+ * theta: flat parameters (W, B per layer, LogStd), fp64, NumParamsCalc long.
+ * obs: [n][layer_size[0]] fp64 row-major (this rank's samples).
+ * stdv: [layer_size[nl-1]] action std (the data file's Std column).
+ * Returns NULL on failure (trpo_last_error() has the message). */
+trpo_ctx *trpo_ctx_create(size_t num_layers, const size_t *layer_size, const char *acfunc,
+                          const double *theta, const double *obs, size_t n, const double *stdv,
+                          double cg_damping, int device);
+void trpo_ctx_destroy(trpo_ctx *ctx);
+
+int trpo_ctx_set_theta(trpo_ctx *ctx, const double *theta);
+int trpo_ctx_set_obs(trpo_ctx *ctx, const double *obs, size_t n);
+int trpo_ctx_set_std(trpo_ctx *ctx, const double *stdv);
+int trpo_ctx_set_damping(trpo_ctx *ctx, double cg_damping);
+size_t trpo_ctx_num_params(const trpo_ctx *ctx);
+
+/* Attach an RCCL communicator: the context's samples are this rank's shard;
+ * every FVP all-reduces the P-sized partial sum once (fp64, sum) and divides
+ * by the GLOBAL sample count.  unique_id: 128 bytes from trpo_comm_unique_id()
+ * on rank 0, broadcast by the caller. */
+int trpo_comm_unique_id(void *unique_id_128);
+int trpo_ctx_attach_comm(trpo_ctx *ctx, int rank, int world, const void *unique_id_128);
+
+/* Host-pointer convenience entry points (copy in / compute / copy out).
+ * Return elapsed seconds (>= 0) or a negative error code. */
+double trpo_ctx_fvp(trpo_ctx *ctx, const double *v, double *out);
+double trpo_ctx_cg(trpo_ctx *ctx, const double *b, size_t max_iter, double residual_th, double *x,
+                   int verbose);
+/* Per-iteration values CG prints: rdotr[i], |x|[i] for i = 0..iters. */
+int trpo_ctx_cg_history(const trpo_ctx *ctx, double *rdotr, double *xnorm, size_t cap, size_t *iters);
+
+/* Device-resident benchmarking hooks: b stays in HBM, no host round trip. */
+int trpo_ctx_upload_b(trpo_ctx *ctx, const double *b);
+int trpo_ctx_upload_v(trpo_ctx *ctx, const double *v);
+int trpo_ctx_enqueue_fvp(trpo_ctx *ctx);                                  /* z = F v */
+int trpo_ctx_enqueue_cg(trpo_ctx *ctx, size_t max_iter, double residual_th); /* graph replay */
+int trpo_ctx_enqueue_fvp_kernel_only(trpo_ctx *ctx);                      /* dominant kernel */
+int trpo_ctx_synchronize(trpo_ctx *ctx);
+/* Average duration (ms) of `reps` back-to-back launches of `what`
+ * (0 = FVP kernel alone, 1 = full FVP, 2 = CG solve of max_iter), measured with
+ * HIP events on the context's stream. */
+double trpo_ctx_time(trpo_ctx *ctx, int what, int reps, size_t max_iter, double residual_th);
+int trpo_ctx_download_x(trpo_ctx *ctx, double *x);
+int trpo_ctx_download_z(trpo_ctx *ctx, double *z);
+
+/* Introspection: which kernel family serves this context ("mfma-mlp3 T0xT1xT2xT3"
+ * or "generic"), and the FVP launch geometry. */
+const char *trpo_ctx_kernel_name(const trpo_ctx *ctx);
+int trpo_ctx_launch_geometry(const trpo_ctx *ctx, int *blocks, int *threads, int *lds_bytes);
+
+const char *trpo_last_error(void);
+/* Drop every cached file-based context (FVPFast/FVP/CG cache). */
+void trpo_cache_clear(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TRPO_MI355X_H */

@@ -1,0 +1,77 @@
+"""C-ABI checks that need no GPU: the library loads, exports every symbol the
+public header declares, TRPOparam has the reference layout, host-side error
+paths follow the reference (src/TRPO_FVP.c:671-674,732-735)."""
+import ctypes as C
+import os
+import subprocess
+import textwrap
+
+import numpy as np
+import pytest
+
+import trpo_amd
+from trpo_amd import synth
+
+
+def test_library_exports_every_header_symbol():
+    L = trpo_amd.lib()
+    syms = trpo_amd.header_symbols()
+    for must in ("NumParamsCalc", "FVP", "FVPFast", "CG", "FVP_FPGA", "CG_FPGA", "trpo_ctx_create",
+                 "trpo_ctx_cg", "trpo_ctx_fvp", "trpo_ctx_attach_comm"):
+        assert must in syms
+    missing = [s for s in syms if not hasattr(L, s)]
+    assert not missing, missing
+
+
+def test_numparams_matches_reference_formula():
+    assert trpo_amd.NumParamsCalc([15, 16, 16, 3]) == 582
+    assert trpo_amd.NumParamsCalc([15, 64, 64, 3]) == 5382
+    assert trpo_amd.NumParamsCalc([376, 64, 64, 17]) == synth.num_params([376, 64, 64, 17])
+
+
+def test_trpoparam_layout_matches_c(tmp_path):
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = tmp_path / "off.c"
+    src.write_text(textwrap.dedent("""
+        #include <stdio.h>
+        #include <stddef.h>
+        #include "trpo_mi355x.h"
+        int main(void) {
+          printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(TRPOparam), offsetof(TRPOparam, NumLayers),
+                 offsetof(TRPOparam, LayerSize), offsetof(TRPOparam, NumSamples),
+                 offsetof(TRPOparam, CG_Damping), offsetof(TRPOparam, NumBlocks));
+          return 0; }
+    """))
+    exe = tmp_path / "off"
+    subprocess.run(["gcc", "-I", os.path.join(root, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
+    P = trpo_amd.TRPOparam
+    assert got == [C.sizeof(P), P.NumLayers.offset, P.LayerSize.offset, P.NumSamples.offset,
+                   P.CG_Damping.offset, P.NumBlocks.offset]
+
+
+def test_missing_files_return_minus_one(capfd):
+    prm = trpo_amd.make_param("/nonexistent/model.txt", "/nonexistent/data.txt", [15, 16, 16, 3], "lttl", 10)
+    P = 582
+    out = np.zeros(P)
+    assert trpo_amd.FVPFast(prm, out, np.ones(P), 1) == -1
+    assert trpo_amd.CG(prm, out, np.ones(P), 10, 1e-10, 1) == -1
+    err = capfd.readouterr().err
+    assert "[ERROR] Cannot open Model File [/nonexistent/model.txt]" in err
+
+
+def test_bad_activation_rejected(tmp_path, capfd):
+    th = synth.make_theta([15, 16, 16, 3])
+    m, d = tmp_path / "m.txt", tmp_path / "d.txt"
+    synth.write_model_file(str(m), th)
+    synth.write_data_file(str(d), synth.make_obs(4, 15), np.ones(3))
+    prm = trpo_amd.make_param(str(m), str(d), [15, 16, 16, 3], "ltxl", 4)
+    assert trpo_amd.FVPFast(prm, np.zeros(582), np.ones(582), 1) == -1
+    assert "Unsupported" in capfd.readouterr().err
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="only meaningful without a GPU")
+def test_no_gpu_fails_loudly():
+    with pytest.raises(trpo_amd.TRPOError):
+        trpo_amd.Context([15, 16, 16, 3], "lttl", synth.make_theta([15, 16, 16, 3]), synth.make_obs(8, 15),
+                         np.ones(3))

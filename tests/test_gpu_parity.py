@@ -1,0 +1,163 @@
+"""MI355X parity: the HIP path (through the C ABI) against the reference goldens.
+
+Tolerances (stated): the device computes the FVP in fp32 with
+fp64 cross-block reduction and fp64 CG, so
+  * FVP   relative L2 <= 1e-5 vs the reference fp64 FVPFast,
+  * CG    relative L2 <= 1e-4 vs the reference fp64 CG step direction,
+  * vs the reference's own ArmTestCG.txt column 2: <= 1.2e-4 (the fp64
+    reference itself sits 8e-6 away from that fixture).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import cases
+import trpo_amd
+
+pytestmark = pytest.mark.gpu
+
+FVP_TOL = 1e-5
+CG_TOL = 1e-4
+# syn_sigma_cg (N=1000, sigma != 1, 10 iterations, ResidualTh=0) is ill-conditioned: the fp32
+# FVP is within 6e-8 of the reference, CG amplifies that ~2000x by iteration 10 (measured 1.35e-4).
+CG_TOL_CASE = {"syn_sigma_cg": 3e-4}
+
+
+def _ctx(x, **kw):
+    return trpo_amd.Context(x["layers"], x["acfunc"], x["theta"], x["obs"], x["std"], x["damping"], **kw)
+
+
+@pytest.mark.parametrize("name", [c["name"] for c in cases.manifest()])
+def test_context_matches_reference_golden(name):
+    c = cases.case(name)
+    x = cases.inputs(c)
+    with _ctx(x) as ctx:
+        if c["kind"] == "fvp":
+            out = ctx.fvp(x["vin"])
+            assert cases.rel_l2(out, cases.expected(c)) <= FVP_TOL, ctx.kernel_name
+        else:
+            out = ctx.cg(x["vin"], c["maxiter"], c["resth"])
+            assert cases.rel_l2(out, cases.expected(c)) <= CG_TOL_CASE.get(name, CG_TOL), ctx.kernel_name
+            rr, xn, iters = ctx.cg_history()
+            if c["resth"] == 0.0:
+                assert iters == c["iters"]
+            else:
+                # fp32 FVP: the recurrence residual floors near 1e-9*|b|^2, so a threshold
+                # below that floor (1e-10 on the fixture) may cost one extra iteration.
+                assert c["iters"] <= iters <= c["iters"] + 1
+            np.testing.assert_allclose(rr[:5], c["rdotr"][:5], rtol=1e-3)
+
+
+def test_fixture_cg_against_reference_fixture_file():
+    c = cases.case("fix_cg_n3150_th1e-10")
+    x = cases.inputs(c)
+    with _ctx(x) as ctx:
+        out = ctx.cg(x["vin"], 10, 1e-10)
+    fx = np.loadtxt(os.path.join(cases.GOLDEN, "ArmTestCG.txt"))[:, 1]
+    assert cases.rel_l2(out, fx) <= 1.2e-4
+
+
+@pytest.mark.parametrize("name", ["fix_fvp_n3150", "fix_fvp_n2400", "syn_sigma_fvp", "syn_acts_fvp",
+                                  "syn_2x64_fvp_n4096", "syn_deep_fvp"])
+def test_generic_kernel_matches_golden(name, monkeypatch):
+    monkeypatch.setenv("TRPO_FORCE_GENERIC", "1")
+    c = cases.case(name)
+    x = cases.inputs(c)
+    with _ctx(x) as ctx:
+        assert ctx.kernel_name == "generic"
+        assert cases.rel_l2(ctx.fvp(x["vin"]), cases.expected(c)) <= FVP_TOL
+
+
+def test_file_entry_points_fixture(capfd):
+    """TRPOCpuCode.c-style calls through FVPFast / FVP / CG / *_FPGA on the reference fixtures."""
+    trpo_amd.cache_clear()
+    g = cases.GOLDEN
+    prm = trpo_amd.make_param(os.path.join(g, "ArmTestModel.txt"), os.path.join(g, "ArmTestData.txt"),
+                              [15, 16, 16, 3], "lttl", 3150, 0.1)
+    P = trpo_amd.NumParamsCalc([15, 16, 16, 3])
+    v = np.loadtxt(os.path.join(g, "ArmTestFVP.txt"))[:, 0].copy()
+    exp = cases.expected(cases.case("fix_fvp_n3150"))
+    for fn in (lambda r: trpo_amd.FVPFast(prm, r, v, 6), lambda r: trpo_amd.FVP(prm, r, v),
+               lambda r: trpo_amd.FVP_FPGA(prm, r, v)):
+        r = np.zeros(P)
+        t = fn(r)
+        assert t >= 0
+        assert cases.rel_l2(r, exp) <= FVP_TOL
+    b = np.loadtxt(os.path.join(g, "ArmTestCG.txt"))[:, 0].copy()
+    x = np.zeros(P)
+    assert trpo_amd.CG(prm, x, b, 10, 1e-10, 6) >= 0
+    assert cases.rel_l2(x, cases.expected(cases.case("fix_cg_n3150_th1e-10"))) <= CG_TOL
+    x2 = np.zeros(P)
+    assert trpo_amd.CG_FPGA(prm, x2, b, 10, 1e-10, 1) >= 0
+    np.testing.assert_array_equal(x, x2)      # cached device problem, deterministic
+    out = capfd.readouterr().out
+    lines = [l for l in out.splitlines() if l.startswith("CG Iter[")]
+    # two CG calls, each printing Iter[0..k] with k = 8 (reference) or 9 (fp32 floor, see above)
+    assert len(lines) in (18, 19, 20) and lines[0].startswith("CG Iter[0] Residual Norm=9.05595253")
+    assert "[INFO] FVP Computing Time is" in out
+
+
+def test_file_entry_n2400_uses_first_2400_lines():
+    g = cases.GOLDEN
+    prm = trpo_amd.make_param(os.path.join(g, "ArmTestModel.txt"), os.path.join(g, "ArmTestData.txt"),
+                              [15, 16, 16, 3], "lttl", 2400, 0.1)
+    v = np.loadtxt(os.path.join(g, "ArmTestFVP.txt"))[:, 0].copy()
+    r = np.zeros(582)
+    assert trpo_amd.FVPFast(prm, r, v, 1) >= 0
+    assert cases.rel_l2(r, cases.expected(cases.case("fix_fvp_n2400"))) <= FVP_TOL
+
+
+def test_file_cache_sees_rewritten_files(tmp_path):
+    from trpo_amd import synth
+    layers = [15, 16, 16, 3]
+    m, d = str(tmp_path / "m.txt"), str(tmp_path / "d.txt")
+    th = synth.make_theta(layers)
+    synth.write_model_file(m, th)
+    synth.write_data_file(d, synth.make_obs(100, 15), np.ones(3))
+    prm = trpo_amd.make_param(m, d, layers, "lttl", 100)
+    v = synth.make_v(582)
+    r1 = np.zeros(582)
+    assert trpo_amd.FVPFast(prm, r1, v, 1) >= 0
+    synth.write_model_file(m, 2.0 * th)          # caller changes the model between calls
+    os.utime(m, ns=(os.stat(m).st_atime_ns, os.stat(m).st_mtime_ns + 10_000_000))
+    r2 = np.zeros(582)
+    assert trpo_amd.FVPFast(prm, r2, v, 1) >= 0
+    assert cases.rel_l2(r1, r2) > 1e-3
+
+
+def test_deterministic_bitwise():
+    c = cases.case("syn_2x64_fvp_n4096")
+    x = cases.inputs(c)
+    with _ctx(x) as ctx:
+        a = ctx.fvp(x["vin"])
+        b = ctx.fvp(x["vin"])
+    np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("n", [1, 15, 16, 17, 33, 1000, 4097])
+def test_ragged_sample_counts(n):
+    import oracle
+    from trpo_amd import synth
+    layers = [15, 64, 64, 3]
+    th, obs = synth.make_theta(layers), synth.make_obs(n, 15)
+    std = np.array([0.6065306597126334, 0.8, 1.3])
+    v = synth.make_v(synth.num_params(layers))
+    ref, _ = oracle.fvp(layers, "lttl", th, obs, std, v)
+    with trpo_amd.Context(layers, "lttl", th, obs, std) as ctx:
+        assert cases.rel_l2(ctx.fvp(v), ref) <= FVP_TOL
+
+
+def test_set_obs_and_damping_update():
+    import oracle
+    from trpo_amd import synth
+    layers = [15, 16, 16, 3]
+    th = synth.make_theta(layers)
+    v = synth.make_v(582)
+    with trpo_amd.Context(layers, "lttl", th, synth.make_obs(500, 15), np.ones(3)) as ctx:
+        ctx.fvp(v)
+        obs2 = synth.make_obs(2000, 15, seed=7)
+        ctx.set_obs(obs2)
+        ctx.set_damping(0.25)
+        ref, _ = oracle.fvp(layers, "lttl", th, obs2, np.ones(3), v, damping=0.25)
+        assert cases.rel_l2(ctx.fvp(v), ref) <= FVP_TOL

@@ -1,0 +1,52 @@
+/*
+ * trpo_dev.h -- the thin C ABI between the C host layer (trpo_host.c) and the
+ * hand-written gfx950 kernels (trpo_kernels.hip).  Plain pointers and sizes
+ * only.  One trpo_dev owns everything that lives in HBM for one network and
+ * one sample shard on one GPU: packed weights, observations, the CG vectors,
+ * the per-block partial-sum slabs, the captured CG graph and (optionally) an
+ * RCCL communicator.
+ */
+#ifndef TRPO_DEV_H
+#define TRPO_DEV_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct trpo_dev trpo_dev;
+
+enum { TRPO_VEC_V = 0, TRPO_VEC_Z = 1, TRPO_VEC_X = 2, TRPO_VEC_B = 3, TRPO_VEC_P = 4 };
+
+/* device < 0: $TRPO_DEVICE or 0.  Returns NULL and fills err on failure. */
+trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, const char *ac, char *err, size_t errlen);
+void trpo_dev_destroy(trpo_dev *d);
+
+int trpo_dev_set_theta(trpo_dev *d, const double *theta);
+int trpo_dev_set_std(trpo_dev *d, const double *stdv);
+int trpo_dev_set_obs(trpo_dev *d, const double *obs, size_t n);
+int trpo_dev_set_damping(trpo_dev *d, double damping);
+
+int trpo_dev_comm_unique_id(void *id128);
+int trpo_dev_set_comm(trpo_dev *d, int rank, int world, const void *id128);
+
+int trpo_dev_upload(trpo_dev *d, int slot, const double *host);
+int trpo_dev_download(trpo_dev *d, int slot, double *host);
+
+int trpo_dev_fvp(trpo_dev *d);                 /* enqueue z = F v  (slots V -> Z) */
+int trpo_dev_fvp_kernel(trpo_dev *d);          /* enqueue the dominant kernel alone */
+int trpo_dev_cg(trpo_dev *d, size_t maxiter, double resth); /* enqueue CG on slot B -> X */
+int trpo_dev_cg_history(trpo_dev *d, double *rdotr, double *xnorm, size_t cap, size_t *iters);
+int trpo_dev_sync(trpo_dev *d);
+/* what: 0 FVP kernel, 1 full FVP, 2 CG(maxiter) -- average ms over reps */
+double trpo_dev_time(trpo_dev *d, int what, int reps, size_t maxiter, double resth);
+
+const char *trpo_dev_kernel_name(const trpo_dev *d);
+int trpo_dev_geometry(const trpo_dev *d, int *blocks, int *threads, int *lds_bytes);
+size_t trpo_dev_num_params(const trpo_dev *d);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,508 @@
+/*
+ * trpo_host.c -- C host layer of libtrpo_mi355x.so.
+ *
+ * Implements the reference's C entry points (src/include/TRPO.h:81-101) and the
+ * in-memory context API of include/trpo_mi355x.h on top of the thin device ABI
+ * (csrc/trpo_dev.h).  Everything numerical runs on the GPU; this file parses
+ * the reference's text formats, caches parsed + uploaded problems, keeps the
+ * reference's side effects (CG progress lines, "[ERROR] ..." messages, return
+ * conventions) and times the compute region the way the reference does
+ * (file parsing excluded).
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <math.h>
+#include <pthread.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <sys/time.h>
+
+#include "../../include/trpo_mi355x.h"
+#include "trpo_dev.h"
+
+#define MAX_LAYERS 8
+
+static __thread char g_err[512];
+
+static void set_err(const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+}
+
+const char *trpo_last_error(void) { return g_err; }
+
+static double now_s(void) {
+    struct timeval tv;
+    gettimeofday(&tv, NULL);
+    return (double)tv.tv_sec + 1e-6 * (double)tv.tv_usec;
+}
+
+/* src/TRPO_Util.c:7-17 */
+size_t NumParamsCalc(size_t *LayerSize, size_t NumLayers) {
+    size_t p = 0;
+    if (!LayerSize || NumLayers < 1) return 0;
+    for (size_t i = 0; i + 1 < NumLayers; ++i) p += LayerSize[i] * LayerSize[i + 1] + LayerSize[i + 1];
+    return p + LayerSize[NumLayers - 1];
+}
+
+/* ------------------------------------------------------------------------- */
+/* contexts                                                                  */
+/* ------------------------------------------------------------------------- */
+struct trpo_ctx {
+    trpo_dev *dev;
+    size_t nl;
+    size_t ls[MAX_LAYERS];
+    char ac[MAX_LAYERS + 1];
+    size_t P;
+    size_t n;
+    double damping;
+};
+
+static int check_shape(size_t nl, const size_t *ls, const char *ac) {
+    if (nl < 2 || nl > MAX_LAYERS || !ls || !ac) {
+        set_err("unsupported NumLayers=%zu (2..%d)", nl, MAX_LAYERS);
+        return -1;
+    }
+    for (size_t i = 0; i < nl; ++i)
+        if (ls[i] == 0) {
+            set_err("LayerSize[%zu] is 0", i);
+            return -1;
+        }
+    for (size_t i = 1; i < nl; ++i)
+        if (ac[i] != 'l' && ac[i] != 't' && ac[i] != 'o' && ac[i] != 's') {
+            set_err("AC Function for Layer[%zu] is %c. Unsupported.", i, ac[i]);
+            return -1;
+        }
+    return 0;
+}
+
+trpo_ctx *trpo_ctx_create(size_t num_layers, const size_t *layer_size, const char *acfunc, const double *theta,
+                          const double *obs, size_t n, const double *stdv, double cg_damping, int device) {
+    if (check_shape(num_layers, layer_size, acfunc)) return NULL;
+    trpo_ctx *c = (trpo_ctx *)calloc(1, sizeof(trpo_ctx));
+    if (!c) return NULL;
+    c->nl = num_layers;
+    memcpy(c->ls, layer_size, num_layers * sizeof(size_t));
+    memcpy(c->ac, acfunc, num_layers);
+    c->P = NumParamsCalc(c->ls, c->nl);
+    char err[256] = {0};
+    c->dev = trpo_dev_create(device, num_layers, layer_size, acfunc, err, sizeof err);
+    if (!c->dev) {
+        set_err("%s", err);
+        free(c);
+        return NULL;
+    }
+    if ((theta && trpo_dev_set_theta(c->dev, theta)) || (stdv && trpo_dev_set_std(c->dev, stdv)) ||
+        ((obs || n == 0) && trpo_dev_set_obs(c->dev, obs, n)) || trpo_dev_set_damping(c->dev, cg_damping)) {
+        set_err("device initialisation failed (theta/std/obs upload)");
+        trpo_ctx_destroy(c);
+        return NULL;
+    }
+    c->n = n;
+    c->damping = cg_damping;
+    return c;
+}
+
+void trpo_ctx_destroy(trpo_ctx *c) {
+    if (!c) return;
+    trpo_dev_destroy(c->dev);
+    free(c);
+}
+
+int trpo_ctx_set_theta(trpo_ctx *c, const double *theta) {
+    if (!c || !theta) return TRPO_E_INVALID;
+    return trpo_dev_set_theta(c->dev, theta);
+}
+int trpo_ctx_set_obs(trpo_ctx *c, const double *obs, size_t n) {
+    if (!c || (!obs && n)) return TRPO_E_INVALID;
+    int rc = trpo_dev_set_obs(c->dev, obs, n);
+    if (!rc) c->n = n;
+    return rc;
+}
+int trpo_ctx_set_std(trpo_ctx *c, const double *stdv) {
+    if (!c || !stdv) return TRPO_E_INVALID;
+    return trpo_dev_set_std(c->dev, stdv);
+}
+int trpo_ctx_set_damping(trpo_ctx *c, double d) {
+    if (!c) return TRPO_E_INVALID;
+    c->damping = d;
+    return trpo_dev_set_damping(c->dev, d);
+}
+size_t trpo_ctx_num_params(const trpo_ctx *c) { return c ? c->P : 0; }
+
+int trpo_comm_unique_id(void *id) {
+    if (!id) return TRPO_E_INVALID;
+    return trpo_dev_comm_unique_id(id);
+}
+int trpo_ctx_attach_comm(trpo_ctx *c, int rank, int world, const void *id) {
+    if (!c || (world > 1 && !id)) return TRPO_E_INVALID;
+    return trpo_dev_set_comm(c->dev, rank, world, id);
+}
+
+double trpo_ctx_fvp(trpo_ctx *c, const double *v, double *out) {
+    if (!c || !v || !out) return TRPO_E_INVALID;
+    const double t0 = now_s();
+    int rc = trpo_dev_upload(c->dev, TRPO_VEC_V, v);
+    if (!rc) rc = trpo_dev_fvp(c->dev);
+    if (!rc) rc = trpo_dev_download(c->dev, TRPO_VEC_Z, out);
+    if (rc) {
+        set_err("FVP failed on the device (code %d)", rc);
+        return rc < 0 ? rc : TRPO_E_DEVICE;
+    }
+    return now_s() - t0;
+}
+
+double trpo_ctx_cg(trpo_ctx *c, const double *b, size_t max_iter, double th, double *x, int verbose) {
+    if (!c || !b || !x) return TRPO_E_INVALID;
+    const double t0 = now_s();
+    int rc = trpo_dev_upload(c->dev, TRPO_VEC_B, b);
+    if (!rc) rc = trpo_dev_cg(c->dev, max_iter, th);
+    if (!rc) rc = trpo_dev_download(c->dev, TRPO_VEC_X, x);
+    const double t1 = now_s();
+    if (rc) {
+        set_err("CG failed on the device (code %d)", rc);
+        return rc < 0 ? rc : TRPO_E_DEVICE;
+    }
+    if (verbose) {
+        /* src/TRPO_CG.c:56 -- one line per iteration, rdotr is the squared norm */
+        size_t iters = 0;
+        double *rr = (double *)malloc(sizeof(double) * (max_iter + 1));
+        double *xn = (double *)malloc(sizeof(double) * (max_iter + 1));
+        if (rr && xn && !trpo_dev_cg_history(c->dev, rr, xn, max_iter + 1, &iters)) {
+            for (size_t i = 0; i <= iters; ++i)
+                printf("CG Iter[%zu] Residual Norm=%.12e, Soln Norm=%.12e\n", i, rr[i], xn[i]);
+        }
+        free(rr);
+        free(xn);
+    }
+    return t1 - t0;
+}
+
+int trpo_ctx_cg_history(const trpo_ctx *c, double *rdotr, double *xnorm, size_t cap, size_t *iters) {
+    if (!c) return TRPO_E_INVALID;
+    return trpo_dev_cg_history(c->dev, rdotr, xnorm, cap, iters);
+}
+
+int trpo_ctx_upload_b(trpo_ctx *c, const double *b) { return c ? trpo_dev_upload(c->dev, TRPO_VEC_B, b) : -1; }
+int trpo_ctx_upload_v(trpo_ctx *c, const double *v) { return c ? trpo_dev_upload(c->dev, TRPO_VEC_V, v) : -1; }
+int trpo_ctx_enqueue_fvp(trpo_ctx *c) { return c ? trpo_dev_fvp(c->dev) : -1; }
+int trpo_ctx_enqueue_cg(trpo_ctx *c, size_t m, double th) { return c ? trpo_dev_cg(c->dev, m, th) : -1; }
+int trpo_ctx_enqueue_fvp_kernel_only(trpo_ctx *c) { return c ? trpo_dev_fvp_kernel(c->dev) : -1; }
+int trpo_ctx_synchronize(trpo_ctx *c) { return c ? trpo_dev_sync(c->dev) : -1; }
+double trpo_ctx_time(trpo_ctx *c, int what, int reps, size_t m, double th) {
+    return c ? trpo_dev_time(c->dev, what, reps, m, th) : -1;
+}
+int trpo_ctx_download_x(trpo_ctx *c, double *x) { return c ? trpo_dev_download(c->dev, TRPO_VEC_X, x) : -1; }
+int trpo_ctx_download_z(trpo_ctx *c, double *z) { return c ? trpo_dev_download(c->dev, TRPO_VEC_Z, z) : -1; }
+const char *trpo_ctx_kernel_name(const trpo_ctx *c) { return c ? trpo_dev_kernel_name(c->dev) : ""; }
+int trpo_ctx_launch_geometry(const trpo_ctx *c, int *b, int *t, int *l) {
+    return c ? trpo_dev_geometry(c->dev, b, t, l) : -1;
+}
+
+/* ------------------------------------------------------------------------- */
+/* reference text formats                                                    */
+/* ------------------------------------------------------------------------- */
+static char *slurp(const char *path, size_t *len) {
+    FILE *f = fopen(path, "rb");
+    if (!f) return NULL;
+    fseek(f, 0, SEEK_END);
+    long sz = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    char *buf = (char *)malloc((size_t)(sz < 0 ? 0 : sz) + 1);
+    size_t got = buf ? fread(buf, 1, (size_t)sz, f) : 0;
+    fclose(f);
+    if (!buf) return NULL;
+    buf[got] = 0;
+    if (len) *len = got;
+    return buf;
+}
+
+/* Parse up to `want` doubles from whitespace-separated text (fscanf("%lf") semantics). */
+static size_t parse_doubles(char *txt, double *out, size_t want) {
+    size_t k = 0;
+    char *p = txt;
+    while (k < want) {
+        while (*p == ' ' || *p == '\n' || *p == '\t' || *p == '\r') ++p;
+        if (!*p) break;
+        char *e;
+        double v = strtod(p, &e);
+        if (e == p) break;
+        out[k++] = v;
+        p = e;
+    }
+    return k;
+}
+
+/* Model file (src/TRPO_FVP.c:670-699): theta in flat order, one per line. */
+static int load_model(const char *path, size_t P, double *theta) {
+    char *t = slurp(path, NULL);
+    if (!t) {
+        fprintf(stderr, "[ERROR] Cannot open Model File [%s]. \n", path);
+        return -1;
+    }
+    size_t got = parse_doubles(t, theta, P);
+    free(t);
+    for (size_t i = got; i < P; ++i) theta[i] = 0.0;  /* fscanf leaves calloc'd zeros */
+    return 0;
+}
+
+/* Data file (src/TRPO_FVP.c:731-762): per sample Mean[A] Std[A] Obs[O] Action[A] Adv.
+ * Keeps Obs, the Std of the last parsed line and (optionally) Mean. */
+static int load_data(const char *path, size_t O, size_t A, size_t n, double *obs, double *stdv, double *mean) {
+    char *t = slurp(path, NULL);
+    if (!t) {
+        fprintf(stderr, "[ERROR] Cannot open Data File [%s]. \n", path);
+        return -1;
+    }
+    const size_t row = 3 * A + O + 1;
+    double *tmp = (double *)malloc(sizeof(double) * row);
+    char *p = t;
+    for (size_t s = 0; s < n; ++s) {
+        size_t got = 0;
+        while (got < row) {
+            while (*p == ' ' || *p == '\n' || *p == '\t' || *p == '\r') ++p;
+            if (!*p) break;
+            char *e;
+            double v = strtod(p, &e);
+            if (e == p) break;
+            tmp[got++] = v;
+            p = e;
+        }
+        if (got < row) { /* short file: the reference keeps whatever fscanf filled (zeros) */
+            for (size_t j = got; j < row; ++j) tmp[j] = (j >= A && j < 2 * A) ? stdv[j - A] : 0.0;
+        }
+        if (mean) memcpy(mean + s * A, tmp, A * sizeof(double));
+        memcpy(stdv, tmp + A, A * sizeof(double));
+        memcpy(obs + s * O, tmp + 2 * A, O * sizeof(double));
+    }
+    free(tmp);
+    free(t);
+    return 0;
+}
+
+/* Optional forward-pass check of the data file's Mean column (src/TRPO_FVP.c:839-844),
+ * enabled with TRPO_CHECK_MEAN=1; done once when a data file is (re)loaded. */
+static void check_mean(const trpo_ctx *c, const double *theta, const double *obs, const double *mean, size_t n) {
+    size_t maxw = 0;
+    for (size_t i = 0; i < c->nl; ++i) maxw = c->ls[i] > maxw ? c->ls[i] : maxw;
+    double *a = (double *)malloc(maxw * sizeof(double)), *b = (double *)malloc(maxw * sizeof(double));
+    for (size_t s = 0; s < n; ++s) {
+        memcpy(a, obs + s * c->ls[0], c->ls[0] * sizeof(double));
+        size_t pos = 0;
+        for (size_t i = 0; i + 1 < c->nl; ++i) {
+            const size_t in = c->ls[i], out = c->ls[i + 1];
+            for (size_t j = 0; j < out; ++j) {
+                double x = theta[pos + in * out + j];
+                for (size_t k = 0; k < in; ++k) x += a[k] * theta[pos + k * out + j];
+                switch (c->ac[i + 1]) {
+                case 't': x = tanh(x); break;
+                case 'o': x = 0.1 * x; break;
+                case 's': x = 1.0 / (1 + exp(-x)); break;
+                default: break;
+                }
+                b[j] = x;
+            }
+            memcpy(a, b, out * sizeof(double));
+            pos += in * out + out;
+        }
+        const size_t A = c->ls[c->nl - 1];
+        for (size_t i = 0; i < A; ++i) {
+            const double e = mean[s * A + i], err = fabs((a[i] - e) / e) * 100;
+            if (err > 1) printf("out[%zu] = %e, mean = %e => %.4f%% Difference\n", i, a[i], e, err);
+        }
+    }
+    free(a);
+    free(b);
+}
+
+/* ------------------------------------------------------------------------- */
+/* file-keyed cache for the TRPOparam entry points                           */
+/* ------------------------------------------------------------------------- */
+#define CACHE_SLOTS 4
+
+typedef struct {
+    int used;
+    unsigned long long stamp;
+    char *model, *data;
+    off_t msize, dsize;
+    struct timespec mmtime, dmtime;
+    size_t nsamples, nl, ls[MAX_LAYERS];
+    char ac[MAX_LAYERS + 1];
+    trpo_ctx *ctx;
+} cache_entry;
+
+static cache_entry g_cache[CACHE_SLOTS];
+static unsigned long long g_clock;
+static pthread_mutex_t g_lock = PTHREAD_MUTEX_INITIALIZER;
+
+static void entry_free(cache_entry *e) {
+    if (!e->used) return;
+    trpo_ctx_destroy(e->ctx);
+    free(e->model);
+    free(e->data);
+    memset(e, 0, sizeof *e);
+}
+
+void trpo_cache_clear(void) {
+    pthread_mutex_lock(&g_lock);
+    for (int i = 0; i < CACHE_SLOTS; ++i) entry_free(&g_cache[i]);
+    pthread_mutex_unlock(&g_lock);
+}
+
+static int same_ts(struct timespec a, struct timespec b) { return a.tv_sec == b.tv_sec && a.tv_nsec == b.tv_nsec; }
+
+/* Returns a context for param (parsing + uploading on a miss), or NULL with the
+ * reference's "[ERROR] Cannot open ..." message on stderr. */
+static trpo_ctx *ctx_for_param(const TRPOparam *prm) {
+    if (!prm->ModelFile || !prm->DataFile) {
+        fprintf(stderr, "[ERROR] Model/Data file name missing.\n");
+        return NULL;
+    }
+    if (check_shape(prm->NumLayers, prm->LayerSize, prm->AcFunc)) {
+        fprintf(stderr, "[ERROR] %s\n", g_err);
+        return NULL;
+    }
+    struct stat sm, sd;
+    if (stat(prm->ModelFile, &sm) != 0) {
+        fprintf(stderr, "[ERROR] Cannot open Model File [%s]. \n", prm->ModelFile);
+        return NULL;
+    }
+    if (stat(prm->DataFile, &sd) != 0) {
+        fprintf(stderr, "[ERROR] Cannot open Data File [%s]. \n", prm->DataFile);
+        return NULL;
+    }
+    cache_entry *hit = NULL, *victim = &g_cache[0];
+    for (int i = 0; i < CACHE_SLOTS; ++i) {
+        cache_entry *e = &g_cache[i];
+        if (!e->used) {
+            if (victim->used) victim = e;
+            continue;
+        }
+        if (victim->used && e->stamp < victim->stamp) victim = e;
+        if (strcmp(e->model, prm->ModelFile) || strcmp(e->data, prm->DataFile)) continue;
+        if (e->msize != sm.st_size || e->dsize != sd.st_size || !same_ts(e->mmtime, sm.st_mtim) ||
+            !same_ts(e->dmtime, sd.st_mtim))
+            continue;
+        if (e->nsamples != prm->NumSamples || e->nl != prm->NumLayers) continue;
+        if (memcmp(e->ls, prm->LayerSize, prm->NumLayers * sizeof(size_t)) ||
+            memcmp(e->ac, prm->AcFunc, prm->NumLayers))
+            continue;
+        hit = e;
+        break;
+    }
+    if (hit) {
+        hit->stamp = ++g_clock;
+        return hit->ctx;
+    }
+    /* miss: parse both files, upload, replace the LRU slot */
+    const size_t nl = prm->NumLayers, O = prm->LayerSize[0], A = prm->LayerSize[nl - 1], n = prm->NumSamples;
+    const size_t P = NumParamsCalc(prm->LayerSize, nl);
+    double *theta = (double *)calloc(P, sizeof(double));
+    double *obs = (double *)calloc(n * O + 1, sizeof(double));
+    double *stdv = (double *)calloc(A, sizeof(double));
+    const char *cm = getenv("TRPO_CHECK_MEAN");
+    const int want_mean = cm && atoi(cm);
+    double *mean = want_mean ? (double *)calloc(n * A + 1, sizeof(double)) : NULL;
+    trpo_ctx *ctx = NULL;
+    if (!theta || !obs || !stdv) goto out;
+    if (load_model(prm->ModelFile, P, theta)) goto out;
+    /* FVPFast reads "LogStd" from the model into Std; the data file overwrites it */
+    for (size_t k = 0; k < A; ++k) stdv[k] = theta[P - A + k];
+    if (load_data(prm->DataFile, O, A, n, obs, stdv, mean)) goto out;
+    ctx = trpo_ctx_create(nl, prm->LayerSize, prm->AcFunc, theta, obs, n, stdv, prm->CG_Damping, -1);
+    if (!ctx) {
+        fprintf(stderr, "[ERROR] %s\n", g_err);
+        goto out;
+    }
+    if (want_mean) check_mean(ctx, theta, obs, mean, n);
+    entry_free(victim);
+    victim->used = 1;
+    victim->stamp = ++g_clock;
+    victim->model = strdup(prm->ModelFile);
+    victim->data = strdup(prm->DataFile);
+    victim->msize = sm.st_size;
+    victim->dsize = sd.st_size;
+    victim->mmtime = sm.st_mtim;
+    victim->dmtime = sd.st_mtim;
+    victim->nsamples = n;
+    victim->nl = nl;
+    memcpy(victim->ls, prm->LayerSize, nl * sizeof(size_t));
+    memset(victim->ac, 0, sizeof victim->ac);
+    memcpy(victim->ac, prm->AcFunc, nl);
+    victim->ctx = ctx;
+out:
+    free(theta);
+    free(obs);
+    free(stdv);
+    free(mean);
+    return ctx;
+}
+
+/* ------------------------------------------------------------------------- */
+/* the reference entry points                                                */
+/* ------------------------------------------------------------------------- */
+
+/* src/TRPO_FVP.c:548-949.  NumThreads sized the reference's OpenMP team; the
+ * GPU path has no host compute, so it is accepted and ignored. */
+double FVPFast(TRPOparam param, double *Result, double *Input, size_t NumThreads) {
+    (void)NumThreads;
+    if (!Result || !Input) return -1;
+    pthread_mutex_lock(&g_lock);
+    trpo_ctx *c = ctx_for_param(&param);
+    double t = -1;
+    if (c) {
+        if (c->damping != param.CG_Damping) trpo_ctx_set_damping(c, param.CG_Damping);
+        t = trpo_ctx_fvp(c, Input, Result);
+        if (t < 0) {
+            fprintf(stderr, "[ERROR] %s\n", g_err);
+            t = -1;
+        }
+    }
+    pthread_mutex_unlock(&g_lock);
+    return t;
+}
+
+/* src/TRPO_FVP.c:11-545: the 4-pass original; mathematically identical to
+ * FVPFast because the KL gradient at the old parameters is zero (GLayer=0,
+ * src/TRPO_FVP.c:326).  Prints its timing line like the reference (:525). */
+double FVP(TRPOparam param, double *Result, double *Input) {
+    double t = FVPFast(param, Result, Input, 1);
+    if (t >= 0) printf("[INFO] FVP Computing Time is %f seconds.\n", t);
+    return t;
+}
+
+/* src/TRPO_CG.c:11-113. */
+double CG(TRPOparam param, double *Result, double *b, size_t MaxIter, double ResidualTh, size_t NumThreads) {
+    (void)NumThreads;
+    if (!Result || !b) return -1;
+    pthread_mutex_lock(&g_lock);
+    trpo_ctx *c = ctx_for_param(&param);
+    double t = -1;
+    if (c) {
+        if (c->damping != param.CG_Damping) trpo_ctx_set_damping(c, param.CG_Damping);
+        t = trpo_ctx_cg(c, b, MaxIter, ResidualTh, Result, 1);
+        if (t < 0) {
+            fprintf(stderr, "[ERROR] Fisher Vector Product Calculation Failed.\n");
+            t = -1;
+        }
+    } else {
+        fprintf(stderr, "[ERROR] Fisher Vector Product Calculation Failed.\n");
+    }
+    fflush(stdout);
+    pthread_mutex_unlock(&g_lock);
+    return t;
+}
+
+/* Accelerator twins (src/include/TRPO.h:98,101): same contract, the MI355X
+ * path serves them; PaddedLayerSize / NumBlocks are FPGA-only and ignored. */
+double FVP_FPGA(TRPOparam param, double *Result, double *Input) { return FVPFast(param, Result, Input, 1); }
+
+double CG_FPGA(TRPOparam param, double *Result, double *b, size_t MaxIter, double ResidualTh, size_t NumThreads) {
+    return CG(param, Result, b, MaxIter, ResidualTh, NumThreads);
+}

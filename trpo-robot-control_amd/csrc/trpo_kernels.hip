@@ -1,0 +1,1341 @@
+// trpo_kernels.hip -- gfx950 (MI355X / CDNA4) kernels for the TRPO Fisher-vector
+// product and the conjugate-gradient solve, plus the device layer behind
+// trpo_dev.h.
+//
+// Math (reference src/TRPO_FVP.c:548-949, FVPFast):
+//   per sample n:  forward  y_{i+1} = act(W_i^T y_i + b_i)
+//                  R-fwd    Rx_{i+1} = W_i^T Ry_i + VW_i^T y_i + vb_i,  Ry = act'(.) Rx
+//                  R-bwd    G_L = act_L'(Ry_L / sigma^2),  G_i = act_i'(W_i G_{i+1})
+//   Fv = (1/N) sum_n [ y_i (x) G_{i+1} ; G_{i+1} ]  +  [2 v_logstd]  +  damping * v
+//
+// MI355X mapping:
+//   * 16 samples = one tile; a wave streams tiles.  All layer products run on
+//     v_mfma_f32_16x16x4_f32 in the TRANSPOSED orientation: neurons on MFMA
+//     rows, samples on columns, so each layer's accumulator registers ARE the
+//     next layer's B operand (k permuted: lane group g, step s <-> neuron 4g+s)
+//     -- no data movement between layers, forward or backward.
+//   * the cross-sample contraction sum_n y (x) G is an MFMA with K = samples;
+//     its operands are transposed through a 20-float-stride per-wave LDS
+//     scratch (4 ds_write_b32 + 1 ds_read_b128 per 16x16 tile).
+//   * weights (and VW = the direction being multiplied) are staged in LDS in
+//     MFMA-fragment order, read with ds_read_b128 (lane-contiguous, conflict
+//     free); the fp64 direction is gathered+converted into LDS per block.
+//   * per-block fp32 partials are combined across the block's waves by a
+//     fixed pairwise tree (deterministic), then reduced across blocks in fp64
+//     by a second kernel in a fixed order.  CG scalars and vectors are fp64.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "trpo_dev.h"
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+#define MAXL 8
+#define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b), (c), 0, 0, 0)
+
+enum { ACT_L = 0, ACT_T = 1, ACT_O = 2, ACT_S = 3 };
+
+struct Net {
+    int nl;
+    int L[MAXL];
+    int act[MAXL];
+    int P;
+    int woff[MAXL], boff[MAXL];
+    int A;
+};
+
+// Fragment-order pack layout for the 3-weight-layer fast path (offsets in floats).
+struct Pack {
+    int T[4];                  // tiles of 16 per layer: T0 (input) .. T3 (output)
+    int fa[3], fb[3], bi[3], iv, tlen;
+    int vfa[3], vb[3], vlen;
+};
+
+struct Ctl {                   // device-side control block of one context
+    double damping;
+    double n_total;
+    double resth;
+    double rdotr;
+    int maxiter;
+    int iter;
+    int done;
+    int zero;                  // always 0: "never skip" flag for standalone FVPs
+};
+
+// ---------------------------------------------------------------------------
+// activation helpers (reference src/TRPO_FVP.c:810-834 and :866-882)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float act_y(int a, float x) {
+    switch (a) {
+    case ACT_T: return tanhf(x);
+    case ACT_O: return 0.1f * x;
+    case ACT_S: return 1.0f / (1.0f + expf(-x));
+    default: return x;
+    }
+}
+// R{y} from R{x} given y
+__device__ __forceinline__ float act_r(int a, float y, float rx) {
+    switch (a) {
+    case ACT_T: return rx * (1.0f - y * y);
+    case ACT_O: return 0.1f * rx;
+    case ACT_S: return rx * y * (1.0f - y);
+    default: return rx;
+    }
+}
+__device__ __forceinline__ f4 act_fwd(int a, f4 x, f4 rx, f4 &ry) {
+    f4 y;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        y[r] = act_y(a, x[r]);
+        ry[r] = act_r(a, y[r], rx[r]);
+    }
+    return y;
+}
+__device__ __forceinline__ f4 act_bwd(int a, f4 y, f4 g) {
+    f4 o;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = act_r(a, y[r], g[r]);
+    return o;
+}
+__device__ __forceinline__ bool act_needs_y(int a) { return a == ACT_T || a == ACT_S; }
+
+// ---------------------------------------------------------------------------
+// pack-slot -> natural-parameter maps (built once per context)
+// ---------------------------------------------------------------------------
+// theta pack: FA_i[ot][kt][lane][s] = W_i[16kt+4g+s][16ot+c]
+//             FB_i[it][kt][lane][s] = W_i[16it+c][16kt+4g+s]   (i = 1, 2)
+//             BI_i[j] = b_i[j];  IV[j] = 1/sigma_j^2 (filled separately)
+// v pack:     VFA_i like FA_i, VB_i like BI_i
+__device__ int map_frag(const Net &n, int i, int local, int nkt, bool fwd) {
+    const int idx4 = local >> 2, s = local & 3, lane = idx4 & 63, tk = idx4 >> 6;
+    const int kt = tk % nkt, ot = tk / nkt, g = lane >> 4, c = lane & 15;
+    int in, out;
+    if (fwd) { in = 16 * kt + 4 * g + s; out = 16 * ot + c; }
+    else     { in = 16 * ot + c;         out = 16 * kt + 4 * g + s; }
+    if (in >= n.L[i] || out >= n.L[i + 1]) return -1;
+    return n.woff[i] + in * n.L[i + 1] + out;
+}
+
+__global__ void build_maps_kernel(Net n, Pack pk, int *tmap, int *vmap) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < pk.tlen) {
+        int m = -1;
+        for (int i = 0; i < 3; ++i) {
+            if (e >= pk.fa[i] && e < pk.fa[i] + 256 * pk.T[i] * pk.T[i + 1])
+                m = map_frag(n, i, e - pk.fa[i], pk.T[i], true);
+            if (i > 0 && e >= pk.fb[i] && e < pk.fb[i] + 256 * pk.T[i] * pk.T[i + 1])
+                m = map_frag(n, i, e - pk.fb[i], pk.T[i + 1], false);
+            if (e >= pk.bi[i] && e < pk.bi[i] + 16 * pk.T[i + 1]) {
+                const int j = e - pk.bi[i];
+                m = j < n.L[i + 1] ? n.boff[i] + j : -1;
+            }
+        }
+        tmap[e] = m;
+    }
+    if (e < pk.vlen) {
+        int m = -1;
+        for (int i = 0; i < 3; ++i) {
+            if (e >= pk.vfa[i] && e < pk.vfa[i] + 256 * pk.T[i] * pk.T[i + 1])
+                m = map_frag(n, i, e - pk.vfa[i], pk.T[i], true);
+            if (e >= pk.vb[i] && e < pk.vb[i] + 16 * pk.T[i + 1]) {
+                const int j = e - pk.vb[i];
+                m = j < n.L[i + 1] ? n.boff[i] + j : -1;
+            }
+        }
+        vmap[e] = m;
+    }
+}
+
+__global__ void gather_pack_kernel(float *dst, const double *src, const int *map, int len) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < len) {
+        const int m = map[e];
+        dst[e] = m >= 0 ? (float)src[m] : 0.0f;
+    }
+}
+
+__global__ void set_invvar_kernel(float *iv, const double *stdv, int A, int len) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < len) iv[j] = j < A ? (float)(1.0 / stdv[j] / stdv[j]) : 0.0f;
+}
+
+// observations fp64 [n][L0] -> fp32 [npad][16*T0], zero padded
+__global__ void obs_pad_kernel(float *dst, const double *src, int n, int npad, int L0, int ld) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (long)npad * ld) return;
+    const int s = (int)(e / ld), k = (int)(e % ld);
+    dst[e] = (s < n && k < L0) ? (float)src[(long)s * L0 + k] : 0.0f;
+}
+
+__global__ void to_f32_kernel(float *dst, const double *src, int len) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < len) dst[e] = (float)src[e];
+}
+
+// ---------------------------------------------------------------------------
+// The fused FVP kernel, 3 weight layers (NumLayers == 4), MFMA path.
+// ---------------------------------------------------------------------------
+constexpr int SCR_LD = 20;            // scratch row stride (floats): conflict-free b32 writes
+
+template <int T0, int T1, int T2, int T3>
+struct FastCfg {
+    // theta pack (floats)
+    static constexpr int FA0 = 0;
+    static constexpr int FA1 = FA0 + 256 * T0 * T1;
+    static constexpr int FA2 = FA1 + 256 * T1 * T2;
+    static constexpr int FB1 = FA2 + 256 * T2 * T3;
+    static constexpr int FB2 = FB1 + 256 * T1 * T2;
+    static constexpr int BI0 = FB2 + 256 * T2 * T3;
+    static constexpr int BI1 = BI0 + 16 * T1;
+    static constexpr int BI2 = BI1 + 16 * T2;
+    static constexpr int IV = BI2 + 16 * T3;
+    static constexpr int TLEN = IV + 16 * T3;
+    // v pack (floats), placed right after the theta pack in LDS
+    static constexpr int VFA0 = 0;
+    static constexpr int VFA1 = VFA0 + 256 * T0 * T1;
+    static constexpr int VFA2 = VFA1 + 256 * T1 * T2;
+    static constexpr int VB0 = VFA2 + 256 * T2 * T3;
+    static constexpr int VB1 = VB0 + 16 * T1;
+    static constexpr int VB2 = VB1 + 16 * T2;
+    static constexpr int VLEN = VB2 + 16 * T3;
+    // per-wave transpose scratch: max rows over the three contractions
+    static constexpr int R0 = 16 * (T0 + T1), R1 = 16 * (T1 + T2), R2 = 16 * (T2 + T3);
+    static constexpr int ROWS = R0 > R1 ? (R0 > R2 ? R0 : R2) : (R1 > R2 ? R1 : R2);
+    static constexpr int SCR = ROWS * SCR_LD;
+    // accumulator registers per lane (for the cross-wave tree)
+    static constexpr int NACC = 4 * (T0 * T1 + T1 * T2 + T2 * T3 + T1 + T2 + T3);
+    static constexpr int WAVES = 8;
+    static constexpr int THREADS = 64 * WAVES;
+    static int lds_bytes() {
+        int a = 4 * (TLEN + VLEN + WAVES * SCR);
+        int b = 4 * (WAVES / 2) * NACC * 64;      // tree reduction buffer (reuses the same LDS)
+        return a > b ? a : b;
+    }
+};
+
+__device__ __forceinline__ void scr_put(float *scr, int row0, f4 t, int c, int g) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) scr[(row0 + 4 * g + r) * SCR_LD + c] = t[r];
+}
+__device__ __forceinline__ f4 scr_get(const float *scr, int row0, int c, int g) {
+    return *reinterpret_cast<const f4 *>(scr + (row0 + c) * SCR_LD + 4 * g);
+}
+
+template <int T0, int T1, int T2, int T3>
+__global__ void __launch_bounds__(512)
+fvp_mlp3_kernel(const f4 *__restrict__ obs4, int n, int ntiles, const float *__restrict__ tpack,
+                const double *__restrict__ v, const int *__restrict__ vmap, float *__restrict__ slabs, Net net,
+                const int *__restrict__ skip) {
+    using C = FastCfg<T0, T1, T2, T3>;
+    if (*skip) return;
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float *tw = lds;                                   // theta pack
+    float *vw = lds + C::TLEN;                         // v pack
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int c = lane & 15, g = lane >> 4;
+    float *scr = lds + C::TLEN + C::VLEN + wave * C::SCR;
+
+    // ---- stage the weights (fragment order) and gather+convert the direction ----
+    {
+        const f4 *src = reinterpret_cast<const f4 *>(tpack);
+        f4 *dst = reinterpret_cast<f4 *>(tw);
+        for (int e = tid; e < C::TLEN / 4; e += C::THREADS) dst[e] = src[e];
+        for (int e = tid; e < C::VLEN; e += C::THREADS) {
+            const int m = vmap[e];
+            vw[e] = m >= 0 ? (float)v[m] : 0.0f;
+        }
+    }
+    __syncthreads();
+
+    const int a1 = net.act[1], a2 = net.act[2], a3 = net.act[3];
+    const bool y3_needed = act_needs_y(a3);
+    const f4 *TW = reinterpret_cast<const f4 *>(tw);
+    const f4 *VW = reinterpret_cast<const f4 *>(vw);
+
+    f4 accW0[T0][T1], accW1[T1][T2], accW2[T2][T3];
+    f4 sB1[T1], sB2[T2], sB3[T3];
+    const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int a = 0; a < T0; ++a)
+#pragma unroll
+        for (int b = 0; b < T1; ++b) accW0[a][b] = zero4;
+#pragma unroll
+    for (int a = 0; a < T1; ++a)
+#pragma unroll
+        for (int b = 0; b < T2; ++b) accW1[a][b] = zero4;
+#pragma unroll
+    for (int a = 0; a < T2; ++a)
+#pragma unroll
+        for (int b = 0; b < T3; ++b) accW2[a][b] = zero4;
+#pragma unroll
+    for (int a = 0; a < T1; ++a) sB1[a] = zero4;
+#pragma unroll
+    for (int a = 0; a < T2; ++a) sB2[a] = zero4;
+#pragma unroll
+    for (int a = 0; a < T3; ++a) sB3[a] = zero4;
+
+    const int nwaves = gridDim.x * C::WAVES;
+    for (int tile = blockIdx.x * C::WAVES + wave; tile < ntiles; tile += nwaves) {
+        const int sample = tile * 16 + c;
+        // input tile: lane holds features 16kt+4g..+3 of its sample (D-layout rows)
+        f4 x0[T0];
+#pragma unroll
+        for (int kt = 0; kt < T0; ++kt) x0[kt] = obs4[(long)sample * (4 * T0) + kt * 4 + g];
+
+        // ---- layer 0: x1 = W0^T x0 + b0 ; Rx1 = VW0^T x0 + vb0 (Ry0 = 0) ----
+        f4 y1[T1], r1[T1];
+#pragma unroll
+        for (int ot = 0; ot < T1; ++ot) {
+            f4 a = TW[C::BI0 / 4 + ot * 4 + g];
+            f4 ra = VW[C::VB0 / 4 + ot * 4 + g];
+#pragma unroll
+            for (int kt = 0; kt < T0; ++kt) {
+                const f4 w = TW[C::FA0 / 4 + (ot * T0 + kt) * 64 + lane];
+                const f4 u = VW[C::VFA0 / 4 + (ot * T0 + kt) * 64 + lane];
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    a = MFMA(w[s], x0[kt][s], a);
+                    ra = MFMA(u[s], x0[kt][s], ra);
+                }
+            }
+            y1[ot] = act_fwd(a1, a, ra, r1[ot]);
+        }
+        // ---- layer 1 ----
+        f4 y2[T2], r2[T2];
+#pragma unroll
+        for (int ot = 0; ot < T2; ++ot) {
+            f4 a = TW[C::BI1 / 4 + ot * 4 + g];
+            f4 ra = VW[C::VB1 / 4 + ot * 4 + g];
+#pragma unroll
+            for (int kt = 0; kt < T1; ++kt) {
+                const f4 w = TW[C::FA1 / 4 + (ot * T1 + kt) * 64 + lane];
+                const f4 u = VW[C::VFA1 / 4 + (ot * T1 + kt) * 64 + lane];
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    a = MFMA(w[s], y1[kt][s], a);
+                    ra = MFMA(w[s], r1[kt][s], ra);
+                    ra = MFMA(u[s], y1[kt][s], ra);
+                }
+            }
+            y2[ot] = act_fwd(a2, a, ra, r2[ot]);
+        }
+        // ---- layer 2 (output) and G3 = act3'(Ry3 / sigma^2) ----
+        f4 g3[T3];
+        const bool live = sample < n;
+#pragma unroll
+        for (int ot = 0; ot < T3; ++ot) {
+            f4 a = TW[C::BI2 / 4 + ot * 4 + g];
+            f4 ra = VW[C::VB2 / 4 + ot * 4 + g];
+#pragma unroll
+            for (int kt = 0; kt < T2; ++kt) {
+                const f4 w = TW[C::FA2 / 4 + (ot * T2 + kt) * 64 + lane];
+                const f4 u = VW[C::VFA2 / 4 + (ot * T2 + kt) * 64 + lane];
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    if (y3_needed) a = MFMA(w[s], y2[kt][s], a);
+                    ra = MFMA(w[s], r2[kt][s], ra);
+                    ra = MFMA(u[s], y2[kt][s], ra);
+                }
+            }
+            f4 r3;
+            const f4 y3 = act_fwd(a3, a, ra, r3);
+            const f4 iv = TW[C::IV / 4 + ot * 4 + g];
+            f4 gg = act_bwd(a3, y3, r3 * iv);
+            g3[ot] = live ? gg : zero4;
+            sB3[ot] += g3[ot];
+        }
+        // ---- contraction RGW2 += Y2 . G3^T (K = 16 samples) ----
+#pragma unroll
+        for (int t = 0; t < T2; ++t) scr_put(scr, 16 * t, y2[t], c, g);
+#pragma unroll
+        for (int t = 0; t < T3; ++t) scr_put(scr, 16 * (T2 + t), g3[t], c, g);
+        {
+            f4 gb[T3];
+#pragma unroll
+            for (int t = 0; t < T3; ++t) gb[t] = scr_get(scr, 16 * (T2 + t), c, g);
+#pragma unroll
+            for (int at = 0; at < T2; ++at) {
+                const f4 ya = scr_get(scr, 16 * at, c, g);
+#pragma unroll
+                for (int bt = 0; bt < T3; ++bt)
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) accW2[at][bt] = MFMA(ya[s], gb[bt][s], accW2[at][bt]);
+            }
+        }
+        // ---- G2 = act2'(W2 G3) ----
+        f4 g2[T2];
+#pragma unroll
+        for (int it = 0; it < T2; ++it) {
+            f4 a = zero4;
+#pragma unroll
+            for (int kt = 0; kt < T3; ++kt) {
+                const f4 w = TW[C::FB2 / 4 + (it * T3 + kt) * 64 + lane];
+#pragma unroll
+                for (int s = 0; s < 4; ++s) a = MFMA(w[s], g3[kt][s], a);
+            }
+            g2[it] = act_bwd(a2, y2[it], a);
+            sB2[it] += g2[it];
+        }
+        // ---- contraction RGW1 += Y1 . G2^T ----
+#pragma unroll
+        for (int t = 0; t < T1; ++t) scr_put(scr, 16 * t, y1[t], c, g);
+#pragma unroll
+        for (int t = 0; t < T2; ++t) scr_put(scr, 16 * (T1 + t), g2[t], c, g);
+        {
+            f4 gb[T2];
+#pragma unroll
+            for (int t = 0; t < T2; ++t) gb[t] = scr_get(scr, 16 * (T1 + t), c, g);
+#pragma unroll
+            for (int at = 0; at < T1; ++at) {
+                const f4 ya = scr_get(scr, 16 * at, c, g);
+#pragma unroll
+                for (int bt = 0; bt < T2; ++bt)
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) accW1[at][bt] = MFMA(ya[s], gb[bt][s], accW1[at][bt]);
+            }
+        }
+        // ---- G1 = act1'(W1 G2) ----
+        f4 g1[T1];
+#pragma unroll
+        for (int it = 0; it < T1; ++it) {
+            f4 a = zero4;
+#pragma unroll
+            for (int kt = 0; kt < T2; ++kt) {
+                const f4 w = TW[C::FB1 / 4 + (it * T2 + kt) * 64 + lane];
+#pragma unroll
+                for (int s = 0; s < 4; ++s) a = MFMA(w[s], g2[kt][s], a);
+            }
+            g1[it] = act_bwd(a1, y1[it], a);
+            sB1[it] += g1[it];
+        }
+        // ---- contraction RGW0 += X0 . G1^T ----
+#pragma unroll
+        for (int t = 0; t < T0; ++t) scr_put(scr, 16 * t, x0[t], c, g);
+#pragma unroll
+        for (int t = 0; t < T1; ++t) scr_put(scr, 16 * (T0 + t), g1[t], c, g);
+        {
+            f4 gb[T1];
+#pragma unroll
+            for (int t = 0; t < T1; ++t) gb[t] = scr_get(scr, 16 * (T0 + t), c, g);
+#pragma unroll
+            for (int at = 0; at < T0; ++at) {
+                const f4 ya = scr_get(scr, 16 * at, c, g);
+#pragma unroll
+                for (int bt = 0; bt < T1; ++bt)
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) accW0[at][bt] = MFMA(ya[s], gb[bt][s], accW0[at][bt]);
+            }
+        }
+    }
+
+    // ---- deterministic cross-wave tree: (w, w+h) pairs, h = 4, 2, 1 ----
+    f4 acc[C::NACC / 4];
+    {
+        int k = 0;
+#pragma unroll
+        for (int a = 0; a < T0; ++a)
+#pragma unroll
+            for (int b = 0; b < T1; ++b) acc[k++] = accW0[a][b];
+#pragma unroll
+        for (int a = 0; a < T1; ++a)
+#pragma unroll
+            for (int b = 0; b < T2; ++b) acc[k++] = accW1[a][b];
+#pragma unroll
+        for (int a = 0; a < T2; ++a)
+#pragma unroll
+            for (int b = 0; b < T3; ++b) acc[k++] = accW2[a][b];
+#pragma unroll
+        for (int a = 0; a < T1; ++a) acc[k++] = sB1[a];
+#pragma unroll
+        for (int a = 0; a < T2; ++a) acc[k++] = sB2[a];
+#pragma unroll
+        for (int a = 0; a < T3; ++a) acc[k++] = sB3[a];
+    }
+    f4 *red = reinterpret_cast<f4 *>(lds);
+#pragma unroll
+    for (int h = C::WAVES / 2; h >= 1; h >>= 1) {
+        __syncthreads();
+        if (wave >= h && wave < 2 * h) {
+#pragma unroll
+            for (int k = 0; k < C::NACC / 4; ++k) red[((wave - h) * (C::NACC / 4) + k) * 64 + lane] = acc[k];
+        }
+        __syncthreads();
+        if (wave < h) {
+#pragma unroll
+            for (int k = 0; k < C::NACC / 4; ++k) acc[k] += red[(wave * (C::NACC / 4) + k) * 64 + lane];
+        }
+    }
+    if (wave != 0) return;
+
+    // ---- wave 0 writes the block's partial sums in natural parameter order ----
+    float *slab = slabs + (long)blockIdx.x * net.P;
+    int k = 0;
+    const int Ls[4] = {net.L[0], net.L[1], net.L[2], net.L[3]};
+    const int Ts[4] = {T0, T1, T2, T3};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int TI = Ts[i], TO = Ts[i + 1];
+        for (int at = 0; at < TI; ++at)
+            for (int bt = 0; bt < TO; ++bt, ++k) {
+                const int b = 16 * bt + c;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int a = 16 * at + 4 * g + r;
+                    if (a < Ls[i] && b < Ls[i + 1]) slab[net.woff[i] + a * Ls[i + 1] + b] = acc[k][r];
+                }
+            }
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int TO = Ts[i + 1];
+        for (int t = 0; t < TO; ++t, ++k) {
+            f4 s = acc[k];
+            // sum over the 16 sample columns (lanes with equal g), fixed butterfly
+#pragma unroll
+            for (int off = 1; off < 16; off <<= 1)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) s[r] += __shfl_xor(s[r], off, 64);
+            if (c == 0) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int b = 16 * t + 4 * g + r;
+                    if (b < Ls[i + 1]) slab[net.boff[i] + b] = s[r];
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Generic FVP kernel: any depth, any widths (one thread per sample, fp32).
+// Per-sample activations live in a block-private global scratch laid out
+// [row][256] so that every access is coalesced across the block.
+// ---------------------------------------------------------------------------
+constexpr int GEN_T = 256;
+
+__global__ void __launch_bounds__(GEN_T)
+fvp_generic_kernel(const float *__restrict__ obs, int n, const float *__restrict__ th, const float *__restrict__ v,
+                   const float *__restrict__ iv, float *__restrict__ scratch, int srows, float *__restrict__ slabs,
+                   Net net, const int *__restrict__ skip) {
+    if (*skip) return;
+    const int tid = threadIdx.x;
+    float *Y = scratch + (long)blockIdx.x * 3 * srows * GEN_T;
+    float *RY = Y + (long)srows * GEN_T;
+    float *RG = RY + (long)srows * GEN_T;
+    int roff[MAXL + 1];
+    roff[0] = 0;
+    for (int i = 0; i < net.nl; ++i) roff[i + 1] = roff[i] + net.L[i];
+    float *slab = slabs + (long)blockIdx.x * net.P;
+    const int nw = net.P - net.A;
+    for (int q = tid; q < nw; q += GEN_T) slab[q] = 0.0f;
+
+    const int npass = (n + GEN_T - 1) / GEN_T;
+    for (int pass = blockIdx.x; pass < npass; pass += gridDim.x) {
+        const int s = pass * GEN_T + tid;
+        const bool live = s < n;
+        for (int k = 0; k < net.L[0]; ++k) {
+            Y[k * GEN_T + tid] = live ? obs[(long)s * net.L[0] + k] : 0.0f;
+            RY[k * GEN_T + tid] = 0.0f;
+        }
+        for (int i = 0; i + 1 < net.nl; ++i) {
+            const int in = net.L[i], out = net.L[i + 1];
+            const float *W = th + net.woff[i], *B = th + net.boff[i];
+            const float *VWp = v + net.woff[i], *VB = v + net.boff[i];
+            for (int j = 0; j < out; ++j) {
+                float x = B[j], rx = VB[j];
+                for (int k = 0; k < in; ++k) {
+                    const float yk = Y[(roff[i] + k) * GEN_T + tid], ryk = RY[(roff[i] + k) * GEN_T + tid];
+                    x += yk * W[k * out + j];
+                    rx += ryk * W[k * out + j];
+                    rx += yk * VWp[k * out + j];
+                }
+                const float y = act_y(net.act[i + 1], x);
+                Y[(roff[i + 1] + j) * GEN_T + tid] = y;
+                RY[(roff[i + 1] + j) * GEN_T + tid] = act_r(net.act[i + 1], y, rx);
+            }
+        }
+        const int last = net.nl - 1;
+        for (int j = 0; j < net.A; ++j) {
+            const float y = Y[(roff[last] + j) * GEN_T + tid];
+            const float gg = act_r(net.act[last], y, RY[(roff[last] + j) * GEN_T + tid] * iv[j]);
+            RG[(roff[last] + j) * GEN_T + tid] = live ? gg : 0.0f;
+        }
+        for (int i = last; i >= 2; --i) {
+            const int cur = net.L[i], prev = net.L[i - 1];
+            const float *W = th + net.woff[i - 1];
+            for (int j = 0; j < prev; ++j) {
+                float t = 0.0f;
+                for (int k = 0; k < cur; ++k) t += W[j * cur + k] * RG[(roff[i] + k) * GEN_T + tid];
+                RG[(roff[i - 1] + j) * GEN_T + tid] = act_r(net.act[i - 1], Y[(roff[i - 1] + j) * GEN_T + tid], t);
+            }
+        }
+        __syncthreads();
+        // contraction over the 256 samples of this pass, one parameter per thread
+        for (int q = tid; q < nw; q += GEN_T) {
+            int i = 0;
+            while (i + 2 < net.nl && q >= net.woff[i + 1]) ++i;
+            const int in = net.L[i], out = net.L[i + 1];
+            const int local = q - net.woff[i];
+            float acc = 0.0f;
+            if (local < in * out) {
+                const int a = local / out, b = local % out;
+                const float *ya = Y + (long)(roff[i] + a) * GEN_T, *gb = RG + (long)(roff[i + 1] + b) * GEN_T;
+                for (int t = 0; t < GEN_T; ++t) acc += ya[t] * gb[t];
+            } else {
+                const float *gb = RG + (long)(roff[i + 1] + local - in * out) * GEN_T;
+                for (int t = 0; t < GEN_T; ++t) acc += gb[t];
+            }
+            slab[q] += acc;
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Cross-block reduction (fp64, fixed order) -> zacc[P-A]
+// block = 64 parameters x 16 slab groups
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(1024)
+reduce_slabs_kernel(const float *__restrict__ slabs, int G, int P, int nw, double *__restrict__ zacc,
+                    const int *__restrict__ skip) {
+    if (*skip) return;
+    __shared__ double part[16][64];
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const int q = blockIdx.x * 64 + tx;
+    double s = 0.0;
+    if (q < nw) {
+        int b = ty;
+        for (; b + 48 < G; b += 64) {     // 4 independent loads in flight
+            const float v0 = slabs[(long)b * P + q], v1 = slabs[(long)(b + 16) * P + q];
+            const float v2 = slabs[(long)(b + 32) * P + q], v3 = slabs[(long)(b + 48) * P + q];
+            s += (double)v0;
+            s += (double)v1;
+            s += (double)v2;
+            s += (double)v3;
+        }
+        for (; b < G; b += 16) s += (double)slabs[(long)b * P + q];
+    }
+    part[ty][tx] = s;
+    __syncthreads();
+    if (ty == 0 && q < nw) {
+        double t = 0.0;
+        for (int k = 0; k < 16; ++k) t += part[k][tx];
+        zacc[q] = t;
+    }
+}
+
+// z = zacc / N + damping * v ; log-std block = 2 v + damping v   (src/TRPO_FVP.c:919-931)
+__global__ void fvp_epilogue_kernel(const double *__restrict__ zacc, const double *__restrict__ v,
+                                    double *__restrict__ z, int P, int nw, const Ctl *__restrict__ ctl) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= P) return;
+    const double vq = v[q];
+    z[q] = (q < nw ? zacc[q] / ctl->n_total : 2.0 * vq) + ctl->damping * vq;
+}
+
+// ---------------------------------------------------------------------------
+// CG (src/TRPO_CG.c:11-113), one 1024-thread block, all fp64, fixed-order sums
+// ---------------------------------------------------------------------------
+__device__ double block_sum(double v, double *sh) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    __syncthreads();
+    if (lane == 0) sh[w] = v;
+    __syncthreads();
+    double t = 0.0;
+    for (int k = 0; k < nwv; ++k) t += sh[k];
+    return t;
+}
+
+__global__ void __launch_bounds__(1024)
+cg_init_kernel(const double *__restrict__ b, double *x, double *r, double *p, int P, Ctl *ctl, double *hist,
+               int maxiter, double resth) {
+    __shared__ double sh[16];
+    double s = 0.0;
+    for (int q = threadIdx.x; q < P; q += blockDim.x) {
+        const double bq = b[q];
+        x[q] = 0.0;
+        r[q] = bq;
+        p[q] = bq;
+        s += bq * bq;
+    }
+    const double rr = block_sum(s, sh);
+    if (threadIdx.x == 0) {
+        ctl->maxiter = maxiter;
+        ctl->resth = resth;
+        ctl->rdotr = rr;
+        ctl->iter = 0;
+        hist[0] = rr;
+        hist[1] = 0.0;
+        ctl->done = (rr < resth || maxiter == 0) ? 1 : 0;
+    }
+}
+
+__global__ void __launch_bounds__(1024)
+cg_update_kernel(const double *__restrict__ zacc, double *x, double *r, double *p, int P, int nw, Ctl *ctl,
+                 double *hist) {
+    __shared__ double sh[16];
+    if (ctl->done) return;
+    const double n = ctl->n_total, lam = ctl->damping;
+    constexpr int MAXE = 32;     // per-thread elements kept in registers (P <= 32768)
+    double zr[MAXE];
+    double pz = 0.0;
+#pragma unroll
+    for (int e = 0; e < MAXE; ++e) {
+        const int q = threadIdx.x + e * 1024;
+        if (q < P) {
+            const double pq = p[q];
+            const double zq = (q < nw ? zacc[q] / n : 2.0 * pq) + lam * pq;
+            zr[e] = zq;
+            pz += pq * zq;
+        }
+    }
+    const double rdotr = ctl->rdotr;
+    const double alpha = rdotr / block_sum(pz, sh);
+    double rr = 0.0, xx = 0.0;
+#pragma unroll
+    for (int e = 0; e < MAXE; ++e) {
+        const int q = threadIdx.x + e * 1024;
+        if (q < P) {
+            const double xq = x[q] + alpha * p[q];
+            const double rq = r[q] - alpha * zr[e];
+            x[q] = xq;
+            r[q] = rq;
+            rr += rq * rq;
+            xx += xq * xq;
+        }
+    }
+    const double nr = block_sum(rr, sh);
+    const double xn = block_sum(xx, sh);
+    const double beta = nr / rdotr;
+    for (int q = threadIdx.x; q < P; q += 1024) p[q] = r[q] + beta * p[q];
+    if (threadIdx.x == 0) {
+        const int it = ctl->iter + 1;
+        ctl->iter = it;
+        ctl->rdotr = nr;
+        hist[2 * it] = nr;
+        hist[2 * it + 1] = sqrt(xn);
+        ctl->done = (nr < ctl->resth || it >= ctl->maxiter) ? 1 : 0;
+    }
+}
+
+// ===========================================================================
+// device layer (trpo_dev.h)
+// ===========================================================================
+typedef void (*fast_launch_fn)(dim3, dim3, int, hipStream_t, const f4 *, int, int, const float *, const double *,
+                               const int *, float *, Net, const int *);
+
+template <int T0, int T1, int T2, int T3>
+static void fast_launch(dim3 g, dim3 b, int lds, hipStream_t st, const f4 *obs4, int n, int ntiles,
+                        const float *tp, const double *v, const int *vmap, float *slabs, Net net, const int *skip) {
+    hipLaunchKernelGGL((fvp_mlp3_kernel<T0, T1, T2, T3>), g, b, lds, st, obs4, n, ntiles, tp, v, vmap, slabs, net,
+                       skip);
+}
+template <int T0, int T1, int T2, int T3>
+static hipError_t fast_attr(int lds) {
+    return hipFuncSetAttribute((const void *)fvp_mlp3_kernel<T0, T1, T2, T3>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+}
+
+struct FastEntry {
+    int T[4];
+    fast_launch_fn launch;
+    hipError_t (*attr)(int);
+    int lds, tlen, vlen;
+};
+
+#define FAST_ENTRY(a, b, c, d)                                                                         \
+    {{a, b, c, d}, fast_launch<a, b, c, d>, fast_attr<a, b, c, d>, FastCfg<a, b, c, d>::lds_bytes(),  \
+     FastCfg<a, b, c, d>::TLEN, FastCfg<a, b, c, d>::VLEN}
+
+static const FastEntry kFast[] = {
+    FAST_ENTRY(1, 1, 1, 1), FAST_ENTRY(1, 2, 2, 1), FAST_ENTRY(1, 4, 4, 1),
+    FAST_ENTRY(2, 1, 1, 1), FAST_ENTRY(2, 2, 2, 1), FAST_ENTRY(2, 4, 4, 1),
+};
+
+struct trpo_dev {
+    int device;
+    hipStream_t stream;
+    Net net;
+    int P, nw;
+    // fast path
+    const FastEntry *fast;
+    Pack pack;
+    float *tpack;
+    int *tmap, *vmap;
+    f4 *obs4;
+    // generic path
+    float *th32, *v32, *iv32, *obs32, *scratch;
+    int srows;
+    size_t scratch_blocks;
+    // common
+    double *theta64;            // natural theta (device, fp64)
+    double *std64;
+    double *vec[5];             // V, Z, X, B, P
+    double *r, *zacc;
+    float *slabs;
+    int slab_blocks;            // capacity
+    int grid;                   // FVP blocks for the current n
+    Ctl *ctl;
+    double *hist;               // 2 * (maxiter_cap + 1)
+    int hist_cap;
+    size_t n;                   // local samples
+    size_t npad_cap;
+    double n_total;
+    double damping;
+    // CG graph cache
+    hipGraphExec_t cg_exec;
+    size_t cg_graph_iters;
+    double cg_graph_resth;
+    hipEvent_t ev0, ev1;
+    // RCCL
+    ncclComm_t comm;
+    int rank, world;
+    char name[64];
+};
+
+static int act_code(char a) {
+    switch (a) {
+    case 'l': return ACT_L;
+    case 't': return ACT_T;
+    case 'o': return ACT_O;
+    case 's': return ACT_S;
+    default: return -1;
+    }
+}
+
+#define HCHK(x)                                                                            \
+    do {                                                                                   \
+        hipError_t e_ = (x);                                                               \
+        if (e_ != hipSuccess) {                                                            \
+            fprintf(stderr, "[trpo_mi355x] HIP error %s at %s:%d\n", hipGetErrorString(e_), \
+                    __FILE__, __LINE__);                                                   \
+            return -2;                                                                     \
+        }                                                                                  \
+    } while (0)
+
+static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+extern "C" size_t trpo_dev_num_params(const trpo_dev *d) { return d ? (size_t)d->P : 0; }
+
+extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, const char *ac, char *err,
+                                     size_t errlen) {
+#define FAIL(...)                                      \
+    do {                                               \
+        if (err) snprintf(err, errlen, __VA_ARGS__);   \
+        trpo_dev_destroy(d);                           \
+        return NULL;                                   \
+    } while (0)
+    trpo_dev *d = NULL;
+    if (nl < 2 || nl > MAXL || !ls || !ac) {
+        if (err) snprintf(err, errlen, "invalid network description (NumLayers=%zu)", nl);
+        return NULL;
+    }
+    d = (trpo_dev *)calloc(1, sizeof(trpo_dev));
+    if (!d) return NULL;
+    d->comm = NULL;
+    d->world = 1;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) FAIL("no HIP device available");
+    if (device < 0) {
+        const char *e = getenv("TRPO_DEVICE");
+        device = e ? atoi(e) : 0;
+    }
+    if (device >= ndev) FAIL("device %d out of range (%d devices)", device, ndev);
+    d->device = device;
+    if (hipSetDevice(device) != hipSuccess) FAIL("hipSetDevice(%d) failed", device);
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        FAIL("device %d is %s; this library is built for gfx950 (MI355X) only", device, prop.gcnArchName);
+    Net &n = d->net;
+    memset(&n, 0, sizeof n);
+    n.nl = (int)nl;
+    int pos = 0;
+    for (size_t i = 0; i < nl; ++i) {
+        if (ls[i] == 0 || ls[i] > 65536) FAIL("LayerSize[%zu]=%zu unsupported", i, ls[i]);
+        n.L[i] = (int)ls[i];
+        if (i > 0) {
+            n.act[i] = act_code(ac[i]);
+            if (n.act[i] < 0) FAIL("AC Function for Layer[%zu] is %c. Unsupported.", i, ac[i]);
+        }
+    }
+    for (size_t i = 0; i + 1 < nl; ++i) {
+        n.woff[i] = pos;
+        pos += n.L[i] * n.L[i + 1];
+        n.boff[i] = pos;
+        pos += n.L[i + 1];
+    }
+    n.A = n.L[nl - 1];
+    n.P = pos + n.A;
+    d->P = n.P;
+    d->nw = n.P - n.A;
+    if (d->P > 32 * 1024) FAIL("NumParams=%d exceeds the 32768 supported by the device CG", d->P);
+
+    // pick the kernel family
+    d->fast = NULL;
+    if (nl == 4) {
+        int T[4];
+        for (int i = 0; i < 4; ++i) T[i] = cdiv(n.L[i], 16);
+        const FastEntry *best = NULL;
+        for (const FastEntry &f : kFast) {
+            bool ok = true;
+            for (int i = 0; i < 4; ++i) ok = ok && f.T[i] >= T[i];
+            if (!ok) continue;
+            int cost = f.T[0] * f.T[1] + f.T[1] * f.T[2] + f.T[2] * f.T[3];
+            int bcost = best ? best->T[0] * best->T[1] + best->T[1] * best->T[2] + best->T[2] * best->T[3] : 1 << 30;
+            if (cost < bcost) best = &f;
+        }
+        d->fast = best;
+    }
+    const char *force = getenv("TRPO_FORCE_GENERIC");
+    if (force && atoi(force)) d->fast = NULL;
+
+    if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) FAIL("stream create failed");
+    if (hipEventCreate(&d->ev0) != hipSuccess || hipEventCreate(&d->ev1) != hipSuccess) FAIL("event create");
+    d->hist_cap = 0;
+#define DMALLOC(p, bytes)                                                   \
+    do {                                                                    \
+        if (hipMalloc((void **)&(p), (bytes)) != hipSuccess) FAIL("hipMalloc(%zu) failed", (size_t)(bytes)); \
+        hipMemsetAsync((p), 0, (bytes), d->stream);                         \
+    } while (0)
+    DMALLOC(d->theta64, sizeof(double) * d->P);
+    DMALLOC(d->std64, sizeof(double) * n.A);
+    for (int i = 0; i < 5; ++i) DMALLOC(d->vec[i], sizeof(double) * d->P);
+    DMALLOC(d->r, sizeof(double) * d->P);
+    DMALLOC(d->zacc, sizeof(double) * d->P);
+    DMALLOC(d->ctl, sizeof(Ctl));
+    if (d->fast) {
+        Pack &pk = d->pack;
+        for (int i = 0; i < 4; ++i) pk.T[i] = d->fast->T[i];
+        const int *T = pk.T;
+        pk.fa[0] = 0;
+        pk.fa[1] = pk.fa[0] + 256 * T[0] * T[1];
+        pk.fa[2] = pk.fa[1] + 256 * T[1] * T[2];
+        pk.fb[0] = -1;
+        pk.fb[1] = pk.fa[2] + 256 * T[2] * T[3];
+        pk.fb[2] = pk.fb[1] + 256 * T[1] * T[2];
+        pk.bi[0] = pk.fb[2] + 256 * T[2] * T[3];
+        pk.bi[1] = pk.bi[0] + 16 * T[1];
+        pk.bi[2] = pk.bi[1] + 16 * T[2];
+        pk.iv = pk.bi[2] + 16 * T[3];
+        pk.tlen = pk.iv + 16 * T[3];
+        pk.vfa[0] = 0;
+        pk.vfa[1] = pk.vfa[0] + 256 * T[0] * T[1];
+        pk.vfa[2] = pk.vfa[1] + 256 * T[1] * T[2];
+        pk.vb[0] = pk.vfa[2] + 256 * T[2] * T[3];
+        pk.vb[1] = pk.vb[0] + 16 * T[1];
+        pk.vb[2] = pk.vb[1] + 16 * T[2];
+        pk.vlen = pk.vb[2] + 16 * T[3];
+        if (pk.tlen != d->fast->tlen || pk.vlen != d->fast->vlen) FAIL("internal: pack layout mismatch");
+        DMALLOC(d->tpack, sizeof(float) * pk.tlen);
+        DMALLOC(d->tmap, sizeof(int) * pk.tlen);
+        DMALLOC(d->vmap, sizeof(int) * pk.vlen);
+        const int len = pk.tlen > pk.vlen ? pk.tlen : pk.vlen;
+        hipLaunchKernelGGL(build_maps_kernel, dim3(cdiv(len, 256)), dim3(256), 0, d->stream, n, pk, d->tmap, d->vmap);
+        if (d->fast->attr(d->fast->lds) != hipSuccess) FAIL("hipFuncSetAttribute(LDS=%d) failed", d->fast->lds);
+        snprintf(d->name, sizeof d->name, "mfma-mlp3 %dx%dx%dx%d", T[0], T[1], T[2], T[3]);
+    } else {
+        DMALLOC(d->th32, sizeof(float) * d->P);
+        DMALLOC(d->v32, sizeof(float) * d->P);
+        DMALLOC(d->iv32, sizeof(float) * n.A);
+        int rows = 0;
+        for (int i = 0; i < n.nl; ++i) rows += n.L[i];
+        d->srows = rows;
+        snprintf(d->name, sizeof d->name, "generic");
+    }
+    if (hipStreamSynchronize(d->stream) != hipSuccess) FAIL("initialisation kernels failed");
+    d->damping = 0.1;
+    d->n_total = 0;
+    Ctl c0;
+    memset(&c0, 0, sizeof c0);
+    c0.damping = d->damping;
+    if (hipMemcpyAsync(d->ctl, &c0, sizeof c0, hipMemcpyHostToDevice, d->stream) != hipSuccess ||
+        hipStreamSynchronize(d->stream) != hipSuccess)
+        FAIL("control block upload failed");
+    return d;
+#undef FAIL
+#undef DMALLOC
+}
+
+extern "C" void trpo_dev_destroy(trpo_dev *d) {
+    if (!d) return;
+    if (d->stream) hipStreamSynchronize(d->stream);
+    if (d->cg_exec) hipGraphExecDestroy(d->cg_exec);
+    if (d->comm) ncclCommDestroy(d->comm);
+    void *ptrs[] = {d->tpack, d->tmap, d->vmap, d->obs4, d->th32, d->v32, d->iv32, d->obs32, d->scratch,
+                    d->theta64, d->std64, d->r, d->zacc, d->slabs, d->ctl, d->hist};
+    for (void *p : ptrs)
+        if (p) hipFree(p);
+    for (int i = 0; i < 5; ++i)
+        if (d->vec[i]) hipFree(d->vec[i]);
+    if (d->ev0) hipEventDestroy(d->ev0);
+    if (d->ev1) hipEventDestroy(d->ev1);
+    if (d->stream) hipStreamDestroy(d->stream);
+    free(d);
+}
+
+static int sync_ctl_scalars(trpo_dev *d) {
+    // damping and N live in the control block so captured graphs stay valid
+    HCHK(hipMemcpyAsync(&d->ctl->damping, &d->damping, sizeof(double), hipMemcpyHostToDevice, d->stream));
+    HCHK(hipMemcpyAsync(&d->ctl->n_total, &d->n_total, sizeof(double), hipMemcpyHostToDevice, d->stream));
+    HCHK(hipStreamSynchronize(d->stream));
+    return 0;
+}
+
+extern "C" int trpo_dev_set_damping(trpo_dev *d, double damping) {
+    if (!d) return -1;
+    HCHK(hipSetDevice(d->device));
+    d->damping = damping;
+    return sync_ctl_scalars(d);
+}
+
+extern "C" int trpo_dev_set_theta(trpo_dev *d, const double *theta) {
+    if (!d || !theta) return -1;
+    HCHK(hipSetDevice(d->device));
+    HCHK(hipMemcpyAsync(d->theta64, theta, sizeof(double) * d->P, hipMemcpyHostToDevice, d->stream));
+    if (d->fast) {
+        hipLaunchKernelGGL(gather_pack_kernel, dim3(cdiv(d->pack.iv, 256)), dim3(256), 0, d->stream, d->tpack,
+                           d->theta64, d->tmap, d->pack.iv);
+    } else {
+        hipLaunchKernelGGL(to_f32_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, d->th32, d->theta64, d->P);
+    }
+    HCHK(hipGetLastError());
+    HCHK(hipStreamSynchronize(d->stream));
+    return 0;
+}
+
+extern "C" int trpo_dev_set_std(trpo_dev *d, const double *stdv) {
+    if (!d || !stdv) return -1;
+    HCHK(hipSetDevice(d->device));
+    for (int j = 0; j < d->net.A; ++j)
+        if (!(stdv[j] > 0.0) && !(stdv[j] < 0.0)) return -1;     // sigma must be non-zero
+    HCHK(hipMemcpyAsync(d->std64, stdv, sizeof(double) * d->net.A, hipMemcpyHostToDevice, d->stream));
+    if (d->fast) {
+        const int len = 16 * d->pack.T[3];
+        hipLaunchKernelGGL(set_invvar_kernel, dim3(1), dim3(cdiv(len, 64) * 64), 0, d->stream,
+                           d->tpack + d->pack.iv, d->std64, d->net.A, len);
+    } else {
+        hipLaunchKernelGGL(set_invvar_kernel, dim3(cdiv(d->net.A, 256)), dim3(256), 0, d->stream, d->iv32, d->std64,
+                           d->net.A, d->net.A);
+    }
+    HCHK(hipGetLastError());
+    HCHK(hipStreamSynchronize(d->stream));
+    return 0;
+}
+
+static int choose_grid(trpo_dev *d) {
+    // one 8-wave block per CU at most; at least one tile per wave
+    int cus = 256;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, d->device) == hipSuccess && prop.multiProcessorCount > 0)
+        cus = prop.multiProcessorCount;
+    const char *e = getenv("TRPO_FVP_BLOCKS");
+    if (d->fast) {
+        const int ntiles = cdiv((long)d->n, 16);
+        int g = cdiv(ntiles, 8);
+        if (g > cus) g = cus;
+        if (e && atoi(e) > 0) g = atoi(e);
+        return g < 1 ? 1 : g;
+    }
+    const int npass = cdiv((long)d->n, GEN_T);
+    int g = npass < cus ? npass : cus;
+    if (e && atoi(e) > 0) g = atoi(e);
+    return g < 1 ? 1 : g;
+}
+
+static int refresh_n_total(trpo_dev *d);
+
+extern "C" int trpo_dev_set_obs(trpo_dev *d, const double *obs, size_t n) {
+    if (!d || (!obs && n) || n > (size_t)1 << 30) return -1;
+    HCHK(hipSetDevice(d->device));
+    const int L0 = d->net.L[0];
+    double *tmp = NULL;
+    if (n) {
+        HCHK(hipMalloc((void **)&tmp, sizeof(double) * n * L0));
+        HCHK(hipMemcpyAsync(tmp, obs, sizeof(double) * n * L0, hipMemcpyHostToDevice, d->stream));
+    }
+    d->n = n;
+    d->grid = choose_grid(d);
+    if (d->fast) {
+        const size_t npad = (size_t)cdiv((long)n, 16) * 16 + 16;
+        const int ld = 16 * d->pack.T[0];
+        if (npad > d->npad_cap) {
+            if (d->obs4) hipFree(d->obs4);
+            HCHK(hipMalloc((void **)&d->obs4, sizeof(float) * npad * ld));
+            d->npad_cap = npad;
+        }
+        if (n)
+            hipLaunchKernelGGL(obs_pad_kernel, dim3(cdiv((long)npad * ld, 256)), dim3(256), 0, d->stream,
+                               (float *)d->obs4, tmp, (int)n, (int)npad, L0, ld);
+    } else {
+        if ((size_t)n * L0 > d->npad_cap) {
+            if (d->obs32) hipFree(d->obs32);
+            HCHK(hipMalloc((void **)&d->obs32, sizeof(float) * (n * L0 + 1)));
+            d->npad_cap = n * L0;
+        }
+        if (n) hipLaunchKernelGGL(to_f32_kernel, dim3(cdiv((long)n * L0, 256)), dim3(256), 0, d->stream, d->obs32,
+                                  tmp, (int)(n * L0));
+        if ((size_t)d->grid > d->scratch_blocks) {
+            if (d->scratch) hipFree(d->scratch);
+            HCHK(hipMalloc((void **)&d->scratch, sizeof(float) * 3 * (size_t)d->srows * GEN_T * d->grid));
+            d->scratch_blocks = d->grid;
+        }
+    }
+    if (d->grid > d->slab_blocks) {
+        if (d->slabs) hipFree(d->slabs);
+        HCHK(hipMalloc((void **)&d->slabs, sizeof(float) * (size_t)d->P * d->grid));
+        HCHK(hipMemsetAsync(d->slabs, 0, sizeof(float) * (size_t)d->P * d->grid, d->stream));
+        d->slab_blocks = d->grid;
+    }
+    HCHK(hipGetLastError());
+    HCHK(hipStreamSynchronize(d->stream));
+    if (tmp) hipFree(tmp);
+    if (d->cg_exec) {     // geometry may have changed: recapture next time
+        hipGraphExecDestroy(d->cg_exec);
+        d->cg_exec = NULL;
+    }
+    return refresh_n_total(d);
+}
+
+// N is the global sample count: local n, or the all-reduced n under RCCL
+static int refresh_n_total(trpo_dev *d) {
+    const size_t n = d->n;
+    if (d->comm) {
+        double nl = (double)n, *dn = NULL;
+        HCHK(hipMalloc((void **)&dn, sizeof(double)));
+        HCHK(hipMemcpyAsync(dn, &nl, sizeof(double), hipMemcpyHostToDevice, d->stream));
+        if (ncclAllReduce(dn, dn, 1, ncclFloat64, ncclSum, d->comm, d->stream) != ncclSuccess) return -4;
+        HCHK(hipStreamSynchronize(d->stream));
+        HCHK(hipMemcpyAsync(&d->n_total, dn, sizeof(double), hipMemcpyDeviceToHost, d->stream));
+        HCHK(hipStreamSynchronize(d->stream));
+        hipFree(dn);
+    } else {
+        d->n_total = (double)n;
+    }
+    return sync_ctl_scalars(d);
+}
+
+extern "C" int trpo_dev_comm_unique_id(void *id128) {
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return -4;
+    memcpy(id128, &id, sizeof(id) < 128 ? sizeof(id) : 128);
+    return 0;
+}
+
+extern "C" int trpo_dev_set_comm(trpo_dev *d, int rank, int world, const void *id128) {
+    if (!d || world < 1 || rank < 0 || rank >= world) return -1;
+    HCHK(hipSetDevice(d->device));
+    if (d->comm) {
+        ncclCommDestroy(d->comm);
+        d->comm = NULL;
+    }
+    if (world > 1) {
+        ncclUniqueId id;
+        memcpy(&id, id128, sizeof(id));
+        if (ncclCommInitRank(&d->comm, world, id, rank) != ncclSuccess) return -4;
+    }
+    d->rank = rank;
+    d->world = world;
+    if (d->cg_exec) {
+        hipGraphExecDestroy(d->cg_exec);
+        d->cg_exec = NULL;
+    }
+    return refresh_n_total(d);
+}
+
+extern "C" int trpo_dev_upload(trpo_dev *d, int slot, const double *host) {
+    if (!d || slot < 0 || slot > 4 || !host) return -1;
+    HCHK(hipSetDevice(d->device));
+    HCHK(hipMemcpyAsync(d->vec[slot], host, sizeof(double) * d->P, hipMemcpyHostToDevice, d->stream));
+    HCHK(hipStreamSynchronize(d->stream));
+    return 0;
+}
+
+extern "C" int trpo_dev_download(trpo_dev *d, int slot, double *host) {
+    if (!d || slot < 0 || slot > 4 || !host) return -1;
+    HCHK(hipSetDevice(d->device));
+    HCHK(hipMemcpyAsync(host, d->vec[slot], sizeof(double) * d->P, hipMemcpyDeviceToHost, d->stream));
+    HCHK(hipStreamSynchronize(d->stream));
+    return 0;
+}
+
+// enqueue: partial sums of F*src into d->zacc (global over ranks)
+static int enqueue_fvp_core(trpo_dev *d, const double *src, const int *skip) {
+    const Net &n = d->net;
+    if (d->n == 0) {
+        HCHK(hipMemsetAsync(d->zacc, 0, sizeof(double) * d->P, d->stream));
+    } else if (d->fast) {
+        const int ntiles = cdiv((long)d->n, 16);
+        d->fast->launch(dim3(d->grid), dim3(512), d->fast->lds, d->stream, d->obs4, (int)d->n, ntiles, d->tpack, src,
+                        d->vmap, d->slabs, n, skip);
+        HCHK(hipGetLastError());
+    } else {
+        hipLaunchKernelGGL(to_f32_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, d->v32, src, d->P);
+        hipLaunchKernelGGL(fvp_generic_kernel, dim3(d->grid), dim3(GEN_T), 0, d->stream, d->obs32, (int)d->n,
+                           d->th32, d->v32, d->iv32, d->scratch, d->srows, d->slabs, n, skip);
+        HCHK(hipGetLastError());
+    }
+    if (d->n) {
+        hipLaunchKernelGGL(reduce_slabs_kernel, dim3(cdiv(d->nw, 64)), dim3(1024), 0, d->stream, d->slabs, d->grid,
+                           d->P, d->nw, d->zacc, skip);
+        HCHK(hipGetLastError());
+    }
+    if (d->comm) {
+        if (ncclAllReduce(d->zacc, d->zacc, d->nw, ncclFloat64, ncclSum, d->comm, d->stream) != ncclSuccess) return -4;
+    }
+    return 0;
+}
+
+extern "C" int trpo_dev_fvp(trpo_dev *d) {
+    if (!d) return -1;
+    if (d->n_total <= 0) return -1;
+    HCHK(hipSetDevice(d->device));
+    int rc = enqueue_fvp_core(d, d->vec[TRPO_VEC_V], &d->ctl->zero);
+    if (rc) return rc;
+    hipLaunchKernelGGL(fvp_epilogue_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, d->zacc,
+                       d->vec[TRPO_VEC_V], d->vec[TRPO_VEC_Z], d->P, d->nw, d->ctl);
+    HCHK(hipGetLastError());
+    return 0;
+}
+
+extern "C" int trpo_dev_fvp_kernel(trpo_dev *d) {
+    if (!d || d->n == 0) return -1;
+    HCHK(hipSetDevice(d->device));
+    if (d->fast) {
+        const int ntiles = cdiv((long)d->n, 16);
+        d->fast->launch(dim3(d->grid), dim3(512), d->fast->lds, d->stream, d->obs4, (int)d->n, ntiles, d->tpack,
+                        d->vec[TRPO_VEC_V], d->vmap, d->slabs, d->net, &d->ctl->zero);
+    } else {
+        hipLaunchKernelGGL(fvp_generic_kernel, dim3(d->grid), dim3(GEN_T), 0, d->stream, d->obs32, (int)d->n,
+                           d->th32, d->v32, d->iv32, d->scratch, d->srows, d->slabs, d->net, &d->ctl->zero);
+    }
+    HCHK(hipGetLastError());
+    return 0;
+}
+
+static int ensure_hist(trpo_dev *d, size_t maxiter) {
+    if ((int)maxiter + 1 <= d->hist_cap) return 0;
+    if (d->hist) hipFree(d->hist);
+    d->hist = NULL;
+    HCHK(hipMalloc((void **)&d->hist, sizeof(double) * 2 * (maxiter + 1)));
+    d->hist_cap = (int)maxiter + 1;
+    if (d->cg_exec) {
+        hipGraphExecDestroy(d->cg_exec);
+        d->cg_exec = NULL;
+    }
+    return 0;
+}
+
+static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
+    double *x = d->vec[TRPO_VEC_X], *p = d->vec[TRPO_VEC_P], *b = d->vec[TRPO_VEC_B];
+    hipLaunchKernelGGL(cg_init_kernel, dim3(1), dim3(1024), 0, d->stream, b, x, d->r, p, d->P, d->ctl, d->hist,
+                       (int)maxiter, resth);
+    for (size_t it = 0; it < maxiter; ++it) {
+        int rc = enqueue_fvp_core(d, p, &d->ctl->done);
+        if (rc) return rc;
+        hipLaunchKernelGGL(cg_update_kernel, dim3(1), dim3(1024), 0, d->stream, d->zacc, x, d->r, p, d->P, d->nw,
+                           d->ctl, d->hist);
+    }
+    HCHK(hipGetLastError());
+    return 0;
+}
+
+extern "C" int trpo_dev_cg(trpo_dev *d, size_t maxiter, double resth) {
+    if (!d || d->n_total <= 0) return -1;
+    HCHK(hipSetDevice(d->device));
+    if (maxiter > 100000) return -1;
+    int rc = ensure_hist(d, maxiter);
+    if (rc) return rc;
+    const char *ng = getenv("TRPO_NO_GRAPH");
+    if (ng && atoi(ng)) return enqueue_cg_body(d, maxiter, resth);
+    // the graph bakes (maxiter, resth) into cg_init's arguments: key on both
+    if (!d->cg_exec || d->cg_graph_iters != maxiter || d->cg_graph_resth != resth) {
+        if (d->cg_exec) {
+            hipGraphExecDestroy(d->cg_exec);
+            d->cg_exec = NULL;
+        }
+        hipGraph_t graph;
+        HCHK(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
+        rc = enqueue_cg_body(d, maxiter, resth);
+        hipError_t e = hipStreamEndCapture(d->stream, &graph);
+        if (rc) return rc;
+        HCHK(e);
+        e = hipGraphInstantiate(&d->cg_exec, graph, NULL, NULL, 0);
+        hipGraphDestroy(graph);
+        HCHK(e);
+        d->cg_graph_iters = maxiter;
+        d->cg_graph_resth = resth;
+    }
+    HCHK(hipGraphLaunch(d->cg_exec, d->stream));
+    return 0;
+}
+
+extern "C" int trpo_dev_cg_history(trpo_dev *d, double *rdotr, double *xnorm, size_t cap, size_t *iters) {
+    if (!d || !d->hist) return -1;
+    HCHK(hipSetDevice(d->device));
+    HCHK(hipStreamSynchronize(d->stream));
+    Ctl c;
+    HCHK(hipMemcpyAsync(&c, d->ctl, sizeof c, hipMemcpyDeviceToHost, d->stream));
+    HCHK(hipStreamSynchronize(d->stream));
+    const size_t n = (size_t)c.iter + 1;
+    double *h = (double *)malloc(sizeof(double) * 2 * n);
+    if (!h) return -3;
+    HCHK(hipMemcpyAsync(h, d->hist, sizeof(double) * 2 * n, hipMemcpyDeviceToHost, d->stream));
+    HCHK(hipStreamSynchronize(d->stream));
+    for (size_t i = 0; i < n && i < cap; ++i) {
+        if (rdotr) rdotr[i] = h[2 * i];
+        if (xnorm) xnorm[i] = h[2 * i + 1];
+    }
+    free(h);
+    if (iters) *iters = (size_t)c.iter;
+    return 0;
+}
+
+extern "C" int trpo_dev_sync(trpo_dev *d) {
+    if (!d) return -1;
+    HCHK(hipSetDevice(d->device));
+    HCHK(hipStreamSynchronize(d->stream));
+    return 0;
+}
+
+extern "C" double trpo_dev_time(trpo_dev *d, int what, int reps, size_t maxiter, double resth) {
+    if (!d || reps < 1) return -1;
+    if (hipSetDevice(d->device) != hipSuccess) return -2;
+    int rc = 0;
+    // warm once (also captures the CG graph)
+    if (what == 0) rc = trpo_dev_fvp_kernel(d);
+    else if (what == 1) rc = trpo_dev_fvp(d);
+    else rc = trpo_dev_cg(d, maxiter, resth);
+    if (rc) return rc;
+    if (hipStreamSynchronize(d->stream) != hipSuccess) return -2;
+    hipEventRecord(d->ev0, d->stream);
+    for (int i = 0; i < reps && !rc; ++i) {
+        if (what == 0) rc = trpo_dev_fvp_kernel(d);
+        else if (what == 1) rc = trpo_dev_fvp(d);
+        else rc = trpo_dev_cg(d, maxiter, resth);
+    }
+    hipEventRecord(d->ev1, d->stream);
+    if (rc) return rc;
+    if (hipEventSynchronize(d->ev1) != hipSuccess) return -2;
+    float ms = 0;
+    hipEventElapsedTime(&ms, d->ev0, d->ev1);
+    return (double)ms / reps;
+}
+
+extern "C" const char *trpo_dev_kernel_name(const trpo_dev *d) { return d ? d->name : ""; }
+
+extern "C" int trpo_dev_geometry(const trpo_dev *d, int *blocks, int *threads, int *lds_bytes) {
+    if (!d) return -1;
+    if (blocks) *blocks = d->grid;
+    if (threads) *threads = d->fast ? 512 : GEN_T;
+    if (lds_bytes) *lds_bytes = d->fast ? d->fast->lds : 0;
+    return 0;
+}

@@ -1,0 +1,312 @@
+"""Python mirror of the reference's FVP/CG operator interface over libtrpo_mi355x.so.
+
+Everything here is a ctypes view of the C ABI in include/trpo_mi355x.h -- the
+same entry points the reference's C callers link against
+(src/include/TRPO.h:81-101): ``NumParamsCalc``, ``FVP``, ``FVPFast``, ``CG``,
+``FVP_FPGA``, ``CG_FPGA`` with a field-for-field ``TRPOparam`` -- plus the
+in-memory :class:`Context`.  There is no CPU fallback: if the HIP library is
+missing or no MI355X is visible, calls fail loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libtrpo_mi355x.so")
+HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "trpo_mi355x.h")
+
+_lib = None
+_dp = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+
+
+class TRPOparam(C.Structure):
+    """Layout of TRPOparam, src/include/TRPO.h:6-49 (passed BY VALUE)."""
+    _fields_ = [
+        ("ModelFile", C.c_char_p),
+        ("BaselineFile", C.c_char_p),
+        ("ResultFile", C.c_char_p),
+        ("DataFile", C.c_char_p),
+        ("NumLayers", C.c_size_t),
+        ("AcFunc", C.c_char_p),
+        ("LayerSize", C.POINTER(C.c_size_t)),
+        ("NumSamples", C.c_size_t),
+        ("CG_Damping", C.c_double),
+        ("PaddedLayerSize", C.POINTER(C.c_size_t)),
+        ("NumBlocks", C.POINTER(C.c_size_t)),
+    ]
+
+
+class TRPOError(RuntimeError):
+    pass
+
+
+def build(verbose: bool = False) -> str:
+    """Compile lib/libtrpo_mi355x.so for gfx950 (hipcc cross-compiles; no GPU needed)."""
+    import subprocess
+    out = subprocess.run(["make", "-s", "-C", PKG_DIR, "-j4"], capture_output=not verbose, text=True)
+    if out.returncode != 0:
+        raise TRPOError("build failed:\n" + (out.stdout or "") + (out.stderr or ""))
+    return LIB_PATH
+
+
+def lib():
+    """Load libtrpo_mi355x.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise TRPOError("libtrpo_mi355x.so not built: run trpo_amd.build() / make -C trpo-robot-control_amd")
+    L = C.CDLL(LIB_PATH)
+    sz = C.c_size_t
+    P = C.POINTER
+    L.NumParamsCalc.restype = sz
+    L.NumParamsCalc.argtypes = [P(sz), sz]
+    for name in ("FVPFast",):
+        getattr(L, name).restype = C.c_double
+        getattr(L, name).argtypes = [TRPOparam, _dp, _dp, sz]
+    for name in ("FVP", "FVP_FPGA"):
+        getattr(L, name).restype = C.c_double
+        getattr(L, name).argtypes = [TRPOparam, _dp, _dp]
+    for name in ("CG", "CG_FPGA"):
+        getattr(L, name).restype = C.c_double
+        getattr(L, name).argtypes = [TRPOparam, _dp, _dp, sz, C.c_double, sz]
+    L.trpo_ctx_create.restype = C.c_void_p
+    L.trpo_ctx_create.argtypes = [sz, P(sz), C.c_char_p, C.c_void_p, C.c_void_p, sz, C.c_void_p, C.c_double, C.c_int]
+    L.trpo_ctx_destroy.restype = None
+    L.trpo_ctx_destroy.argtypes = [C.c_void_p]
+    for name in ("trpo_ctx_set_theta", "trpo_ctx_set_std", "trpo_ctx_upload_b", "trpo_ctx_upload_v",
+                 "trpo_ctx_download_x", "trpo_ctx_download_z"):
+        getattr(L, name).restype = C.c_int
+        getattr(L, name).argtypes = [C.c_void_p, _dp]
+    L.trpo_ctx_set_obs.restype = C.c_int
+    L.trpo_ctx_set_obs.argtypes = [C.c_void_p, C.c_void_p, sz]
+    L.trpo_ctx_set_damping.restype = C.c_int
+    L.trpo_ctx_set_damping.argtypes = [C.c_void_p, C.c_double]
+    L.trpo_ctx_num_params.restype = sz
+    L.trpo_ctx_num_params.argtypes = [C.c_void_p]
+    L.trpo_comm_unique_id.restype = C.c_int
+    L.trpo_comm_unique_id.argtypes = [C.c_char_p]
+    L.trpo_ctx_attach_comm.restype = C.c_int
+    L.trpo_ctx_attach_comm.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_char_p]
+    L.trpo_ctx_fvp.restype = C.c_double
+    L.trpo_ctx_fvp.argtypes = [C.c_void_p, _dp, _dp]
+    L.trpo_ctx_cg.restype = C.c_double
+    L.trpo_ctx_cg.argtypes = [C.c_void_p, _dp, sz, C.c_double, _dp, C.c_int]
+    L.trpo_ctx_cg_history.restype = C.c_int
+    L.trpo_ctx_cg_history.argtypes = [C.c_void_p, _dp, _dp, sz, P(sz)]
+    for name in ("trpo_ctx_enqueue_fvp", "trpo_ctx_enqueue_fvp_kernel_only", "trpo_ctx_synchronize"):
+        getattr(L, name).restype = C.c_int
+        getattr(L, name).argtypes = [C.c_void_p]
+    L.trpo_ctx_enqueue_cg.restype = C.c_int
+    L.trpo_ctx_enqueue_cg.argtypes = [C.c_void_p, sz, C.c_double]
+    L.trpo_ctx_time.restype = C.c_double
+    L.trpo_ctx_time.argtypes = [C.c_void_p, C.c_int, C.c_int, sz, C.c_double]
+    L.trpo_ctx_kernel_name.restype = C.c_char_p
+    L.trpo_ctx_kernel_name.argtypes = [C.c_void_p]
+    L.trpo_ctx_launch_geometry.restype = C.c_int
+    L.trpo_ctx_launch_geometry.argtypes = [C.c_void_p, P(C.c_int), P(C.c_int), P(C.c_int)]
+    L.trpo_last_error.restype = C.c_char_p
+    L.trpo_last_error.argtypes = []
+    L.trpo_cache_clear.restype = None
+    L.trpo_cache_clear.argtypes = []
+    _lib = L
+    return L
+
+
+def last_error() -> str:
+    return lib().trpo_last_error().decode(errors="replace")
+
+
+# --------------------------------------------------------------------------
+# reference-shaped entry points (src/include/TRPO.h:81-101)
+# --------------------------------------------------------------------------
+def _sizes(layers):
+    arr = (C.c_size_t * len(layers))(*layers)
+    return arr
+
+
+def make_param(model_file: str, data_file: str, layers, acfunc: str, num_samples: int,
+               cg_damping: float = 0.1) -> TRPOparam:
+    """Build a TRPOparam as TRPOCpuCode.c does (src/TRPOCpuCode.c:88-95)."""
+    p = TRPOparam()
+    p._keep = (model_file.encode(), data_file.encode(), acfunc.encode(), _sizes(layers))
+    p.ModelFile, p.DataFile, ac, ls = p._keep
+    p.AcFunc = ac
+    p.LayerSize = C.cast(ls, C.POINTER(C.c_size_t))
+    p.NumLayers = len(layers)
+    p.NumSamples = num_samples
+    p.CG_Damping = cg_damping
+    return p
+
+
+def NumParamsCalc(layers) -> int:
+    return int(lib().NumParamsCalc(_sizes(layers), len(layers)))
+
+
+def FVPFast(param: TRPOparam, result: np.ndarray, inp: np.ndarray, num_threads: int = 1) -> float:
+    return float(lib().FVPFast(param, result, inp, num_threads))
+
+
+def FVP(param: TRPOparam, result: np.ndarray, inp: np.ndarray) -> float:
+    return float(lib().FVP(param, result, inp))
+
+
+def CG(param: TRPOparam, result: np.ndarray, b: np.ndarray, max_iter: int = 10, residual_th: float = 1e-10,
+       num_threads: int = 1) -> float:
+    return float(lib().CG(param, result, b, max_iter, residual_th, num_threads))
+
+
+def FVP_FPGA(param: TRPOparam, result: np.ndarray, inp: np.ndarray) -> float:
+    return float(lib().FVP_FPGA(param, result, inp))
+
+
+def CG_FPGA(param: TRPOparam, result: np.ndarray, b: np.ndarray, max_iter: int = 10,
+            residual_th: float = 1e-10, num_threads: int = 1) -> float:
+    return float(lib().CG_FPGA(param, result, b, max_iter, residual_th, num_threads))
+
+
+# --------------------------------------------------------------------------
+# in-memory context (include/trpo_mi355x.h part 2)
+# --------------------------------------------------------------------------
+class Context:
+    """Device-resident FVP/CG problem: weights, observations and P-vectors stay in HBM."""
+
+    def __init__(self, layers, acfunc: str, theta, obs, std, cg_damping: float = 0.1, device: int = -1):
+        L = lib()
+        self.layers = [int(x) for x in layers]
+        self.acfunc = acfunc
+        self.P = NumParamsCalc(self.layers)
+        theta = np.ascontiguousarray(theta, dtype=np.float64)
+        obs = np.ascontiguousarray(obs, dtype=np.float64)
+        std = np.ascontiguousarray(std, dtype=np.float64)
+        if theta.size != self.P or obs.ndim != 2 or obs.shape[1] != self.layers[0] or std.size != self.layers[-1]:
+            raise ValueError("shape mismatch: theta %s obs %s std %s for layers %s"
+                             % (theta.shape, obs.shape, std.shape, self.layers))
+        self.n = obs.shape[0]
+        self._h = L.trpo_ctx_create(len(self.layers), _sizes(self.layers), acfunc.encode(),
+                                    theta.ctypes.data, obs.ctypes.data, self.n, std.ctypes.data, cg_damping,
+                                    device)
+        if not self._h:
+            raise TRPOError("trpo_ctx_create failed: " + last_error())
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().trpo_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @staticmethod
+    def _chk(rc, what):
+        if rc < 0:
+            raise TRPOError("%s failed (%s): %s" % (what, rc, last_error()))
+        return rc
+
+    def set_theta(self, theta):
+        self._chk(lib().trpo_ctx_set_theta(self._h, np.ascontiguousarray(theta, np.float64)), "set_theta")
+
+    def set_std(self, std):
+        self._chk(lib().trpo_ctx_set_std(self._h, np.ascontiguousarray(std, np.float64)), "set_std")
+
+    def set_obs(self, obs):
+        obs = np.ascontiguousarray(obs, dtype=np.float64)
+        self._chk(lib().trpo_ctx_set_obs(self._h, obs.ctypes.data, obs.shape[0]), "set_obs")
+        self.n = obs.shape[0]
+
+    def set_damping(self, d):
+        self._chk(lib().trpo_ctx_set_damping(self._h, d), "set_damping")
+
+    def attach_comm(self, rank: int, world: int, unique_id: bytes):
+        self._chk(lib().trpo_ctx_attach_comm(self._h, rank, world, unique_id), "attach_comm")
+
+    def fvp(self, v):
+        out = np.zeros(self.P)
+        self._chk(lib().trpo_ctx_fvp(self._h, np.ascontiguousarray(v, np.float64), out), "fvp")
+        return out
+
+    def cg(self, b, max_iter=10, residual_th=1e-10, verbose=False):
+        x = np.zeros(self.P)
+        self._chk(lib().trpo_ctx_cg(self._h, np.ascontiguousarray(b, np.float64), max_iter, residual_th, x,
+                                    1 if verbose else 0), "cg")
+        return x
+
+    def cg_history(self, cap=1024):
+        rr, xn, it = np.zeros(cap), np.zeros(cap), C.c_size_t(0)
+        self._chk(lib().trpo_ctx_cg_history(self._h, rr, xn, cap, C.byref(it)), "cg_history")
+        n = it.value + 1
+        return rr[:n], xn[:n], it.value
+
+    # device-resident hooks used by bench.py
+    def upload_b(self, b):
+        self._chk(lib().trpo_ctx_upload_b(self._h, np.ascontiguousarray(b, np.float64)), "upload_b")
+
+    def upload_v(self, v):
+        self._chk(lib().trpo_ctx_upload_v(self._h, np.ascontiguousarray(v, np.float64)), "upload_v")
+
+    def enqueue_cg(self, max_iter=10, residual_th=0.0):
+        self._chk(lib().trpo_ctx_enqueue_cg(self._h, max_iter, residual_th), "enqueue_cg")
+
+    def enqueue_fvp(self):
+        self._chk(lib().trpo_ctx_enqueue_fvp(self._h), "enqueue_fvp")
+
+    def enqueue_fvp_kernel(self):
+        self._chk(lib().trpo_ctx_enqueue_fvp_kernel_only(self._h), "enqueue_fvp_kernel")
+
+    def synchronize(self):
+        self._chk(lib().trpo_ctx_synchronize(self._h), "synchronize")
+
+    def time_ms(self, what: int, reps: int, max_iter: int = 10, residual_th: float = 0.0) -> float:
+        return self._chk(lib().trpo_ctx_time(self._h, what, reps, max_iter, residual_th), "time")
+
+    def download_x(self):
+        x = np.zeros(self.P)
+        self._chk(lib().trpo_ctx_download_x(self._h, x), "download_x")
+        return x
+
+    def download_z(self):
+        z = np.zeros(self.P)
+        self._chk(lib().trpo_ctx_download_z(self._h, z), "download_z")
+        return z
+
+    @property
+    def kernel_name(self) -> str:
+        return lib().trpo_ctx_kernel_name(self._h).decode()
+
+    @property
+    def geometry(self):
+        b, t, l = C.c_int(0), C.c_int(0), C.c_int(0)
+        lib().trpo_ctx_launch_geometry(self._h, C.byref(b), C.byref(t), C.byref(l))
+        return dict(blocks=b.value, threads=t.value, lds_bytes=l.value)
+
+
+def unique_id() -> bytes:
+    buf = C.create_string_buffer(128)
+    rc = lib().trpo_comm_unique_id(buf)
+    if rc < 0:
+        raise TRPOError("ncclGetUniqueId failed")
+    return buf.raw
+
+
+def cache_clear():
+    lib().trpo_cache_clear()
+
+
+def header_symbols(path: str = HEADER):
+    """Function names declared in include/trpo_mi355x.h (for the export test)."""
+    import re
+    txt = open(path).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\(", txt)) - {"if", "defined", "sizeof"})
