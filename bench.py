@@ -1,0 +1,253 @@
+#!/usr/bin/env python3
+"""Headline benchmark: FVP samples/sec + 10-iteration CG wall time, armDOF_0 policy.
+
+BASELINE.json metric "FVP samples/sec + 10-iter CG wall time, armDOF_0 policy,
+1/2/4/8 MI355X".  One STEP = one complete 10-iteration CG solve (ResidualTh=0,
+so exactly 10 Fisher-vector products + the fp64 CG vector updates) over a
+synthetic armDOF_0 batch of 50 000 samples resident in HBM (SURVEY.md §8d,
+configs C3/C4).  With --gpus N the 50 000 samples are split into contiguous
+shards, one per rank, and every FVP all-reduces the P-sized partial sum over
+RCCL (strong scaling, config C4).
+
+    python bench.py                      # N=1
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Rank 0 prints ONE JSON line.  value = 10 * 50 000 / (seconds per solve), the
+whole-job FVP throughput; ms_per_step = the CG wall time.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "trpo-robot-control_amd"), os.path.join(ROOT, "oracle")]
+
+import trpo_amd  # noqa: E402
+from trpo_amd import synth  # noqa: E402
+
+ARM = [15, 16, 16, 3]
+N_TOTAL = 50_000
+CG_ITERS = 10
+DAMPING = 0.1
+PEAK_FP32_TFLOPS = 157.3     # MI355X dense FP32 (vector = matrix), MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0
+
+
+def flops_per_sample(L):
+    """2(5S - 2 L0 L1) + 7(L1 + L2) + 2 L3, S = sum L_i L_{i+1}."""
+    S = sum(L[i] * L[i + 1] for i in range(len(L) - 1))
+    return 2 * (5 * S - 2 * L[0] * L[1]) + 7 * sum(L[1:-1]) + 2 * L[-1]
+
+
+def bytes_per_fvp(L, n):
+    """observations read once + v in, Fv out, theta read once (fp32)."""
+    return 4 * n * L[0] + 12 * synth.num_params(L)
+
+
+from trpo_amd.dist import shard_range as shard  # noqa: E402
+
+
+class Dist:
+    """torch.distributed (gloo) only for bootstrap, barriers and the max-over-ranks
+    timing; the data path all-reduce is RCCL inside libtrpo_mi355x.so."""
+
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.pg = None
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+            self.dist = dist
+
+    def barrier(self):
+        if self.pg is None and self.world > 1:
+            self.dist.barrier()
+
+    def bcast_bytes(self, b: bytes | None) -> bytes:
+        if self.world == 1:
+            return b
+        obj = [b]
+        self.dist.broadcast_object_list(obj, src=0)
+        return obj[0]
+
+    def max(self, x: float) -> float:
+        if self.world == 1:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.world > 1:
+            self.dist.destroy_process_group()
+
+
+def make_ctx(L, n_total, dist, device):
+    theta = synth.make_theta(L)
+    obs_all = synth.make_obs(n_total, L[0])
+    lo, hi = shard(n_total, dist.rank, dist.world)
+    ctx = trpo_amd.Context(L, "lttl", theta, obs_all[lo:hi], np.ones(L[-1]), DAMPING, device=device)
+    if dist.world > 1:
+        uid = dist.bcast_bytes(trpo_amd.unique_id() if dist.rank == 0 else None)
+        ctx.attach_comm(dist.rank, dist.world, uid)
+    return ctx, theta, obs_all
+
+
+def time_steps(ctx, dist, steps, warmup, b):
+    ctx.upload_b(b)
+    for _ in range(warmup):
+        ctx.enqueue_cg(CG_ITERS, 0.0)
+    ctx.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ctx.enqueue_cg(CG_ITERS, 0.0)
+    ctx.synchronize()
+    t1 = time.perf_counter()
+    dist.barrier()
+    return dist.max(t1 - t0)
+
+
+def cpu_baseline(theta, obs_all, b, gpu_x):
+    """The reference's own CG (oracle/_ref, compiled from src/TRPO_FVP.c + TRPO_CG.c with
+    the Makefile.cpuonly flags) on 1 host core, full 10-iteration solve at N=50k; falls back
+    to the clean-room port (oracle/liboracle.so) when oracle/_ref was not built."""
+    import oracle
+    n = obs_all.shape[0]
+    res = dict(unit="FVP samples/s", cores=1,
+               sample="one full 10-iteration CG solve, armDOF_0, N=50000, ResidualTh=0, 1 thread")
+    x_ref = None
+    if os.path.exists(oracle.REF_DRIVER_FAST):
+        with tempfile.TemporaryDirectory() as tmp:
+            mf, df, bf, xf = (os.path.join(tmp, f) for f in ("m.txt", "d.txt", "b.txt", "x.txt"))
+            synth.write_model_file(mf, theta)
+            synth.write_data_file(df, obs_all, np.ones(ARM[-1]))
+            synth.write_vector_file(bf, b)
+            cmd = [oracle.REF_DRIVER_FAST, "cg", mf, df, str(n), ",".join(map(str, ARM)), "lttl", str(DAMPING), bf,
+                   str(CG_ITERS), "0", xf, "1"]
+            w0 = time.perf_counter()
+            out = subprocess.run(cmd, capture_output=True, text=True)
+            wall = time.perf_counter() - w0
+            if out.returncode == 0:
+                x_ref = np.loadtxt(xf)
+                # compute seconds exclude the reference's per-call file parsing: time it separately
+                tcmd = [oracle.REF_DRIVER_FAST, "time", mf, df, str(n), ",".join(map(str, ARM)), "lttl",
+                        str(DAMPING), bf, str(CG_ITERS), "0", "1"]
+                tout = subprocess.run(tcmd, capture_output=True, text=True)
+                tj = json.loads(tout.stderr.strip().splitlines()[-1])
+                res.update(kind="reference", value=CG_ITERS * n / tj["compute_s"], compute_s=tj["compute_s"],
+                           wall_s_incl_file_parse=tj["wall_s"])
+    if x_ref is None:
+        r = oracle.cg(ARM, "lttl", theta, obs_all, np.ones(ARM[-1]), b, CG_ITERS, 0.0, DAMPING, threads=1)
+        x_ref = r["x"]
+        res.update(kind="port", value=CG_ITERS * n / r["seconds"], compute_s=r["seconds"])
+    try:
+        res["cpu_model"] = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if "model name" in l][0]
+    except Exception:
+        pass
+    rel = float(np.linalg.norm(gpu_x - x_ref) / np.linalg.norm(x_ref))
+    return res, rel
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--extra", action="store_true", help="also time the 2x64 configs (C2/C3)")
+    args = ap.parse_args()
+
+    dist = Dist()
+    if dist.world != args.gpus and dist.rank == 0:
+        print("warning: --gpus %d but WORLD_SIZE=%d" % (args.gpus, dist.world), file=sys.stderr)
+    device = dist.local_rank
+
+    ctx, theta, obs_all = make_ctx(ARM, N_TOTAL, dist, device)
+    P = synth.num_params(ARM)
+    b = synth.make_b(P)
+
+    t = time_steps(ctx, dist, args.steps, args.warmup, b)
+    ms_per_step = 1e3 * t / args.steps
+    value = CG_ITERS * N_TOTAL / (t / args.steps)
+    x = ctx.download_x()
+
+    # dominant kernel: the fused FVP kernel, timed with HIP events on the context's stream
+    ctx.upload_v(synth.make_v(P))
+    reps = 200
+    k_ms = ctx.time_ms(0, reps)
+    fvp_ms = ctx.time_ms(1, reps)
+    n_local = ctx.n
+    flops = flops_per_sample(ARM) * n_local
+    achieved_tflops = flops / (k_ms * 1e-3) / 1e12
+    bytes_alg = bytes_per_fvp(ARM, n_local)
+
+    result = {
+        "metric": "FVP samples/sec + 10-iter CG wall time, armDOF_0 policy",
+        "value": value,
+        "unit": "FVP samples/s",
+        "n_gpus": dist.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (seeded splitmix64, SURVEY §8d)",
+        "config": {"workload": "cg10_armDOF_0_N50000", "policy": "armDOF_0 [15,16,16,3] lttl",
+                   "samples": N_TOTAL, "cg_iters": CG_ITERS, "residual_th": 0.0, "damping": DAMPING,
+                   "parallelism": "dp%d (contiguous sample shards, RCCL all-reduce per FVP)" % dist.world,
+                   "cg_scalars": "fp64", "fvp_kernel": ctx.kernel_name, "geometry": ctx.geometry},
+        "cg_wall_ms": ms_per_step,
+        "fvp_ms": fvp_ms,
+        "roofline": {"bound": "mfma", "achieved": achieved_tflops, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved_tflops / PEAK_FP32_TFLOPS, "traffic": None,
+                     "kernel": "fvp_mlp3_kernel", "kernel_ms": k_ms, "flops_per_launch": flops,
+                     "alg_bytes_per_launch": bytes_alg,
+                     "hbm_gbs_algorithmic": bytes_alg / (k_ms * 1e-3) / 1e9,
+                     "hbm_frac_algorithmic": bytes_alg / (k_ms * 1e-3) / 1e9 / PEAK_HBM_GBS},
+    }
+
+    if args.extra and dist.world == 1:
+        extra = {}
+        L2 = [15, 64, 64, 3]
+        c2, th2, obs2 = make_ctx(L2, 4096, dist, device)
+        c2.upload_v(synth.make_v(synth.num_params(L2)))
+        k2 = c2.time_ms(0, reps)
+        f2 = c2.time_ms(1, reps)
+        extra["C2_fvp_2x64_N4096"] = {"fvp_ms": f2, "kernel_ms": k2, "fvp_samples_per_s": 4096 / (f2 * 1e-3),
+                                      "kernel_tflops": flops_per_sample(L2) * 4096 / (k2 * 1e-3) / 1e12}
+        c2.close()
+        c3, th3, obs3 = make_ctx(L2, N_TOTAL, dist, device)
+        t3 = time_steps(c3, dist, 20, 3, synth.make_b(synth.num_params(L2)))
+        k3 = c3.time_ms(0, reps)
+        extra["C3_cg10_2x64_N50000"] = {"cg_wall_ms": 1e3 * t3 / 20, "fvp_samples_per_s": CG_ITERS * N_TOTAL / (t3 / 20),
+                                        "kernel_ms": k3,
+                                        "kernel_tflops": flops_per_sample(L2) * N_TOTAL / (k3 * 1e-3) / 1e12}
+        c3.close()
+        result["extra"] = extra
+
+    if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
+        cb, rel = cpu_baseline(theta, obs_all, b, x)
+        result["cpu_baseline"] = cb
+        result["parity"] = {"cg_step_relL2_vs_cpu": rel, "tolerance": 1e-4}
+    ctx.close()
+    dist.close()
+    if dist.rank == 0:
+        print(json.dumps(result), flush=True)
+
+
+if __name__ == "__main__":
+    main()

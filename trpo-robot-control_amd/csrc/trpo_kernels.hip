@@ -91,18 +91,32 @@ __device__ __forceinline__ float act_r(int a, float y, float rx) {
 }
 __device__ __forceinline__ f4 act_fwd(int a, f4 x, f4 rx, f4 &ry) {
     f4 y;
+    if (a == ACT_T) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        y[r] = act_y(a, x[r]);
-        ry[r] = act_r(a, y[r], rx[r]);
+        for (int r = 0; r < 4; ++r) {
+            y[r] = tanhf(x[r]);
+            ry[r] = rx[r] * (1.0f - y[r] * y[r]);
+        }
+    } else if (a == ACT_S) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            y[r] = 1.0f / (1.0f + expf(-x[r]));
+            ry[r] = rx[r] * y[r] * (1.0f - y[r]);
+        }
+    } else if (a == ACT_O) {
+        y = 0.1f * x;
+        ry = 0.1f * rx;
+    } else {
+        y = x;
+        ry = rx;
     }
     return y;
 }
 __device__ __forceinline__ f4 act_bwd(int a, f4 y, f4 g) {
-    f4 o;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) o[r] = act_r(a, y[r], g[r]);
-    return o;
+    if (a == ACT_T) return g * (1.0f - y * y);
+    if (a == ACT_S) return g * y * (1.0f - y);
+    if (a == ACT_O) return 0.1f * g;
+    return g;
 }
 __device__ __forceinline__ bool act_needs_y(int a) { return a == ACT_T || a == ACT_S; }
 
@@ -161,6 +175,38 @@ __global__ void gather_pack_kernel(float *dst, const double *src, const int *map
     }
 }
 
+// slab position -> natural parameter index (or -1) for the fast kernel's accumulator order:
+// f4 k over [W0 tiles (T0 x T1), W1 (T1 x T2), W2 (T2 x T3), B1 (T1), B2 (T2), B3 (T3)], then lane, r.
+__global__ void build_imap_kernel(Net n, Pack pk, int *imap, int slab) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= slab) return;
+    const int k = j >> 8, lane = (j >> 2) & 63, r = j & 3, c = lane & 15, g = lane >> 4;
+    const int *T = pk.T;
+    int base = 0, m = -1;
+    for (int i = 0; i < 3 && m == -1; ++i) {
+        const int nt = T[i] * T[i + 1];
+        if (k < base + nt) {
+            const int at = (k - base) / T[i + 1], bt = (k - base) % T[i + 1];
+            const int a = 16 * at + 4 * g + r, b = 16 * bt + c;
+            m = (a < n.L[i] && b < n.L[i + 1]) ? n.woff[i] + a * n.L[i + 1] + b : -2;
+        }
+        base += nt;
+    }
+    for (int i = 0; i < 3 && m == -1; ++i) {
+        if (k < base + T[i + 1]) {
+            const int b = 16 * (k - base) + 4 * g + r;
+            m = (c == 0 && b < n.L[i + 1]) ? n.boff[i] + b : -2;
+        }
+        base += T[i + 1];
+    }
+    imap[j] = m < 0 ? -1 : m;
+}
+
+__global__ void iota_kernel(int *v, int len, int valid) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < len) v[j] = j < valid ? j : -1;
+}
+
 __global__ void set_invvar_kernel(float *iv, const double *stdv, int A, int len) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j < len) iv[j] = j < A ? (float)(1.0 / stdv[j] / stdv[j]) : 0.0f;
@@ -178,6 +224,22 @@ __global__ void to_f32_kernel(float *dst, const double *src, int len) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e < len) dst[e] = (float)src[e];
 }
+
+// ---------------------------------------------------------------------------
+// Diagnostic build only (-DTRPO_STAMPS): s_memrealtime (100 MHz) stamps per block.
+// ---------------------------------------------------------------------------
+#ifdef TRPO_STAMPS
+__device__ unsigned long long g_stamps[1024 * 16];
+#define STAMP(k)                                                                             \
+    do {                                                                                     \
+        if (threadIdx.x == 0 && blockIdx.x < 1024) {                                         \
+            g_stamps[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memrealtime();              \
+            g_stamps[blockIdx.x * 16 + 8 + (k)] = __builtin_amdgcn_s_memtime();              \
+        }                                                                                    \
+    } while (0)
+#else
+#define STAMP(k) do { } while (0)
+#endif
 
 // ---------------------------------------------------------------------------
 // The fused FVP kernel, 3 weight layers (NumLayers == 4), MFMA path.
@@ -209,16 +271,36 @@ struct FastCfg {
     static constexpr int R0 = 16 * (T0 + T1), R1 = 16 * (T1 + T2), R2 = 16 * (T2 + T3);
     static constexpr int ROWS = R0 > R1 ? (R0 > R2 ? R0 : R2) : (R1 > R2 ? R1 : R2);
     static constexpr int SCR = ROWS * SCR_LD;
-    // accumulator registers per lane (for the cross-wave tree)
+    // accumulator registers per lane; the block's partial sums are written in this
+    // "accumulator order" (f4 k, lane, r) -- SLAB floats per block, mapped back to
+    // natural parameter order by the reduce kernel (imap)
     static constexpr int NACC = 4 * (T0 * T1 + T1 * T2 + T2 * T3 + T1 + T2 + T3);
+    static constexpr int SLAB = NACC * 64;
     static constexpr int WAVES = 8;
     static constexpr int THREADS = 64 * WAVES;
+    static constexpr int MAIN_BYTES = 4 * (TLEN + VLEN + WAVES * SCR);
+    static constexpr int CAP = MAIN_BYTES > 65536 ? MAIN_BYTES : 65536;
+    // waves combined per epilogue round (largest divisor of WAVES whose dumps fit)
+    static constexpr int RW = (8 * SLAB * 4 <= CAP) ? 8 : (4 * SLAB * 4 <= CAP) ? 4 : (2 * SLAB * 4 <= CAP) ? 2 : 1;
+    static constexpr int EPT = (SLAB / 4 + THREADS - 1) / THREADS;   // f4 slices per thread in the combine
     static int lds_bytes() {
-        int a = 4 * (TLEN + VLEN + WAVES * SCR);
-        int b = 4 * (WAVES / 2) * NACC * 64;      // tree reduction buffer (reuses the same LDS)
-        return a > b ? a : b;
+        const int b = 4 * RW * SLAB;
+        return MAIN_BYTES > b ? MAIN_BYTES : b;
     }
 };
+
+// sum over the 16 lanes of a DPP row (the 16 sample columns of a D tile), all lanes get it
+__device__ __forceinline__ float rowsum16(float v) {
+    int x = __float_as_int(v);
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false));   // quad_perm xor 1
+    x = __float_as_int(v);
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false));   // quad_perm xor 2
+    x = __float_as_int(v);
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x124, 0xF, 0xF, false));  // row_ror 4
+    x = __float_as_int(v);
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, x, 0x128, 0xF, 0xF, false));  // row_ror 8
+    return v;
+}
 
 __device__ __forceinline__ void scr_put(float *scr, int row0, f4 t, int c, int g) {
 #pragma unroll
@@ -228,33 +310,59 @@ __device__ __forceinline__ f4 scr_get(const float *scr, int row0, int c, int g) 
     return *reinterpret_cast<const f4 *>(scr + (row0 + c) * SCR_LD + 4 * g);
 }
 
-template <int T0, int T1, int T2, int T3>
+// ACT >= 0: activations of layers 1..3 fixed at compile time (a1 | a2 << 2 | a3 << 4);
+// ACT == -1: read from net.act at run time (wave-uniform branches).
+template <int T0, int T1, int T2, int T3, int ACT>
 __global__ void __launch_bounds__(512)
 fvp_mlp3_kernel(const f4 *__restrict__ obs4, int n, int ntiles, const float *__restrict__ tpack,
-                const double *__restrict__ v, const int *__restrict__ vmap, float *__restrict__ slabs, Net net,
-                const int *__restrict__ skip) {
+                const float *__restrict__ vpack, float *__restrict__ slabs, Net net, const int *__restrict__ skip) {
     using C = FastCfg<T0, T1, T2, T3>;
-    if (*skip) return;
+    (void)net;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     float *tw = lds;                                   // theta pack
-    float *vw = lds + C::TLEN;                         // v pack
+    float *vw = lds + C::TLEN;                         // v pack (fragment order, fp32)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int c = lane & 15, g = lane >> 4;
     float *scr = lds + C::TLEN + C::VLEN + wave * C::SCR;
+    const int nwaves = gridDim.x * C::WAVES;
+    STAMP(0);
 
-    // ---- stage the weights (fragment order) and gather+convert the direction ----
+    // ---- prologue: ONE round of global loads (skip flag, both packs, first tile) ----
+    constexpr int NT4 = C::TLEN / 4, NALL = (C::TLEN + C::VLEN) / 4;
+    constexpr int PER = (NALL + C::THREADS - 1) / C::THREADS;
+    const int skipv = *skip;
+    f4 st[PER];
     {
-        const f4 *src = reinterpret_cast<const f4 *>(tpack);
-        f4 *dst = reinterpret_cast<f4 *>(tw);
-        for (int e = tid; e < C::TLEN / 4; e += C::THREADS) dst[e] = src[e];
-        for (int e = tid; e < C::VLEN; e += C::THREADS) {
-            const int m = vmap[e];
-            vw[e] = m >= 0 ? (float)v[m] : 0.0f;
+        const f4 *tp4 = reinterpret_cast<const f4 *>(tpack);
+        const f4 *vp4 = reinterpret_cast<const f4 *>(vpack);
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int e = tid + k * C::THREADS;
+            if (e < NT4) st[k] = tp4[e];
+            else if (e < NALL) st[k] = vp4[e - NT4];
+        }
+    }
+    int tile = blockIdx.x * C::WAVES + wave;
+    f4 xn[T0];
+#pragma unroll
+    for (int kt = 0; kt < T0; ++kt)
+        xn[kt] = tile < ntiles ? obs4[(long)(tile * 16 + c) * (4 * T0) + kt * 4 + g] : f4{0.f, 0.f, 0.f, 0.f};
+    if (skipv) return;                                 // grid-uniform
+    {
+        f4 *dst = reinterpret_cast<f4 *>(lds);
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int e = tid + k * C::THREADS;
+            if (e < NALL) dst[e] = st[k];
         }
     }
     __syncthreads();
+    STAMP(1);
+    bool first_tile = true;
 
-    const int a1 = net.act[1], a2 = net.act[2], a3 = net.act[3];
+    const int a1 = ACT >= 0 ? (ACT & 3) : net.act[1];
+    const int a2 = ACT >= 0 ? ((ACT >> 2) & 3) : net.act[2];
+    const int a3 = ACT >= 0 ? ((ACT >> 4) & 3) : net.act[3];
     const bool y3_needed = act_needs_y(a3);
     const f4 *TW = reinterpret_cast<const f4 *>(tw);
     const f4 *VW = reinterpret_cast<const f4 *>(vw);
@@ -281,13 +389,17 @@ fvp_mlp3_kernel(const f4 *__restrict__ obs4, int n, int ntiles, const float *__r
 #pragma unroll
     for (int a = 0; a < T3; ++a) sB3[a] = zero4;
 
-    const int nwaves = gridDim.x * C::WAVES;
-    for (int tile = blockIdx.x * C::WAVES + wave; tile < ntiles; tile += nwaves) {
+    for (; tile < ntiles; tile += nwaves) {
         const int sample = tile * 16 + c;
-        // input tile: lane holds features 16kt+4g..+3 of its sample (D-layout rows)
+        // input tile: lane holds features 16kt+4g..+3 of its sample (D-layout rows);
+        // the next tile's observations are prefetched while this one computes
         f4 x0[T0];
 #pragma unroll
-        for (int kt = 0; kt < T0; ++kt) x0[kt] = obs4[(long)sample * (4 * T0) + kt * 4 + g];
+        for (int kt = 0; kt < T0; ++kt) x0[kt] = xn[kt];
+        if (tile + nwaves < ntiles) {
+#pragma unroll
+            for (int kt = 0; kt < T0; ++kt) xn[kt] = obs4[(long)(sample + 16 * nwaves) * (4 * T0) + kt * 4 + g];
+        }
 
         // ---- layer 0: x1 = W0^T x0 + b0 ; Rx1 = VW0^T x0 + vb0 (Ry0 = 0) ----
         f4 y1[T1], r1[T1];
@@ -313,6 +425,7 @@ fvp_mlp3_kernel(const f4 *__restrict__ obs4, int n, int ntiles, const float *__r
         for (int ot = 0; ot < T2; ++ot) {
             f4 a = TW[C::BI1 / 4 + ot * 4 + g];
             f4 ra = VW[C::VB1 / 4 + ot * 4 + g];
+            f4 rb = zero4;                    // second chain: halves the dependent MFMA depth
 #pragma unroll
             for (int kt = 0; kt < T1; ++kt) {
                 const f4 w = TW[C::FA1 / 4 + (ot * T1 + kt) * 64 + lane];
@@ -321,10 +434,10 @@ fvp_mlp3_kernel(const f4 *__restrict__ obs4, int n, int ntiles, const float *__r
                 for (int s = 0; s < 4; ++s) {
                     a = MFMA(w[s], y1[kt][s], a);
                     ra = MFMA(w[s], r1[kt][s], ra);
-                    ra = MFMA(u[s], y1[kt][s], ra);
+                    rb = MFMA(u[s], y1[kt][s], rb);
                 }
             }
-            y2[ot] = act_fwd(a2, a, ra, r2[ot]);
+            y2[ot] = act_fwd(a2, a, ra + rb, r2[ot]);
         }
         // ---- layer 2 (output) and G3 = act3'(Ry3 / sigma^2) ----
         f4 g3[T3];
@@ -333,6 +446,7 @@ fvp_mlp3_kernel(const f4 *__restrict__ obs4, int n, int ntiles, const float *__r
         for (int ot = 0; ot < T3; ++ot) {
             f4 a = TW[C::BI2 / 4 + ot * 4 + g];
             f4 ra = VW[C::VB2 / 4 + ot * 4 + g];
+            f4 rb = zero4;
 #pragma unroll
             for (int kt = 0; kt < T2; ++kt) {
                 const f4 w = TW[C::FA2 / 4 + (ot * T2 + kt) * 64 + lane];
@@ -341,16 +455,17 @@ fvp_mlp3_kernel(const f4 *__restrict__ obs4, int n, int ntiles, const float *__r
                 for (int s = 0; s < 4; ++s) {
                     if (y3_needed) a = MFMA(w[s], y2[kt][s], a);
                     ra = MFMA(w[s], r2[kt][s], ra);
-                    ra = MFMA(u[s], y2[kt][s], ra);
+                    rb = MFMA(u[s], y2[kt][s], rb);
                 }
             }
             f4 r3;
-            const f4 y3 = act_fwd(a3, a, ra, r3);
+            const f4 y3 = act_fwd(a3, a, ra + rb, r3);
             const f4 iv = TW[C::IV / 4 + ot * 4 + g];
             f4 gg = act_bwd(a3, y3, r3 * iv);
             g3[ot] = live ? gg : zero4;
             sB3[ot] += g3[ot];
         }
+        if (first_tile) STAMP(2);
         // ---- contraction RGW2 += Y2 . G3^T (K = 16 samples) ----
 #pragma unroll
         for (int t = 0; t < T2; ++t) scr_put(scr, 16 * t, y2[t], c, g);
@@ -433,9 +548,30 @@ fvp_mlp3_kernel(const f4 *__restrict__ obs4, int n, int ntiles, const float *__r
                     for (int s = 0; s < 4; ++s) accW0[at][bt] = MFMA(ya[s], gb[bt][s], accW0[at][bt]);
             }
         }
+#ifdef TRPO_STAMPS
+        if (first_tile) {
+            asm volatile("" ::"v"(accW0[0][0]));
+            STAMP(3);
+        }
+        first_tile = false;
+#endif
     }
 
-    // ---- deterministic cross-wave tree: (w, w+h) pairs, h = 4, 2, 1 ----
+    STAMP(4);
+    // ---- epilogue: bias partials summed over the 16 sample columns (DPP), then the
+    //      block's 8 wave copies combined in LDS in a fixed order, all threads writing ----
+#pragma unroll
+    for (int a = 0; a < T1; ++a)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sB1[a][r] = rowsum16(sB1[a][r]);
+#pragma unroll
+    for (int a = 0; a < T2; ++a)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sB2[a][r] = rowsum16(sB2[a][r]);
+#pragma unroll
+    for (int a = 0; a < T3; ++a)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sB3[a][r] = rowsum16(sB3[a][r]);
     f4 acc[C::NACC / 4];
     {
         int k = 0;
@@ -459,58 +595,36 @@ fvp_mlp3_kernel(const f4 *__restrict__ obs4, int n, int ntiles, const float *__r
         for (int a = 0; a < T3; ++a) acc[k++] = sB3[a];
     }
     f4 *red = reinterpret_cast<f4 *>(lds);
+    f4 part[C::EPT];
 #pragma unroll
-    for (int h = C::WAVES / 2; h >= 1; h >>= 1) {
+    for (int j = 0; j < C::EPT; ++j) part[j] = zero4;
+#pragma unroll
+    for (int w0 = 0; w0 < C::WAVES; w0 += C::RW) {
         __syncthreads();
-        if (wave >= h && wave < 2 * h) {
+        if (wave >= w0 && wave < w0 + C::RW) {
 #pragma unroll
-            for (int k = 0; k < C::NACC / 4; ++k) red[((wave - h) * (C::NACC / 4) + k) * 64 + lane] = acc[k];
+            for (int k = 0; k < C::NACC / 4; ++k) red[(wave - w0) * (C::SLAB / 4) + k * 64 + lane] = acc[k];
         }
         __syncthreads();
-        if (wave < h) {
 #pragma unroll
-            for (int k = 0; k < C::NACC / 4; ++k) acc[k] += red[(wave * (C::NACC / 4) + k) * 64 + lane];
-        }
-    }
-    if (wave != 0) return;
-
-    // ---- wave 0 writes the block's partial sums in natural parameter order ----
-    float *slab = slabs + (long)blockIdx.x * net.P;
-    int k = 0;
-    const int Ls[4] = {net.L[0], net.L[1], net.L[2], net.L[3]};
-    const int Ts[4] = {T0, T1, T2, T3};
+        for (int j = 0; j < C::EPT; ++j) {
+            const int e = tid + j * C::THREADS;
+            if (e < C::SLAB / 4) {
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const int TI = Ts[i], TO = Ts[i + 1];
-        for (int at = 0; at < TI; ++at)
-            for (int bt = 0; bt < TO; ++bt, ++k) {
-                const int b = 16 * bt + c;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int a = 16 * at + 4 * g + r;
-                    if (a < Ls[i] && b < Ls[i + 1]) slab[net.woff[i] + a * Ls[i + 1] + b] = acc[k][r];
-                }
-            }
-    }
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const int TO = Ts[i + 1];
-        for (int t = 0; t < TO; ++t, ++k) {
-            f4 s = acc[k];
-            // sum over the 16 sample columns (lanes with equal g), fixed butterfly
-#pragma unroll
-            for (int off = 1; off < 16; off <<= 1)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) s[r] += __shfl_xor(s[r], off, 64);
-            if (c == 0) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int b = 16 * t + 4 * g + r;
-                    if (b < Ls[i + 1]) slab[net.boff[i] + b] = s[r];
-                }
+                for (int w = 0; w < C::RW; ++w) part[j] += red[w * (C::SLAB / 4) + e];
             }
         }
     }
+    STAMP(5);
+    {
+        f4 *slab4 = reinterpret_cast<f4 *>(slabs + (long)blockIdx.x * C::SLAB);
+#pragma unroll
+        for (int j = 0; j < C::EPT; ++j) {
+            const int e = tid + j * C::THREADS;
+            if (e < C::SLAB / 4) slab4[e] = part[j];
+        }
+    }
+    STAMP(6);
 }
 
 // ---------------------------------------------------------------------------
@@ -602,32 +716,36 @@ fvp_generic_kernel(const float *__restrict__ obs, int n, const float *__restrict
 // Cross-block reduction (fp64, fixed order) -> zacc[P-A]
 // block = 64 parameters x 16 slab groups
 // ---------------------------------------------------------------------------
+// zacc[imap[j]] = sum over blocks of slabs[b][j], fp64, fixed order; j runs over the slab
+// layout (contiguous, coalesced).  block = 64 slab positions x 16 block groups.
 __global__ void __launch_bounds__(1024)
-reduce_slabs_kernel(const float *__restrict__ slabs, int G, int P, int nw, double *__restrict__ zacc,
-                    const int *__restrict__ skip) {
-    if (*skip) return;
+reduce_slabs_kernel(const float *__restrict__ slabs, int G, int slab, const int *__restrict__ imap,
+                    double *__restrict__ zacc, const int *__restrict__ skip) {
     __shared__ double part[16][64];
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-    const int q = blockIdx.x * 64 + tx;
+    const int j = blockIdx.x * 64 + tx;
+    const int m = j < slab ? imap[j] : -1;
+    if (*skip) return;
     double s = 0.0;
-    if (q < nw) {
-        int b = ty;
-        for (; b + 48 < G; b += 64) {     // 4 independent loads in flight
-            const float v0 = slabs[(long)b * P + q], v1 = slabs[(long)(b + 16) * P + q];
-            const float v2 = slabs[(long)(b + 32) * P + q], v3 = slabs[(long)(b + 48) * P + q];
-            s += (double)v0;
-            s += (double)v1;
-            s += (double)v2;
-            s += (double)v3;
+    if (j < slab) {
+        for (int b0 = 0; b0 < G; b0 += 256) {      // 16 independent loads in flight per chunk
+            float v[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const int b = b0 + ty + 16 * k;
+                v[k] = b < G ? slabs[(long)b * slab + j] : 0.0f;
+            }
+#pragma unroll
+            for (int k = 0; k < 16; ++k) s += (double)v[k];
         }
-        for (; b < G; b += 16) s += (double)slabs[(long)b * P + q];
     }
     part[ty][tx] = s;
     __syncthreads();
-    if (ty == 0 && q < nw) {
+    if (ty == 0 && m >= 0) {
         double t = 0.0;
+#pragma unroll
         for (int k = 0; k < 16; ++k) t += part[k][tx];
-        zacc[q] = t;
+        zacc[m] = t;
     }
 }
 
@@ -655,17 +773,37 @@ __device__ double block_sum(double v, double *sh) {
     return t;
 }
 
+// p -> fragment-order fp32 pack for the next FVP (fast path only; vlen == 0 otherwise)
+__device__ void write_vpack(const double *sp, const int *__restrict__ vmap, float *__restrict__ vpack, int vlen) {
+    for (int e = threadIdx.x; e < vlen; e += blockDim.x) {
+        const int m = vmap[e];
+        vpack[e] = m >= 0 ? (float)sp[m] : 0.0f;
+    }
+}
+
+template <int E>
 __global__ void __launch_bounds__(1024)
 cg_init_kernel(const double *__restrict__ b, double *x, double *r, double *p, int P, Ctl *ctl, double *hist,
-               int maxiter, double resth) {
+               int maxiter, double resth, const int *__restrict__ vmap, float *__restrict__ vpack, int vlen) {
     __shared__ double sh[16];
+    extern __shared__ double sp[];
+    double bv[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int q = threadIdx.x + e * 1024;
+        bv[e] = q < P ? b[q] : 0.0;
+    }
     double s = 0.0;
-    for (int q = threadIdx.x; q < P; q += blockDim.x) {
-        const double bq = b[q];
-        x[q] = 0.0;
-        r[q] = bq;
-        p[q] = bq;
-        s += bq * bq;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int q = threadIdx.x + e * 1024;
+        if (q < P) {
+            x[q] = 0.0;
+            r[q] = bv[e];
+            p[q] = bv[e];
+            if (vlen) sp[q] = bv[e];
+            s += bv[e] * bv[e];
+        }
     }
     const double rr = block_sum(s, sh);
     if (threadIdx.x == 0) {
@@ -677,46 +815,60 @@ cg_init_kernel(const double *__restrict__ b, double *x, double *r, double *p, in
         hist[1] = 0.0;
         ctl->done = (rr < resth || maxiter == 0) ? 1 : 0;
     }
+    write_vpack(sp, vmap, vpack, vlen);    // block_sum's barriers ordered the sp writes
 }
 
+// One CG iteration after z = F p is available as zacc (src/TRPO_CG.c:65-103).  All global
+// loads are issued before the first reduction so the kernel pays one memory round trip.
+template <int E>
 __global__ void __launch_bounds__(1024)
 cg_update_kernel(const double *__restrict__ zacc, double *x, double *r, double *p, int P, int nw, Ctl *ctl,
-                 double *hist) {
+                 double *hist, const int *__restrict__ vmap, float *__restrict__ vpack, int vlen) {
     __shared__ double sh[16];
-    if (ctl->done) return;
-    const double n = ctl->n_total, lam = ctl->damping;
-    constexpr int MAXE = 32;     // per-thread elements kept in registers (P <= 32768)
-    double zr[MAXE];
+    extern __shared__ double sp[];
+    const int done = ctl->done;
+    const double n = ctl->n_total, lam = ctl->damping, rdotr = ctl->rdotr;
+    double pv[E], zv[E], xv[E], rv[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int q = threadIdx.x + e * 1024;
+        const bool in = q < P;
+        pv[e] = in ? p[q] : 0.0;
+        zv[e] = (in && q < nw) ? zacc[q] : 0.0;
+        xv[e] = in ? x[q] : 0.0;
+        rv[e] = in ? r[q] : 0.0;
+    }
+    if (done) return;
     double pz = 0.0;
 #pragma unroll
-    for (int e = 0; e < MAXE; ++e) {
+    for (int e = 0; e < E; ++e) {
         const int q = threadIdx.x + e * 1024;
-        if (q < P) {
-            const double pq = p[q];
-            const double zq = (q < nw ? zacc[q] / n : 2.0 * pq) + lam * pq;
-            zr[e] = zq;
-            pz += pq * zq;
-        }
+        zv[e] = (q < nw ? zv[e] / n : 2.0 * pv[e]) + lam * pv[e];
+        pz += pv[e] * zv[e];
     }
-    const double rdotr = ctl->rdotr;
     const double alpha = rdotr / block_sum(pz, sh);
     double rr = 0.0, xx = 0.0;
 #pragma unroll
-    for (int e = 0; e < MAXE; ++e) {
-        const int q = threadIdx.x + e * 1024;
-        if (q < P) {
-            const double xq = x[q] + alpha * p[q];
-            const double rq = r[q] - alpha * zr[e];
-            x[q] = xq;
-            r[q] = rq;
-            rr += rq * rq;
-            xx += xq * xq;
-        }
+    for (int e = 0; e < E; ++e) {
+        xv[e] += alpha * pv[e];
+        rv[e] -= alpha * zv[e];
+        rr += rv[e] * rv[e];
+        xx += xv[e] * xv[e];
     }
     const double nr = block_sum(rr, sh);
     const double xn = block_sum(xx, sh);
     const double beta = nr / rdotr;
-    for (int q = threadIdx.x; q < P; q += 1024) p[q] = r[q] + beta * p[q];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int q = threadIdx.x + e * 1024;
+        if (q < P) {
+            const double pn = rv[e] + beta * pv[e];
+            x[q] = xv[e];
+            r[q] = rv[e];
+            p[q] = pn;
+            if (vlen) sp[q] = pn;
+        }
+    }
     if (threadIdx.x == 0) {
         const int it = ctl->iter + 1;
         ctl->iter = it;
@@ -725,40 +877,63 @@ cg_update_kernel(const double *__restrict__ zacc, double *x, double *r, double *
         hist[2 * it + 1] = sqrt(xn);
         ctl->done = (nr < ctl->resth || it >= ctl->maxiter) ? 1 : 0;
     }
+    if (vlen) {
+        __syncthreads();
+        write_vpack(sp, vmap, vpack, vlen);
+    }
 }
 
 // ===========================================================================
 // device layer (trpo_dev.h)
 // ===========================================================================
-typedef void (*fast_launch_fn)(dim3, dim3, int, hipStream_t, const f4 *, int, int, const float *, const double *,
-                               const int *, float *, Net, const int *);
+typedef void (*fast_launch_fn)(dim3, dim3, int, hipStream_t, const f4 *, int, int, const float *, const float *,
+                               float *, Net, const int *);
 
-template <int T0, int T1, int T2, int T3>
+template <int T0, int T1, int T2, int T3, int ACT>
 static void fast_launch(dim3 g, dim3 b, int lds, hipStream_t st, const f4 *obs4, int n, int ntiles,
-                        const float *tp, const double *v, const int *vmap, float *slabs, Net net, const int *skip) {
-    hipLaunchKernelGGL((fvp_mlp3_kernel<T0, T1, T2, T3>), g, b, lds, st, obs4, n, ntiles, tp, v, vmap, slabs, net,
+                        const float *tp, const float *vp, float *slabs, Net net, const int *skip) {
+    hipLaunchKernelGGL((fvp_mlp3_kernel<T0, T1, T2, T3, ACT>), g, b, lds, st, obs4, n, ntiles, tp, vp, slabs, net,
                        skip);
 }
-template <int T0, int T1, int T2, int T3>
+
+// CG kernels are templated on the per-thread element count E = ceil(P / 1024)
+static int cg_E(int P) {
+    const int e = (P + 1023) / 1024;
+    return e <= 1 ? 1 : e <= 2 ? 2 : e <= 4 ? 4 : e <= 8 ? 8 : e <= 16 ? 16 : 32;
+}
+#define CG_DISPATCH(E, KERNEL, ...)                                                   \
+    switch (E) {                                                                      \
+    case 1: hipLaunchKernelGGL(KERNEL<1>, __VA_ARGS__); break;                        \
+    case 2: hipLaunchKernelGGL(KERNEL<2>, __VA_ARGS__); break;                        \
+    case 4: hipLaunchKernelGGL(KERNEL<4>, __VA_ARGS__); break;                        \
+    case 8: hipLaunchKernelGGL(KERNEL<8>, __VA_ARGS__); break;                        \
+    case 16: hipLaunchKernelGGL(KERNEL<16>, __VA_ARGS__); break;                      \
+    default: hipLaunchKernelGGL(KERNEL<32>, __VA_ARGS__); break;                      \
+    }
+template <int T0, int T1, int T2, int T3, int ACT>
 static hipError_t fast_attr(int lds) {
-    return hipFuncSetAttribute((const void *)fvp_mlp3_kernel<T0, T1, T2, T3>,
+    return hipFuncSetAttribute((const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 }
 
 struct FastEntry {
     int T[4];
+    int act;                     // -1: run-time activations
     fast_launch_fn launch;
     hipError_t (*attr)(int);
-    int lds, tlen, vlen;
+    int lds, tlen, vlen, slab;
 };
 
-#define FAST_ENTRY(a, b, c, d)                                                                         \
-    {{a, b, c, d}, fast_launch<a, b, c, d>, fast_attr<a, b, c, d>, FastCfg<a, b, c, d>::lds_bytes(),  \
-     FastCfg<a, b, c, d>::TLEN, FastCfg<a, b, c, d>::VLEN}
+#define ACT_TTL (ACT_T | (ACT_T << 2) | (ACT_L << 4))
+#define FAST_ENTRY(a, b, c, d, act)                                                                               \
+    {{a, b, c, d}, act, fast_launch<a, b, c, d, act>, fast_attr<a, b, c, d, act>,                                 \
+     FastCfg<a, b, c, d>::lds_bytes(), FastCfg<a, b, c, d>::TLEN, FastCfg<a, b, c, d>::VLEN,                      \
+     FastCfg<a, b, c, d>::SLAB}
+#define FAST_SHAPE(a, b, c, d) FAST_ENTRY(a, b, c, d, ACT_TTL), FAST_ENTRY(a, b, c, d, -1)
 
 static const FastEntry kFast[] = {
-    FAST_ENTRY(1, 1, 1, 1), FAST_ENTRY(1, 2, 2, 1), FAST_ENTRY(1, 4, 4, 1),
-    FAST_ENTRY(2, 1, 1, 1), FAST_ENTRY(2, 2, 2, 1), FAST_ENTRY(2, 4, 4, 1),
+    FAST_SHAPE(1, 1, 1, 1), FAST_SHAPE(1, 2, 2, 1), FAST_SHAPE(1, 4, 4, 1),
+    FAST_SHAPE(2, 1, 1, 1), FAST_SHAPE(2, 2, 2, 1), FAST_SHAPE(2, 4, 4, 1),
 };
 
 struct trpo_dev {
@@ -769,8 +944,10 @@ struct trpo_dev {
     // fast path
     const FastEntry *fast;
     Pack pack;
-    float *tpack;
+    float *tpack, *vpack;
     int *tmap, *vmap;
+    int *imap;                  // slab position -> natural parameter (reduce kernel)
+    int slab;                   // floats per block partial
     f4 *obs4;
     // generic path
     float *th32, *v32, *iv32, *obs32, *scratch;
@@ -885,13 +1062,14 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
         int T[4];
         for (int i = 0; i < 4; ++i) T[i] = cdiv(n.L[i], 16);
         const FastEntry *best = NULL;
+        const int act = n.act[1] | (n.act[2] << 2) | (n.act[3] << 4);
         for (const FastEntry &f : kFast) {
-            bool ok = true;
+            bool ok = f.act < 0 || f.act == act;
             for (int i = 0; i < 4; ++i) ok = ok && f.T[i] >= T[i];
             if (!ok) continue;
             int cost = f.T[0] * f.T[1] + f.T[1] * f.T[2] + f.T[2] * f.T[3];
             int bcost = best ? best->T[0] * best->T[1] + best->T[1] * best->T[2] + best->T[2] * best->T[3] : 1 << 30;
-            if (cost < bcost) best = &f;
+            if (cost < bcost || (cost == bcost && best && best->act < 0 && f.act >= 0)) best = &f;
         }
         d->fast = best;
     }
@@ -936,12 +1114,18 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
         pk.vlen = pk.vb[2] + 16 * T[3];
         if (pk.tlen != d->fast->tlen || pk.vlen != d->fast->vlen) FAIL("internal: pack layout mismatch");
         DMALLOC(d->tpack, sizeof(float) * pk.tlen);
+        DMALLOC(d->vpack, sizeof(float) * pk.vlen);
         DMALLOC(d->tmap, sizeof(int) * pk.tlen);
         DMALLOC(d->vmap, sizeof(int) * pk.vlen);
         const int len = pk.tlen > pk.vlen ? pk.tlen : pk.vlen;
         hipLaunchKernelGGL(build_maps_kernel, dim3(cdiv(len, 256)), dim3(256), 0, d->stream, n, pk, d->tmap, d->vmap);
         if (d->fast->attr(d->fast->lds) != hipSuccess) FAIL("hipFuncSetAttribute(LDS=%d) failed", d->fast->lds);
-        snprintf(d->name, sizeof d->name, "mfma-mlp3 %dx%dx%dx%d", T[0], T[1], T[2], T[3]);
+        d->slab = d->fast->slab;
+        DMALLOC(d->imap, sizeof(int) * d->slab);
+        hipLaunchKernelGGL(build_imap_kernel, dim3(cdiv(d->slab, 256)), dim3(256), 0, d->stream, n, pk, d->imap,
+                           d->slab);
+        snprintf(d->name, sizeof d->name, "mfma-mlp3 %dx%dx%dx%d%s", T[0], T[1], T[2], T[3],
+                 d->fast->act >= 0 ? " ttl" : "");
     } else {
         DMALLOC(d->th32, sizeof(float) * d->P);
         DMALLOC(d->v32, sizeof(float) * d->P);
@@ -949,6 +1133,9 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
         int rows = 0;
         for (int i = 0; i < n.nl; ++i) rows += n.L[i];
         d->srows = rows;
+        d->slab = d->P;
+        DMALLOC(d->imap, sizeof(int) * d->slab);
+        hipLaunchKernelGGL(iota_kernel, dim3(cdiv(d->slab, 256)), dim3(256), 0, d->stream, d->imap, d->slab, d->nw);
         snprintf(d->name, sizeof d->name, "generic");
     }
     if (hipStreamSynchronize(d->stream) != hipSuccess) FAIL("initialisation kernels failed");
@@ -970,7 +1157,7 @@ extern "C" void trpo_dev_destroy(trpo_dev *d) {
     if (d->stream) hipStreamSynchronize(d->stream);
     if (d->cg_exec) hipGraphExecDestroy(d->cg_exec);
     if (d->comm) ncclCommDestroy(d->comm);
-    void *ptrs[] = {d->tpack, d->tmap, d->vmap, d->obs4, d->th32, d->v32, d->iv32, d->obs32, d->scratch,
+    void *ptrs[] = {d->imap, d->tpack, d->vpack, d->tmap, d->vmap, d->obs4, d->th32, d->v32, d->iv32, d->obs32, d->scratch,
                     d->theta64, d->std64, d->r, d->zacc, d->slabs, d->ctl, d->hist};
     for (void *p : ptrs)
         if (p) hipFree(p);
@@ -1091,8 +1278,8 @@ extern "C" int trpo_dev_set_obs(trpo_dev *d, const double *obs, size_t n) {
     }
     if (d->grid > d->slab_blocks) {
         if (d->slabs) hipFree(d->slabs);
-        HCHK(hipMalloc((void **)&d->slabs, sizeof(float) * (size_t)d->P * d->grid));
-        HCHK(hipMemsetAsync(d->slabs, 0, sizeof(float) * (size_t)d->P * d->grid, d->stream));
+        HCHK(hipMalloc((void **)&d->slabs, sizeof(float) * (size_t)d->slab * d->grid));
+        HCHK(hipMemsetAsync(d->slabs, 0, sizeof(float) * (size_t)d->slab * d->grid, d->stream));
         d->slab_blocks = d->grid;
     }
     HCHK(hipGetLastError());
@@ -1173,9 +1360,10 @@ static int enqueue_fvp_core(trpo_dev *d, const double *src, const int *skip) {
     if (d->n == 0) {
         HCHK(hipMemsetAsync(d->zacc, 0, sizeof(double) * d->P, d->stream));
     } else if (d->fast) {
+        // src has already been packed into d->vpack (by the caller or the CG kernels)
         const int ntiles = cdiv((long)d->n, 16);
-        d->fast->launch(dim3(d->grid), dim3(512), d->fast->lds, d->stream, d->obs4, (int)d->n, ntiles, d->tpack, src,
-                        d->vmap, d->slabs, n, skip);
+        d->fast->launch(dim3(d->grid), dim3(512), d->fast->lds, d->stream, d->obs4, (int)d->n, ntiles, d->tpack,
+                        d->vpack, d->slabs, n, skip);
         HCHK(hipGetLastError());
     } else {
         hipLaunchKernelGGL(to_f32_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, d->v32, src, d->P);
@@ -1184,8 +1372,8 @@ static int enqueue_fvp_core(trpo_dev *d, const double *src, const int *skip) {
         HCHK(hipGetLastError());
     }
     if (d->n) {
-        hipLaunchKernelGGL(reduce_slabs_kernel, dim3(cdiv(d->nw, 64)), dim3(1024), 0, d->stream, d->slabs, d->grid,
-                           d->P, d->nw, d->zacc, skip);
+        hipLaunchKernelGGL(reduce_slabs_kernel, dim3(cdiv(d->slab, 64)), dim3(1024), 0, d->stream, d->slabs, d->grid,
+                           d->slab, d->imap, d->zacc, skip);
         HCHK(hipGetLastError());
     }
     if (d->comm) {
@@ -1198,6 +1386,9 @@ extern "C" int trpo_dev_fvp(trpo_dev *d) {
     if (!d) return -1;
     if (d->n_total <= 0) return -1;
     HCHK(hipSetDevice(d->device));
+    if (d->fast)
+        hipLaunchKernelGGL(gather_pack_kernel, dim3(cdiv(d->pack.vlen, 256)), dim3(256), 0, d->stream, d->vpack,
+                           d->vec[TRPO_VEC_V], d->vmap, d->pack.vlen);
     int rc = enqueue_fvp_core(d, d->vec[TRPO_VEC_V], &d->ctl->zero);
     if (rc) return rc;
     hipLaunchKernelGGL(fvp_epilogue_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, d->zacc,
@@ -1212,7 +1403,7 @@ extern "C" int trpo_dev_fvp_kernel(trpo_dev *d) {
     if (d->fast) {
         const int ntiles = cdiv((long)d->n, 16);
         d->fast->launch(dim3(d->grid), dim3(512), d->fast->lds, d->stream, d->obs4, (int)d->n, ntiles, d->tpack,
-                        d->vec[TRPO_VEC_V], d->vmap, d->slabs, d->net, &d->ctl->zero);
+                        d->vpack, d->slabs, d->net, &d->ctl->zero);
     } else {
         hipLaunchKernelGGL(fvp_generic_kernel, dim3(d->grid), dim3(GEN_T), 0, d->stream, d->obs32, (int)d->n,
                            d->th32, d->v32, d->iv32, d->scratch, d->srows, d->slabs, d->net, &d->ctl->zero);
@@ -1236,13 +1427,16 @@ static int ensure_hist(trpo_dev *d, size_t maxiter) {
 
 static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
     double *x = d->vec[TRPO_VEC_X], *p = d->vec[TRPO_VEC_P], *b = d->vec[TRPO_VEC_B];
-    hipLaunchKernelGGL(cg_init_kernel, dim3(1), dim3(1024), 0, d->stream, b, x, d->r, p, d->P, d->ctl, d->hist,
-                       (int)maxiter, resth);
+    const int E = cg_E(d->P);
+    const int vlen = d->fast ? d->pack.vlen : 0;
+    const size_t shm = d->fast ? sizeof(double) * d->P : 0;
+    CG_DISPATCH(E, cg_init_kernel, dim3(1), dim3(1024), shm, d->stream, b, x, d->r, p, d->P, d->ctl, d->hist,
+                (int)maxiter, resth, d->vmap, d->vpack, vlen);
     for (size_t it = 0; it < maxiter; ++it) {
         int rc = enqueue_fvp_core(d, p, &d->ctl->done);
         if (rc) return rc;
-        hipLaunchKernelGGL(cg_update_kernel, dim3(1), dim3(1024), 0, d->stream, d->zacc, x, d->r, p, d->P, d->nw,
-                           d->ctl, d->hist);
+        CG_DISPATCH(E, cg_update_kernel, dim3(1), dim3(1024), shm, d->stream, d->zacc, x, d->r, p, d->P, d->nw,
+                    d->ctl, d->hist, d->vmap, d->vpack, vlen);
     }
     HCHK(hipGetLastError());
     return 0;
@@ -1331,6 +1525,19 @@ extern "C" double trpo_dev_time(trpo_dev *d, int what, int reps, size_t maxiter,
 }
 
 extern "C" const char *trpo_dev_kernel_name(const trpo_dev *d) { return d ? d->name : ""; }
+
+// Diagnostic builds only: copy the per-block phase stamps (100 MHz ticks) to the host.
+extern "C" int trpo_dev_read_stamps(unsigned long long *out, int n) {
+#ifdef TRPO_STAMPS
+    if (n > 1024 * 16) n = 1024 * 16;
+    HCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * n, 0, hipMemcpyDeviceToHost));
+    return n;
+#else
+    (void)out;
+    (void)n;
+    return -1;
+#endif
+}
 
 extern "C" int trpo_dev_geometry(const trpo_dev *d, int *blocks, int *threads, int *lds_bytes) {
     if (!d) return -1;

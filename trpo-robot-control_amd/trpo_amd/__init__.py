@@ -15,7 +15,7 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libtrpo_mi355x.so")
+LIB_PATH = os.environ.get("TRPO_LIB") or os.path.join(PKG_DIR, "lib", "libtrpo_mi355x.so")
 HEADER = os.path.join(os.path.dirname(PKG_DIR), "include", "trpo_mi355x.h")
 
 _lib = None
