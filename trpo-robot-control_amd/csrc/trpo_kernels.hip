@@ -69,6 +69,76 @@ struct Ctl {                   // device-side control block of one context
     int zero;                  // always 0: "never skip" flag for standalone FVPs
 };
 
+struct CgSt {                  // ping-ponged CG scalars (state k = before FVP k)
+    double rdotr;
+    int iter;
+    int pad;
+};
+
+// Arguments of one fused FVP / CG-iteration launch.
+struct IterArgs {
+    const float4 *obs4;
+    int n, ntiles, P, nw;
+    const float *tpack;
+    const float *vpack;           // plain FVP: the packed direction
+    float *slabs;                 // slab epilogue (acc_out == nullptr)
+    double *acc_out;              // atomic epilogue: R_out fp64 replicas of the P-vector
+    int R_out;
+    double *acc_zero;             // buffer zeroed by block 0 (next-but-one accumulation target)
+    int zero_len;
+    const int *imap;              // slab/accumulator position -> natural parameter
+    const int *skip;
+    // fused CG update prologue (update != 0): z = sum(acc_in)/N + lambda p ; one CG step
+    int update;
+    const double *acc_in;
+    int R_in;
+    const double *p_in, *r_in;
+    double *p_out, *r_out, *x;
+    const CgSt *st_in;
+    CgSt *st_out;
+    Ctl *ctl;
+    double *hist;
+    const int *vmap;
+};
+
+// fixed-order block-wide fp64 sum (every thread gets the result)
+
+// fixed-order block-wide fp64 sum (every thread gets the result)
+__device__ double block_sum(double v, double *sh) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    __syncthreads();
+    if (lane == 0) sh[w] = v;
+    __syncthreads();
+    double t = 0.0;
+    for (int k = 0; k < nwv; ++k) t += sh[k];
+    return t;
+}
+
+// two fixed-order block-wide fp64 sums at once (sh: 2 x 16 doubles)
+__device__ void block_sum2(double a, double b, double *sh, double &sa, double &sb) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        a += __shfl_xor(a, off, 64);
+        b += __shfl_xor(b, off, 64);
+    }
+    __syncthreads();
+    if (lane == 0) {
+        sh[w] = a;
+        sh[16 + w] = b;
+    }
+    __syncthreads();
+    double ta = 0.0, tb = 0.0;
+    for (int k = 0; k < nwv; ++k) {
+        ta += sh[k];
+        tb += sh[16 + k];
+    }
+    sa = ta;
+    sb = tb;
+}
+
 // ---------------------------------------------------------------------------
 // activation helpers (reference src/TRPO_FVP.c:810-834 and :866-882)
 // ---------------------------------------------------------------------------
@@ -276,13 +346,22 @@ struct FastCfg {
     // natural parameter order by the reduce kernel (imap)
     static constexpr int NACC = 4 * (T0 * T1 + T1 * T2 + T2 * T3 + T1 + T2 + T3);
     static constexpr int SLAB = NACC * 64;
+    // small nets: weights live in registers and 16 waves per block keep <= 1 tile per wave
+    static constexpr bool REGW = T0 * T1 + T1 * T2 + T2 * T3 <= 3;
     static constexpr int WAVES = 8;
     static constexpr int THREADS = 64 * WAVES;
     static constexpr int MAIN_BYTES = 4 * (TLEN + VLEN + WAVES * SCR);
-    static constexpr int CAP = MAIN_BYTES > 65536 ? MAIN_BYTES : 65536;
+    static constexpr int CAP = MAIN_BYTES > 131072 ? MAIN_BYTES : 131072;
     // waves combined per epilogue round (largest divisor of WAVES whose dumps fit)
-    static constexpr int RW = (8 * SLAB * 4 <= CAP) ? 8 : (4 * SLAB * 4 <= CAP) ? 4 : (2 * SLAB * 4 <= CAP) ? 2 : 1;
+    static constexpr int RW = (WAVES * SLAB * 4 <= CAP) ? WAVES : (8 * SLAB * 4 <= CAP) ? 8 : (4 * SLAB * 4 <= CAP) ? 4
+                              : (2 * SLAB * 4 <= CAP) ? 2 : 1;
     static constexpr int EPT = (SLAB / 4 + THREADS - 1) / THREADS;   // f4 slices per thread in the combine
+    // fused CG update: natural P-vector elements per thread (upper bound from the padded shape)
+    static constexpr int PMAX = 256 * (T0 * T1 + T1 * T2 + T2 * T3) + 16 * (T1 + T2 + 2 * T3);
+    static constexpr int EMAX = (PMAX + THREADS - 1) / THREADS;
+    static constexpr int VEMAX = (VLEN + THREADS - 1) / THREADS;
+    static constexpr int EMAX_REPLICAS = 4;        // atomic-replica reduction only for EMAX <= this
+    static_assert(2 * PMAX <= WAVES * SCR, "fp64 staging of p must fit the tile scratch");
     static int lds_bytes() {
         const int b = 4 * RW * SLAB;
         return MAIN_BYTES > b ? MAIN_BYTES : b;
@@ -313,47 +392,163 @@ __device__ __forceinline__ f4 scr_get(const float *scr, int row0, int c, int g) 
 // ACT >= 0: activations of layers 1..3 fixed at compile time (a1 | a2 << 2 | a3 << 4);
 // ACT == -1: read from net.act at run time (wave-uniform branches).
 template <int T0, int T1, int T2, int T3, int ACT>
-__global__ void __launch_bounds__(512)
-fvp_mlp3_kernel(const f4 *__restrict__ obs4, int n, int ntiles, const float *__restrict__ tpack,
-                const float *__restrict__ vpack, float *__restrict__ slabs, Net net, const int *__restrict__ skip) {
+__global__ void __launch_bounds__((64 * FastCfg<T0, T1, T2, T3>::WAVES))
+fvp_mlp3_kernel(IterArgs A, Net net) {
     using C = FastCfg<T0, T1, T2, T3>;
     (void)net;
     extern __shared__ __attribute__((aligned(16))) float lds[];
+    __shared__ double sh64[32];
     float *tw = lds;                                   // theta pack
     float *vw = lds + C::TLEN;                         // v pack (fragment order, fp32)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int c = lane & 15, g = lane >> 4;
     float *scr = lds + C::TLEN + C::VLEN + wave * C::SCR;
     const int nwaves = gridDim.x * C::WAVES;
+    const int ntiles = A.ntiles, n = A.n;
+    const f4 *obs4 = reinterpret_cast<const f4 *>(A.obs4);
     STAMP(0);
 
-    // ---- prologue: ONE round of global loads (skip flag, both packs, first tile) ----
+    // ---- prologue: ONE round of global loads (flags, theta pack, [v pack | CG state], first tile) ----
+    const bool upd = A.update != 0;
     constexpr int NT4 = C::TLEN / 4, NALL = (C::TLEN + C::VLEN) / 4;
     constexpr int PER = (NALL + C::THREADS - 1) / C::THREADS;
-    const int skipv = *skip;
+    const int skipv = *A.skip;
+    // NOTE: every prologue load is unconditional (indices clamped, values selected after):
+    // a load guarded by a run-time condition makes hipcc branch around it and drain vmcnt,
+    // which serialises the round trips (cdna_hip_programming.md §5 trap (c)).
     f4 st[PER];
     {
-        const f4 *tp4 = reinterpret_cast<const f4 *>(tpack);
-        const f4 *vp4 = reinterpret_cast<const f4 *>(vpack);
+        const f4 *tp4 = reinterpret_cast<const f4 *>(A.tpack);
+        const f4 *vp4 = reinterpret_cast<const f4 *>(A.vpack);
 #pragma unroll
         for (int k = 0; k < PER; ++k) {
-            const int e = tid + k * C::THREADS;
-            if (e < NT4) st[k] = tp4[e];
-            else if (e < NALL) st[k] = vp4[e - NT4];
+            const int e = min(tid + k * C::THREADS, NALL - 1);
+            st[k] = e < NT4 ? tp4[e] : vp4[e - NT4];
         }
     }
     int tile = blockIdx.x * C::WAVES + wave;
     f4 xn[T0];
+    {
+        const int tl = max(0, min(tile, ntiles - 1));
 #pragma unroll
-    for (int kt = 0; kt < T0; ++kt)
-        xn[kt] = tile < ntiles ? obs4[(long)(tile * 16 + c) * (4 * T0) + kt * 4 + g] : f4{0.f, 0.f, 0.f, 0.f};
+        for (int kt = 0; kt < T0; ++kt) xn[kt] = obs4[(long)(tl * 16 + c) * (4 * T0) + kt * 4 + g];
+    }
+    int im[C::EPT][4];
+    {
+        const int *imap = A.acc_out ? A.imap : A.skip;      // any valid pointer when unused
+#pragma unroll
+        for (int j = 0; j < C::EPT; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int e = 4 * (tid + j * C::THREADS) + r;
+                const int v = imap[A.acc_out ? min(e, C::SLAB - 1) : 0];
+                im[j][r] = e < C::SLAB ? v : -1;
+            }
+    }
+    // CG state for the fused update (src/TRPO_CG.c:77-103), loaded in the same round
+    double pv[C::EMAX], rv[C::EMAX], zv[C::EMAX], xv[C::EMAX];
+    int vm[C::VEMAX];
+    CgSt sin = {0.0, 0, 0};
+    double cn = 1.0, clam = 0.0, cth = 0.0;
+    int cmax = 0;
+    if (upd) {
+        sin = *A.st_in;
+        cn = A.ctl->n_total;
+        clam = A.ctl->damping;
+        cth = A.ctl->resth;
+        cmax = A.ctl->maxiter;
+        const double *xs = blockIdx.x == 0 ? A.x : A.p_in;    // only block 0 needs x
+#pragma unroll
+        for (int e = 0; e < C::EMAX; ++e) {
+            const int q = tid + e * C::THREADS, qc = min(q, A.P - 1), qz = min(q, A.nw - 1);
+            const bool in = q < A.P;
+            const double p0 = A.p_in[qc], r0 = A.r_in[qc], x0 = xs[qc];
+            double z = 0.0;
+            if constexpr (C::EMAX <= C::EMAX_REPLICAS) {
+                // up to 8 atomic replicas (small P only: 8 loads per element in flight)
+                double za[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) za[k] = A.acc_in[(long)min(k, A.R_in - 1) * A.P + qz];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) z += k < A.R_in ? za[k] : 0.0;
+            } else {
+                z = A.acc_in[qz];                         // slab mode: one reduced vector
+            }
+            pv[e] = in ? p0 : 0.0;
+            rv[e] = in ? r0 : 0.0;
+            xv[e] = (in && blockIdx.x == 0) ? x0 : 0.0;
+            zv[e] = q < A.nw ? z : 0.0;
+        }
+#pragma unroll
+        for (int e = 0; e < C::VEMAX; ++e) {
+            const int ve = tid + e * C::THREADS;
+            const int v = A.vmap[min(ve, C::VLEN - 1)];
+            vm[e] = ve < C::VLEN ? v : -1;
+        }
+    }
     if (skipv) return;                                 // grid-uniform
     {
         f4 *dst = reinterpret_cast<f4 *>(lds);
 #pragma unroll
         for (int k = 0; k < PER; ++k) {
             const int e = tid + k * C::THREADS;
-            if (e < NALL) dst[e] = st[k];
+            if (e < NT4 || (e < NALL && !upd)) dst[e] = st[k];
+        }
+    }
+    STAMP(7);
+    if (upd) {
+        // every block runs the identical fp64 CG step (fixed-order sums => bitwise-equal
+        // results in all blocks); block 0 publishes the new state
+        double pz = 0.0;
+#pragma unroll
+        for (int e = 0; e < C::EMAX; ++e) {
+            const int q = tid + e * C::THREADS;
+            zv[e] = (q < A.nw ? zv[e] / cn : 2.0 * pv[e]) + clam * pv[e];
+            pz += pv[e] * zv[e];
+        }
+        const double alpha = sin.rdotr / block_sum(pz, sh64);
+        double rr = 0.0, xx = 0.0;
+#pragma unroll
+        for (int e = 0; e < C::EMAX; ++e) {
+            rv[e] -= alpha * zv[e];
+            rr += rv[e] * rv[e];
+            xv[e] += alpha * pv[e];
+            xx += xv[e] * xv[e];
+        }
+        double nr, xn2;
+        block_sum2(rr, xx, sh64, nr, xn2);
+        const double beta = nr / sin.rdotr;
+        double *stage = reinterpret_cast<double *>(lds + C::TLEN + C::VLEN);
+#pragma unroll
+        for (int e = 0; e < C::EMAX; ++e) {
+            const int q = tid + e * C::THREADS;
+            pv[e] = rv[e] + beta * pv[e];
+            if (q < A.P) {
+                stage[q] = pv[e];
+                if (blockIdx.x == 0) {
+                    A.p_out[q] = pv[e];
+                    A.r_out[q] = rv[e];
+                    A.x[q] = xv[e];
+                }
+            }
+        }
+        const int it = sin.iter + 1;
+        const int done = (nr < cth || it >= cmax) ? 1 : 0;
+        if (blockIdx.x == 0 && tid == 0) {
+            A.st_out->rdotr = nr;
+            A.st_out->iter = it;
+            A.hist[2 * it] = nr;
+            A.hist[2 * it + 1] = sqrt(xn2);
+            A.ctl->rdotr = nr;
+            A.ctl->iter = it;
+            A.ctl->done = done;
+        }
+        if (done) return;                              // block-uniform (identical in every block)
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < C::VEMAX; ++e) {
+            const int ve = tid + e * C::THREADS;
+            if (ve < C::VLEN) vw[ve] = vm[e] >= 0 ? (float)stage[vm[e]] : 0.0f;
         }
     }
     __syncthreads();
@@ -367,9 +562,23 @@ fvp_mlp3_kernel(const f4 *__restrict__ obs4, int n, int ntiles, const float *__r
     const f4 *TW = reinterpret_cast<const f4 *>(tw);
     const f4 *VW = reinterpret_cast<const f4 *>(vw);
 
+    const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
+    // small nets: every fragment held in registers across the tile loop (no LDS on the chain)
+    f4 rFA0 = zero4, rVFA0 = zero4, rFA1 = zero4, rVFA1 = zero4, rFA2 = zero4, rVFA2 = zero4, rFB1 = zero4,
+       rFB2 = zero4;
+    if constexpr (C::REGW) {
+        rFA0 = TW[C::FA0 / 4 + lane];
+        rVFA0 = VW[C::VFA0 / 4 + lane];
+        rFA1 = TW[C::FA1 / 4 + lane];
+        rVFA1 = VW[C::VFA1 / 4 + lane];
+        rFA2 = TW[C::FA2 / 4 + lane];
+        rVFA2 = VW[C::VFA2 / 4 + lane];
+        rFB1 = TW[C::FB1 / 4 + lane];
+        rFB2 = TW[C::FB2 / 4 + lane];
+    }
+#define WLD(REG, EXPR) (C::REGW ? (REG) : (EXPR))
     f4 accW0[T0][T1], accW1[T1][T2], accW2[T2][T3];
     f4 sB1[T1], sB2[T2], sB3[T3];
-    const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int a = 0; a < T0; ++a)
 #pragma unroll
@@ -396,9 +605,10 @@ fvp_mlp3_kernel(const f4 *__restrict__ obs4, int n, int ntiles, const float *__r
         f4 x0[T0];
 #pragma unroll
         for (int kt = 0; kt < T0; ++kt) x0[kt] = xn[kt];
-        if (tile + nwaves < ntiles) {
+        {
+            const int tn = min(tile + nwaves, ntiles - 1);     // unconditional prefetch (clamped)
 #pragma unroll
-            for (int kt = 0; kt < T0; ++kt) xn[kt] = obs4[(long)(sample + 16 * nwaves) * (4 * T0) + kt * 4 + g];
+            for (int kt = 0; kt < T0; ++kt) xn[kt] = obs4[(long)(tn * 16 + c) * (4 * T0) + kt * 4 + g];
         }
 
         // ---- layer 0: x1 = W0^T x0 + b0 ; Rx1 = VW0^T x0 + vb0 (Ry0 = 0) ----
@@ -409,8 +619,8 @@ fvp_mlp3_kernel(const f4 *__restrict__ obs4, int n, int ntiles, const float *__r
             f4 ra = VW[C::VB0 / 4 + ot * 4 + g];
 #pragma unroll
             for (int kt = 0; kt < T0; ++kt) {
-                const f4 w = TW[C::FA0 / 4 + (ot * T0 + kt) * 64 + lane];
-                const f4 u = VW[C::VFA0 / 4 + (ot * T0 + kt) * 64 + lane];
+                const f4 w = WLD(rFA0, TW[C::FA0 / 4 + (ot * T0 + kt) * 64 + lane]);
+                const f4 u = WLD(rVFA0, VW[C::VFA0 / 4 + (ot * T0 + kt) * 64 + lane]);
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
                     a = MFMA(w[s], x0[kt][s], a);
@@ -428,8 +638,8 @@ fvp_mlp3_kernel(const f4 *__restrict__ obs4, int n, int ntiles, const float *__r
             f4 rb = zero4;                    // second chain: halves the dependent MFMA depth
 #pragma unroll
             for (int kt = 0; kt < T1; ++kt) {
-                const f4 w = TW[C::FA1 / 4 + (ot * T1 + kt) * 64 + lane];
-                const f4 u = VW[C::VFA1 / 4 + (ot * T1 + kt) * 64 + lane];
+                const f4 w = WLD(rFA1, TW[C::FA1 / 4 + (ot * T1 + kt) * 64 + lane]);
+                const f4 u = WLD(rVFA1, VW[C::VFA1 / 4 + (ot * T1 + kt) * 64 + lane]);
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
                     a = MFMA(w[s], y1[kt][s], a);
@@ -449,8 +659,8 @@ fvp_mlp3_kernel(const f4 *__restrict__ obs4, int n, int ntiles, const float *__r
             f4 rb = zero4;
 #pragma unroll
             for (int kt = 0; kt < T2; ++kt) {
-                const f4 w = TW[C::FA2 / 4 + (ot * T2 + kt) * 64 + lane];
-                const f4 u = VW[C::VFA2 / 4 + (ot * T2 + kt) * 64 + lane];
+                const f4 w = WLD(rFA2, TW[C::FA2 / 4 + (ot * T2 + kt) * 64 + lane]);
+                const f4 u = WLD(rVFA2, VW[C::VFA2 / 4 + (ot * T2 + kt) * 64 + lane]);
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
                     if (y3_needed) a = MFMA(w[s], y2[kt][s], a);
@@ -491,7 +701,7 @@ fvp_mlp3_kernel(const f4 *__restrict__ obs4, int n, int ntiles, const float *__r
             f4 a = zero4;
 #pragma unroll
             for (int kt = 0; kt < T3; ++kt) {
-                const f4 w = TW[C::FB2 / 4 + (it * T3 + kt) * 64 + lane];
+                const f4 w = WLD(rFB2, TW[C::FB2 / 4 + (it * T3 + kt) * 64 + lane]);
 #pragma unroll
                 for (int s = 0; s < 4; ++s) a = MFMA(w[s], g3[kt][s], a);
             }
@@ -523,7 +733,7 @@ fvp_mlp3_kernel(const f4 *__restrict__ obs4, int n, int ntiles, const float *__r
             f4 a = zero4;
 #pragma unroll
             for (int kt = 0; kt < T2; ++kt) {
-                const f4 w = TW[C::FB1 / 4 + (it * T2 + kt) * 64 + lane];
+                const f4 w = WLD(rFB1, TW[C::FB1 / 4 + (it * T2 + kt) * 64 + lane]);
 #pragma unroll
                 for (int s = 0; s < 4; ++s) a = MFMA(w[s], g2[kt][s], a);
             }
@@ -616,8 +826,19 @@ fvp_mlp3_kernel(const f4 *__restrict__ obs4, int n, int ntiles, const float *__r
         }
     }
     STAMP(5);
-    {
-        f4 *slab4 = reinterpret_cast<f4 *>(slabs + (long)blockIdx.x * C::SLAB);
+    if (A.acc_out) {
+        // cross-block sum by fp64 atomics into R replicas: the fp32 block partials are added
+        // exactly unless their exponents span > 29 bits, so the order cannot matter in practice
+        double *dst = A.acc_out + (long)(blockIdx.x % A.R_out) * A.P;
+#pragma unroll
+        for (int j = 0; j < C::EPT; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (im[j][r] >= 0) unsafeAtomicAdd(dst + im[j][r], (double)part[j][r]);
+        if (blockIdx.x == 0)
+            for (int e = tid; e < A.zero_len; e += C::THREADS) A.acc_zero[e] = 0.0;
+    } else {
+        f4 *slab4 = reinterpret_cast<f4 *>(A.slabs + (long)blockIdx.x * C::SLAB);
 #pragma unroll
         for (int j = 0; j < C::EPT; ++j) {
             const int e = tid + j * C::THREADS;
@@ -625,6 +846,7 @@ fvp_mlp3_kernel(const f4 *__restrict__ obs4, int n, int ntiles, const float *__r
         }
     }
     STAMP(6);
+#undef WLD
 }
 
 // ---------------------------------------------------------------------------
@@ -761,17 +983,6 @@ __global__ void fvp_epilogue_kernel(const double *__restrict__ zacc, const doubl
 // ---------------------------------------------------------------------------
 // CG (src/TRPO_CG.c:11-113), one 1024-thread block, all fp64, fixed-order sums
 // ---------------------------------------------------------------------------
-__device__ double block_sum(double v, double *sh) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nwv = blockDim.x >> 6;
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-    __syncthreads();
-    if (lane == 0) sh[w] = v;
-    __syncthreads();
-    double t = 0.0;
-    for (int k = 0; k < nwv; ++k) t += sh[k];
-    return t;
-}
 
 // p -> fragment-order fp32 pack for the next FVP (fast path only; vlen == 0 otherwise)
 __device__ void write_vpack(const double *sp, const int *__restrict__ vmap, float *__restrict__ vpack, int vlen) {
@@ -781,10 +992,12 @@ __device__ void write_vpack(const double *sp, const int *__restrict__ vmap, floa
     }
 }
 
+// x = 0, r = p = b, state 0; packs p for the first FVP; zeroes the first atomic target.
 template <int E>
 __global__ void __launch_bounds__(1024)
-cg_init_kernel(const double *__restrict__ b, double *x, double *r, double *p, int P, Ctl *ctl, double *hist,
-               int maxiter, double resth, const int *__restrict__ vmap, float *__restrict__ vpack, int vlen) {
+cg_init_kernel(const double *__restrict__ b, double *x, double *r, double *p, int P, Ctl *ctl, CgSt *st,
+               double *hist, int maxiter, double resth, const int *__restrict__ vmap, float *__restrict__ vpack,
+               int vlen, double *acc_zero, int zero_len) {
     __shared__ double sh[16];
     extern __shared__ double sp[];
     double bv[E];
@@ -793,6 +1006,7 @@ cg_init_kernel(const double *__restrict__ b, double *x, double *r, double *p, in
         const int q = threadIdx.x + e * 1024;
         bv[e] = q < P ? b[q] : 0.0;
     }
+    for (int e = threadIdx.x; e < zero_len; e += 1024) acc_zero[e] = 0.0;
     double s = 0.0;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -811,6 +1025,8 @@ cg_init_kernel(const double *__restrict__ b, double *x, double *r, double *p, in
         ctl->resth = resth;
         ctl->rdotr = rr;
         ctl->iter = 0;
+        st->rdotr = rr;
+        st->iter = 0;
         hist[0] = rr;
         hist[1] = 0.0;
         ctl->done = (rr < resth || maxiter == 0) ? 1 : 0;
@@ -818,25 +1034,32 @@ cg_init_kernel(const double *__restrict__ b, double *x, double *r, double *p, in
     write_vpack(sp, vmap, vpack, vlen);    // block_sum's barriers ordered the sp writes
 }
 
-// One CG iteration after z = F p is available as zacc (src/TRPO_CG.c:65-103).  All global
-// loads are issued before the first reduction so the kernel pays one memory round trip.
+// One CG step after z = F p is available as R_in fp64 partial-sum replicas (src/TRPO_CG.c:65-103):
+// used after the last FVP of a solve, and for every step of the generic (non-fused) path.
+// All global loads are issued before the first reduction.
 template <int E>
 __global__ void __launch_bounds__(1024)
-cg_update_kernel(const double *__restrict__ zacc, double *x, double *r, double *p, int P, int nw, Ctl *ctl,
-                 double *hist, const int *__restrict__ vmap, float *__restrict__ vpack, int vlen) {
+cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restrict__ p_in,
+                 const double *__restrict__ r_in, double *p_out, double *r_out, double *x, int P, int nw, Ctl *ctl,
+                 const CgSt *st_in, CgSt *st_out, double *hist) {
     __shared__ double sh[16];
-    extern __shared__ double sp[];
     const int done = ctl->done;
-    const double n = ctl->n_total, lam = ctl->damping, rdotr = ctl->rdotr;
+    const double n = ctl->n_total, lam = ctl->damping, th = ctl->resth;
+    const int maxiter = ctl->maxiter;
+    const CgSt sin = *st_in;
     double pv[E], zv[E], xv[E], rv[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const int q = threadIdx.x + e * 1024;
         const bool in = q < P;
-        pv[e] = in ? p[q] : 0.0;
-        zv[e] = (in && q < nw) ? zacc[q] : 0.0;
+        pv[e] = in ? p_in[q] : 0.0;
         xv[e] = in ? x[q] : 0.0;
-        rv[e] = in ? r[q] : 0.0;
+        rv[e] = in ? r_in[q] : 0.0;
+        double z = 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (k < R_in && q < nw) z += acc[(long)k * P + q];
+        zv[e] = z;
     }
     if (done) return;
     double pz = 0.0;
@@ -846,7 +1069,7 @@ cg_update_kernel(const double *__restrict__ zacc, double *x, double *r, double *
         zv[e] = (q < nw ? zv[e] / n : 2.0 * pv[e]) + lam * pv[e];
         pz += pv[e] * zv[e];
     }
-    const double alpha = rdotr / block_sum(pz, sh);
+    const double alpha = sin.rdotr / block_sum(pz, sh);
     double rr = 0.0, xx = 0.0;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -857,43 +1080,37 @@ cg_update_kernel(const double *__restrict__ zacc, double *x, double *r, double *
     }
     const double nr = block_sum(rr, sh);
     const double xn = block_sum(xx, sh);
-    const double beta = nr / rdotr;
+    const double beta = nr / sin.rdotr;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const int q = threadIdx.x + e * 1024;
         if (q < P) {
-            const double pn = rv[e] + beta * pv[e];
             x[q] = xv[e];
-            r[q] = rv[e];
-            p[q] = pn;
-            if (vlen) sp[q] = pn;
+            r_out[q] = rv[e];
+            p_out[q] = rv[e] + beta * pv[e];
         }
     }
     if (threadIdx.x == 0) {
-        const int it = ctl->iter + 1;
+        const int it = sin.iter + 1;
+        st_out->rdotr = nr;
+        st_out->iter = it;
         ctl->iter = it;
         ctl->rdotr = nr;
         hist[2 * it] = nr;
         hist[2 * it + 1] = sqrt(xn);
-        ctl->done = (nr < ctl->resth || it >= ctl->maxiter) ? 1 : 0;
-    }
-    if (vlen) {
-        __syncthreads();
-        write_vpack(sp, vmap, vpack, vlen);
+        ctl->done = (nr < th || it >= maxiter) ? 1 : 0;
     }
 }
 
 // ===========================================================================
 // device layer (trpo_dev.h)
 // ===========================================================================
-typedef void (*fast_launch_fn)(dim3, dim3, int, hipStream_t, const f4 *, int, int, const float *, const float *,
-                               float *, Net, const int *);
+typedef void (*fast_launch_fn)(dim3, int, hipStream_t, const IterArgs &, const Net &);
 
 template <int T0, int T1, int T2, int T3, int ACT>
-static void fast_launch(dim3 g, dim3 b, int lds, hipStream_t st, const f4 *obs4, int n, int ntiles,
-                        const float *tp, const float *vp, float *slabs, Net net, const int *skip) {
-    hipLaunchKernelGGL((fvp_mlp3_kernel<T0, T1, T2, T3, ACT>), g, b, lds, st, obs4, n, ntiles, tp, vp, slabs, net,
-                       skip);
+static void fast_launch(dim3 g, int lds, hipStream_t st, const IterArgs &a, const Net &net) {
+    hipLaunchKernelGGL((fvp_mlp3_kernel<T0, T1, T2, T3, ACT>), g, dim3(64 * FastCfg<T0, T1, T2, T3>::WAVES), lds,
+                       st, a, net);
 }
 
 // CG kernels are templated on the per-thread element count E = ceil(P / 1024)
@@ -921,14 +1138,14 @@ struct FastEntry {
     int act;                     // -1: run-time activations
     fast_launch_fn launch;
     hipError_t (*attr)(int);
-    int lds, tlen, vlen, slab;
+    int lds, tlen, vlen, slab, emax, waves;
 };
 
 #define ACT_TTL (ACT_T | (ACT_T << 2) | (ACT_L << 4))
 #define FAST_ENTRY(a, b, c, d, act)                                                                               \
     {{a, b, c, d}, act, fast_launch<a, b, c, d, act>, fast_attr<a, b, c, d, act>,                                 \
      FastCfg<a, b, c, d>::lds_bytes(), FastCfg<a, b, c, d>::TLEN, FastCfg<a, b, c, d>::VLEN,                      \
-     FastCfg<a, b, c, d>::SLAB}
+     FastCfg<a, b, c, d>::SLAB, FastCfg<a, b, c, d>::EMAX, FastCfg<a, b, c, d>::WAVES}
 #define FAST_SHAPE(a, b, c, d) FAST_ENTRY(a, b, c, d, ACT_TTL), FAST_ENTRY(a, b, c, d, -1)
 
 static const FastEntry kFast[] = {
@@ -958,6 +1175,10 @@ struct trpo_dev {
     double *std64;
     double *vec[5];             // V, Z, X, B, P
     double *r, *zacc;
+    double *pbuf[2], *rbuf[2];  // ping-ponged CG direction / residual
+    CgSt *st;                   // 2 ping-ponged CG scalar states
+    double *accbuf;             // atomic mode: 3 x R fp64 replicas of the P-vector
+    int atomic, R;
     float *slabs;
     int slab_blocks;            // capacity
     int grid;                   // FVP blocks for the current n
@@ -1090,6 +1311,13 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
     DMALLOC(d->r, sizeof(double) * d->P);
     DMALLOC(d->zacc, sizeof(double) * d->P);
     DMALLOC(d->ctl, sizeof(Ctl));
+    DMALLOC(d->st, 2 * sizeof(CgSt));
+    for (int i = 0; i < 2; ++i) {
+        DMALLOC(d->pbuf[i], sizeof(double) * d->P);
+        DMALLOC(d->rbuf[i], sizeof(double) * d->P);
+    }
+    d->R = 8;
+    DMALLOC(d->accbuf, sizeof(double) * 3 * d->R * d->P);
     if (d->fast) {
         Pack &pk = d->pack;
         for (int i = 0; i < 4; ++i) pk.T[i] = d->fast->T[i];
@@ -1157,7 +1385,7 @@ extern "C" void trpo_dev_destroy(trpo_dev *d) {
     if (d->stream) hipStreamSynchronize(d->stream);
     if (d->cg_exec) hipGraphExecDestroy(d->cg_exec);
     if (d->comm) ncclCommDestroy(d->comm);
-    void *ptrs[] = {d->imap, d->tpack, d->vpack, d->tmap, d->vmap, d->obs4, d->th32, d->v32, d->iv32, d->obs32, d->scratch,
+    void *ptrs[] = {d->st, d->pbuf[0], d->pbuf[1], d->rbuf[0], d->rbuf[1], d->accbuf, d->imap, d->tpack, d->vpack, d->tmap, d->vmap, d->obs4, d->th32, d->v32, d->iv32, d->obs32, d->scratch,
                     d->theta64, d->std64, d->r, d->zacc, d->slabs, d->ctl, d->hist};
     for (void *p : ptrs)
         if (p) hipFree(p);
@@ -1218,6 +1446,16 @@ extern "C" int trpo_dev_set_std(trpo_dev *d, const double *stdv) {
     return 0;
 }
 
+static void choose_reduction(trpo_dev *d) {
+    // fused single-kernel CG iterations with fp64 atomics when the block partials are small
+    // (G x P values per FVP); otherwise block slabs + a reduce kernel
+    // decided from P only, so every rank of a sharded run picks the same collective pattern
+    const char *e = getenv("TRPO_ATOMIC");
+    const bool ok = d->fast && d->fast->emax <= 4 && d->P <= 2048;
+    d->atomic = ok && 256L * d->P <= 400000;
+    if (e) d->atomic = ok && atoi(e) != 0;
+}
+
 static int choose_grid(trpo_dev *d) {
     // one 8-wave block per CU at most; at least one tile per wave
     int cus = 256;
@@ -1227,7 +1465,7 @@ static int choose_grid(trpo_dev *d) {
     const char *e = getenv("TRPO_FVP_BLOCKS");
     if (d->fast) {
         const int ntiles = cdiv((long)d->n, 16);
-        int g = cdiv(ntiles, 8);
+        int g = cdiv(ntiles, d->fast->waves);
         if (g > cus) g = cus;
         if (e && atoi(e) > 0) g = atoi(e);
         return g < 1 ? 1 : g;
@@ -1251,6 +1489,7 @@ extern "C" int trpo_dev_set_obs(trpo_dev *d, const double *obs, size_t n) {
     }
     d->n = n;
     d->grid = choose_grid(d);
+    choose_reduction(d);
     if (d->fast) {
         const size_t npad = (size_t)cdiv((long)n, 16) * 16 + 16;
         const int ld = 16 * d->pack.T[0];
@@ -1354,16 +1593,31 @@ extern "C" int trpo_dev_download(trpo_dev *d, int slot, double *host) {
     return 0;
 }
 
+static IterArgs plain_args(trpo_dev *d, const int *skip) {
+    IterArgs a;
+    memset(&a, 0, sizeof a);
+    a.obs4 = reinterpret_cast<const float4 *>(d->obs4);
+    a.n = (int)d->n;
+    a.ntiles = cdiv((long)d->n, 16);
+    a.P = d->P;
+    a.nw = d->nw;
+    a.tpack = d->tpack;
+    a.vpack = d->vpack;
+    a.slabs = d->slabs;
+    a.imap = d->imap;
+    a.skip = skip;
+    a.R_out = 1;
+    a.R_in = 1;
+    return a;
+}
+
 // enqueue: partial sums of F*src into d->zacc (global over ranks)
 static int enqueue_fvp_core(trpo_dev *d, const double *src, const int *skip) {
     const Net &n = d->net;
-    if (d->n == 0) {
-        HCHK(hipMemsetAsync(d->zacc, 0, sizeof(double) * d->P, d->stream));
-    } else if (d->fast) {
+    if (d->fast) {
         // src has already been packed into d->vpack (by the caller or the CG kernels)
-        const int ntiles = cdiv((long)d->n, 16);
-        d->fast->launch(dim3(d->grid), dim3(512), d->fast->lds, d->stream, d->obs4, (int)d->n, ntiles, d->tpack,
-                        d->vpack, d->slabs, n, skip);
+        IterArgs a = plain_args(d, skip);
+        d->fast->launch(dim3(d->grid), d->fast->lds, d->stream, a, n);
         HCHK(hipGetLastError());
     } else {
         hipLaunchKernelGGL(to_f32_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, d->v32, src, d->P);
@@ -1371,11 +1625,9 @@ static int enqueue_fvp_core(trpo_dev *d, const double *src, const int *skip) {
                            d->th32, d->v32, d->iv32, d->scratch, d->srows, d->slabs, n, skip);
         HCHK(hipGetLastError());
     }
-    if (d->n) {
-        hipLaunchKernelGGL(reduce_slabs_kernel, dim3(cdiv(d->slab, 64)), dim3(1024), 0, d->stream, d->slabs, d->grid,
-                           d->slab, d->imap, d->zacc, skip);
-        HCHK(hipGetLastError());
-    }
+    hipLaunchKernelGGL(reduce_slabs_kernel, dim3(cdiv(d->slab, 64)), dim3(1024), 0, d->stream, d->slabs, d->grid,
+                       d->slab, d->imap, d->zacc, skip);
+    HCHK(hipGetLastError());
     if (d->comm) {
         if (ncclAllReduce(d->zacc, d->zacc, d->nw, ncclFloat64, ncclSum, d->comm, d->stream) != ncclSuccess) return -4;
     }
@@ -1401,9 +1653,8 @@ extern "C" int trpo_dev_fvp_kernel(trpo_dev *d) {
     if (!d || d->n == 0) return -1;
     HCHK(hipSetDevice(d->device));
     if (d->fast) {
-        const int ntiles = cdiv((long)d->n, 16);
-        d->fast->launch(dim3(d->grid), dim3(512), d->fast->lds, d->stream, d->obs4, (int)d->n, ntiles, d->tpack,
-                        d->vpack, d->slabs, d->net, &d->ctl->zero);
+        IterArgs a = plain_args(d, &d->ctl->zero);
+        d->fast->launch(dim3(d->grid), d->fast->lds, d->stream, a, d->net);
     } else {
         hipLaunchKernelGGL(fvp_generic_kernel, dim3(d->grid), dim3(GEN_T), 0, d->stream, d->obs32, (int)d->n,
                            d->th32, d->v32, d->iv32, d->scratch, d->srows, d->slabs, d->net, &d->ctl->zero);
@@ -1425,18 +1676,78 @@ static int ensure_hist(trpo_dev *d, size_t maxiter) {
     return 0;
 }
 
+static double *acc_slot(trpo_dev *d, long j) { return d->accbuf + (j % 3) * (long)d->R * d->P; }
+
+static int allreduce(trpo_dev *d, double *buf, size_t count) {
+    if (!d->comm) return 0;
+    return ncclAllReduce(buf, buf, count, ncclFloat64, ncclSum, d->comm, d->stream) == ncclSuccess ? 0 : -4;
+}
+
+// CG(maxiter) as a straight-line launch sequence (captured into a hipGraph by trpo_dev_cg).
+// Fast path: init, K_0 .. K_{M-1} (K_j fuses CG step j-1 -> j with FVP j), final step.
 static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
-    double *x = d->vec[TRPO_VEC_X], *p = d->vec[TRPO_VEC_P], *b = d->vec[TRPO_VEC_B];
+    double *x = d->vec[TRPO_VEC_X], *b = d->vec[TRPO_VEC_B];
     const int E = cg_E(d->P);
     const int vlen = d->fast ? d->pack.vlen : 0;
     const size_t shm = d->fast ? sizeof(double) * d->P : 0;
-    CG_DISPATCH(E, cg_init_kernel, dim3(1), dim3(1024), shm, d->stream, b, x, d->r, p, d->P, d->ctl, d->hist,
-                (int)maxiter, resth, d->vmap, d->vpack, vlen);
-    for (size_t it = 0; it < maxiter; ++it) {
-        int rc = enqueue_fvp_core(d, p, &d->ctl->done);
-        if (rc) return rc;
-        CG_DISPATCH(E, cg_update_kernel, dim3(1), dim3(1024), shm, d->stream, d->zacc, x, d->r, p, d->P, d->nw,
-                    d->ctl, d->hist, d->vmap, d->vpack, vlen);
+    const int *done = &d->ctl->done;
+    const long M = (long)maxiter;
+    const int RP = d->R * d->P;
+    CG_DISPATCH(E, cg_init_kernel, dim3(1), dim3(1024), shm, d->stream, b, x, d->rbuf[0], d->pbuf[0], d->P, d->ctl,
+                d->st, d->hist, (int)maxiter, resth, d->vmap, d->vpack, vlen, d->atomic ? acc_slot(d, 0) : nullptr,
+                d->atomic ? RP : 0);
+    if (d->fast) {
+        for (long j = 0; j < M; ++j) {
+            IterArgs a = plain_args(d, done);
+            if (d->atomic) {
+                a.acc_out = acc_slot(d, j);
+                a.R_out = d->R;
+                a.acc_zero = acc_slot(d, j + 1);
+                a.zero_len = RP;
+            }
+            if (j > 0) {
+                const int in = (int)((j - 1) & 1), out = (int)(j & 1);
+                a.update = 1;
+                a.acc_in = d->atomic ? acc_slot(d, j - 1) : d->zacc;
+                a.R_in = d->atomic ? d->R : 1;
+                a.p_in = d->pbuf[in];
+                a.r_in = d->rbuf[in];
+                a.p_out = d->pbuf[out];
+                a.r_out = d->rbuf[out];
+                a.x = x;
+                a.st_in = d->st + in;
+                a.st_out = d->st + out;
+                a.ctl = d->ctl;
+                a.hist = d->hist;
+                a.vmap = d->vmap;
+            }
+            d->fast->launch(dim3(d->grid), d->fast->lds, d->stream, a, d->net);
+            int rc;
+            if (d->atomic) {
+                rc = allreduce(d, acc_slot(d, j), (size_t)RP);
+            } else {
+                hipLaunchKernelGGL(reduce_slabs_kernel, dim3(cdiv(d->slab, 64)), dim3(1024), 0, d->stream, d->slabs,
+                                   d->grid, d->slab, d->imap, d->zacc, done);
+                rc = allreduce(d, d->zacc, d->nw);
+            }
+            if (rc) return rc;
+        }
+        if (M > 0) {
+            const int in = (int)((M - 1) & 1), out = (int)(M & 1);
+            CG_DISPATCH(E, cg_update_kernel, dim3(1), dim3(1024), 0, d->stream,
+                        d->atomic ? acc_slot(d, M - 1) : d->zacc, d->atomic ? d->R : 1, d->pbuf[in], d->rbuf[in],
+                        d->pbuf[out], d->rbuf[out], x, d->P, d->nw, d->ctl, d->st + in, d->st + out, d->hist);
+        }
+    } else {
+        // generic kernel (or an empty local shard): FVP, reduce, [all-reduce], CG step per iteration
+        for (long j = 0; j < M; ++j) {
+            const int cur = (int)(j & 1), nxt = (int)((j + 1) & 1);
+            int rc = enqueue_fvp_core(d, d->pbuf[cur], done);
+            if (rc) return rc;
+            CG_DISPATCH(E, cg_update_kernel, dim3(1), dim3(1024), 0, d->stream, d->zacc, 1, d->pbuf[cur],
+                        d->rbuf[cur], d->pbuf[nxt], d->rbuf[nxt], x, d->P, d->nw, d->ctl, d->st + cur, d->st + nxt,
+                        d->hist);
+        }
     }
     HCHK(hipGetLastError());
     return 0;
@@ -1542,7 +1853,7 @@ extern "C" int trpo_dev_read_stamps(unsigned long long *out, int n) {
 extern "C" int trpo_dev_geometry(const trpo_dev *d, int *blocks, int *threads, int *lds_bytes) {
     if (!d) return -1;
     if (blocks) *blocks = d->grid;
-    if (threads) *threads = d->fast ? 512 : GEN_T;
+    if (threads) *threads = d->fast ? 64 * d->fast->waves : GEN_T;
     if (lds_bytes) *lds_bytes = d->fast ? d->fast->lds : 0;
     return 0;
 }
