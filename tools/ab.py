@@ -1,0 +1,36 @@
+"""Interleaved A/B of library variants in ONE process (separate dlopen copies).
+usage: python tools/ab.py lib1.so lib2.so ...   (env SHAPES=arm,2x64 ROUNDS=5)"""
+import ctypes as C, os, sys, importlib, numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "trpo-robot-control_amd")]
+libs = sys.argv[1:]
+mods = []
+for i, path in enumerate(libs):
+    os.environ["TRPO_LIB"] = path
+    for m in [k for k in sys.modules if k.startswith("trpo_amd")]:
+        del sys.modules[m]
+    mod = importlib.import_module("trpo_amd")
+    mod.lib()
+    mods.append(mod)
+from trpo_amd import synth
+SH = {"arm": [15, 16, 16, 3], "2x64": [15, 64, 64, 3]}
+for sname in os.environ.get("SHAPES", "arm,2x64").split(","):
+    L = SH[sname]; n = int(os.environ.get("N", "50000"))
+    th, obs = synth.make_theta(L), synth.make_obs(n, 15)
+    P = synth.num_params(L); b = synth.make_b(P); v = synth.make_v(P)
+    ctxs = []
+    for m in mods:
+        c = m.Context(L, "lttl", th, obs, np.ones(3)); c.upload_b(b); c.upload_v(v); ctxs.append(c)
+    res = {i: {"cg": [], "k": []} for i in range(len(mods))}
+    xs = []
+    for r in range(int(os.environ.get("ROUNDS", "5"))):
+        for i, c in enumerate(ctxs):
+            res[i]["cg"].append(c.time_ms(2, 20, 10, 0.0) * 1e3)
+            res[i]["k"].append(c.time_ms(0, 50) * 1e3)
+    for i, c in enumerate(ctxs):
+        x = c.cg(b, 10, 0.0); xs.append(x)
+    for i, path in enumerate(libs):
+        rel = np.linalg.norm(xs[i] - xs[0]) / np.linalg.norm(xs[0])
+        print("%-5s %-40s cg10 med %.1f min %.1f us | fvp-kernel med %.2f us | x vs lib0 %.1e" % (
+            sname, os.path.basename(path), np.median(res[i]["cg"]), np.min(res[i]["cg"]), np.median(res[i]["k"]), rel), flush=True)
+    for c in ctxs: c.close()

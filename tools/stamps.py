@@ -18,9 +18,9 @@ for name, layers, n in [("arm", [15,16,16,3], 16), ("arm", [15,16,16,3], 50000),
             ctx.enqueue_fvp_kernel()
         ctx.synchronize()
         G = ctx.geometry["blocks"]
-        buf = (C.c_ulonglong * (1024 * 16))()
-        L.trpo_dev_read_stamps(buf, 1024 * 16)
-        a = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 16)[:G, :7].astype(np.int64)
+        buf = (C.c_ulonglong * (1024 * 32))()
+        L.trpo_dev_read_stamps(buf, 1024 * 32)
+        a = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 32)[:G, :7].astype(np.int64)
         t0 = a[:, 0].min()
         rel = (a - t0) * 10 / 1000.0   # us
         print("%s N=%d G=%d  block0 phases (us): %s" % (name, n, G, " ".join("%.2f" % x for x in rel[0])))
@@ -28,7 +28,7 @@ for name, layers, n in [("arm", [15,16,16,3], 16), ("arm", [15,16,16,3], 50000),
             rel[:,0].min(), np.median(rel[:,0]), rel[:,0].max(), rel[:,6].min(), np.median(rel[:,6]), rel[:,6].max()))
         d = np.diff(rel, axis=1)
         print("   median phase durations 0>1 1>2 2>3 3>4 4>5 5>6: %s" % " ".join("%.2f" % x for x in np.median(d, axis=0)))
-        cyc = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 16)[:G, 8:15].astype(np.int64)
+        cyc = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 32)[:G, 16:23].astype(np.int64)
         clk = (cyc[:, 6] - cyc[:, 0]) / np.maximum(1, (a[:, 6] - a[:, 0])) * 100.0   # MHz
         print("   shader clock (MHz) median %.0f  min %.0f  max %.0f" % (np.median(clk), clk.min(), clk.max()))
         print("   kernel_us(events) %.2f" % (ctx.time_ms(0, 50) * 1e3))

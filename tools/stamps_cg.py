@@ -10,9 +10,11 @@ from trpo_amd import synth
 L = trpo_amd.lib()
 L.trpo_dev_read_stamps.restype = C.c_int
 L.trpo_dev_read_stamps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
-order = [0, 7, 1, 2, 3, 4, 5, 6]
-cfgs = [("arm", [15,16,16,3], 50000, g) for g in os.environ.get("GRIDS", "0").split(",")] + [("2x64", [15,64,64,3], 50000, "0")]
-for name, layers, n, grid in cfgs:
+order = [0, 7, 8, 9, 10, 11, 12, 1, 2, 3, 4, 5, 6]
+cfgs = [("arm", [15,16,16,3], 50000, g, r) for g in os.environ.get("GRIDS", "0").split(",") for r in os.environ.get("REPL", "8").split(",")]
+cfgs += [("2x64", [15,64,64,3], 50000, "0", "8")]
+for name, layers, n, grid, repl in cfgs:
+    os.environ["TRPO_REPLICAS"] = repl
     if grid != "0": os.environ["TRPO_FVP_BLOCKS"] = grid
     else: os.environ.pop("TRPO_FVP_BLOCKS", None)
     th = synth.make_theta(layers); P = synth.num_params(layers)
@@ -22,13 +24,13 @@ for name, layers, n, grid in cfgs:
             ctx.enqueue_cg(10, 0.0)
         ctx.synchronize()
         G = ctx.geometry["blocks"]
-        buf = (C.c_ulonglong * (1024 * 16))()
-        L.trpo_dev_read_stamps(buf, 1024 * 16)
-        a = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 16)[:G].astype(np.int64)
+        buf = (C.c_ulonglong * (1024 * 32))()
+        L.trpo_dev_read_stamps(buf, 1024 * 32)
+        a = np.frombuffer(buf, dtype=np.uint64).reshape(1024, 32)[:G].astype(np.int64)
         t = a[:, order]
         rel = (t - t[:, 0].min()) * 10 / 1000.0
         d = np.diff(rel, axis=1)
-        print("%s N=%d G=%d cg10_us=%.1f" % (name, n, G, ctx.time_ms(2, 20, 10, 0.0) * 1e3))
+        print("%s N=%d G=%d R=%s cg10_us=%.1f" % (name, n, G, repl, ctx.time_ms(2, 20, 10, 0.0) * 1e3))
         print("   entry min/med/max %.2f %.2f %.2f  end min/med/max %.2f %.2f %.2f" % (
             rel[:, 0].min(), np.median(rel[:, 0]), rel[:, 0].max(), rel[:, -1].min(), np.median(rel[:, -1]), rel[:, -1].max()))
-        print("   median phases  load>staged %.2f  update %.2f  fwd1 %.2f  tile1 %.2f  rest %.2f  combine %.2f  write %.2f" % tuple(np.median(d, axis=0)))
+        print("   median phases  load>staged %.2f  zwait %.2f  red1 %.2f  red2 %.2f  stage %.2f  bar %.2f  gather %.2f | fwd1 %.2f  tile1 %.2f  rest %.2f  combine %.2f  write %.2f" % tuple(np.median(d, axis=0)))

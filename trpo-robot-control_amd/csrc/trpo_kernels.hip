@@ -116,6 +116,41 @@ __device__ double block_sum(double v, double *sh) {
     return t;
 }
 
+// fp64 DPP row (16-lane) sum; every lane of the row gets it.  Fixed order => deterministic.
+template <int CTRL>
+__device__ __forceinline__ double dpp64(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double rowsum16_f64(double v) {
+    v += dpp64<0xB1>(v);    // quad_perm xor 1
+    v += dpp64<0x4E>(v);    // quad_perm xor 2
+    v += dpp64<0x124>(v);   // row_ror 4
+    v += dpp64<0x128>(v);   // row_ror 8
+    return v;
+}
+// block-wide fp64 sums of K values with ONE barrier: DPP row sums, then every thread adds the
+// (waves x 4 rows) partials from LDS in a fixed order.  sh must hold K * 4 * waves doubles and
+// must not be reused by another call before the block passes another barrier.
+template <int K>
+__device__ __forceinline__ void block_sums_dpp(double (&v)[K], double *sh) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nr = (blockDim.x >> 6) * 4;
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = rowsum16_f64(v[k]);
+    if ((lane & 15) == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) sh[k * nr + w * 4 + (lane >> 4)] = v[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        double t = 0.0;
+        for (int j = 0; j < nr; ++j) t += sh[k * nr + j];
+        v[k] = t;
+    }
+}
+
 // two fixed-order block-wide fp64 sums at once (sh: 2 x 16 doubles)
 __device__ void block_sum2(double a, double b, double *sh, double &sa, double &sb) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nwv = blockDim.x >> 6;
@@ -207,6 +242,46 @@ __device__ int map_frag(const Net &n, int i, int local, int nkt, bool fwd) {
     return n.woff[i] + in * n.L[i + 1] + out;
 }
 
+// v-pack slot -> natural parameter (or -1).  Pure integer math on the shape, so the fused
+// kernel evaluates it in registers instead of loading a map (T compile-time there).
+__device__ __forceinline__ int vmap_at(const Net &n, const int (&T)[4], int e) {
+    const int vfa1 = 256 * T[0] * T[1], vfa2 = vfa1 + 256 * T[1] * T[2], vb0 = vfa2 + 256 * T[2] * T[3];
+    const int vb1 = vb0 + 16 * T[1], vb2 = vb1 + 16 * T[2], end = vb2 + 16 * T[3];
+    if (e < vfa1) return map_frag(n, 0, e, T[0], true);
+    if (e < vfa2) return map_frag(n, 1, e - vfa1, T[1], true);
+    if (e < vb0) return map_frag(n, 2, e - vfa2, T[2], true);
+    if (e < vb1) return e - vb0 < n.L[1] ? n.boff[0] + (e - vb0) : -1;
+    if (e < vb2) return e - vb1 < n.L[2] ? n.boff[1] + (e - vb1) : -1;
+    if (e < end) return e - vb2 < n.L[3] ? n.boff[2] + (e - vb2) : -1;
+    return -1;
+}
+
+// accumulator-order slab position -> natural parameter (or -1): f4 k over
+// [W0 tiles (T0 x T1), W1 (T1 x T2), W2 (T2 x T3), B1 (T1), B2 (T2), B3 (T3)], then lane, r.
+__device__ __forceinline__ int imap_at(const Net &n, const int (&T)[4], int j) {
+    const int k = j >> 8, lane = (j >> 2) & 63, r = j & 3, c = lane & 15, g = lane >> 4;
+    int base = 0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int nt = T[i] * T[i + 1];
+        if (k >= base && k < base + nt) {
+            const int at = (k - base) / T[i + 1], bt = (k - base) % T[i + 1];
+            const int a = 16 * at + 4 * g + r, b = 16 * bt + c;
+            return (a < n.L[i] && b < n.L[i + 1]) ? n.woff[i] + a * n.L[i + 1] + b : -1;
+        }
+        base += nt;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        if (k >= base && k < base + T[i + 1]) {
+            const int b = 16 * (k - base) + 4 * g + r;
+            return (c == 0 && b < n.L[i + 1]) ? n.boff[i] + b : -1;
+        }
+        base += T[i + 1];
+    }
+    return -1;
+}
+
 __global__ void build_maps_kernel(Net n, Pack pk, int *tmap, int *vmap) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e < pk.tlen) {
@@ -223,18 +298,7 @@ __global__ void build_maps_kernel(Net n, Pack pk, int *tmap, int *vmap) {
         }
         tmap[e] = m;
     }
-    if (e < pk.vlen) {
-        int m = -1;
-        for (int i = 0; i < 3; ++i) {
-            if (e >= pk.vfa[i] && e < pk.vfa[i] + 256 * pk.T[i] * pk.T[i + 1])
-                m = map_frag(n, i, e - pk.vfa[i], pk.T[i], true);
-            if (e >= pk.vb[i] && e < pk.vb[i] + 16 * pk.T[i + 1]) {
-                const int j = e - pk.vb[i];
-                m = j < n.L[i + 1] ? n.boff[i] + j : -1;
-            }
-        }
-        vmap[e] = m;
-    }
+    if (e < pk.vlen) vmap[e] = vmap_at(n, pk.T, e);
 }
 
 __global__ void gather_pack_kernel(float *dst, const double *src, const int *map, int len) {
@@ -249,27 +313,7 @@ __global__ void gather_pack_kernel(float *dst, const double *src, const int *map
 // f4 k over [W0 tiles (T0 x T1), W1 (T1 x T2), W2 (T2 x T3), B1 (T1), B2 (T2), B3 (T3)], then lane, r.
 __global__ void build_imap_kernel(Net n, Pack pk, int *imap, int slab) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= slab) return;
-    const int k = j >> 8, lane = (j >> 2) & 63, r = j & 3, c = lane & 15, g = lane >> 4;
-    const int *T = pk.T;
-    int base = 0, m = -1;
-    for (int i = 0; i < 3 && m == -1; ++i) {
-        const int nt = T[i] * T[i + 1];
-        if (k < base + nt) {
-            const int at = (k - base) / T[i + 1], bt = (k - base) % T[i + 1];
-            const int a = 16 * at + 4 * g + r, b = 16 * bt + c;
-            m = (a < n.L[i] && b < n.L[i + 1]) ? n.woff[i] + a * n.L[i + 1] + b : -2;
-        }
-        base += nt;
-    }
-    for (int i = 0; i < 3 && m == -1; ++i) {
-        if (k < base + T[i + 1]) {
-            const int b = 16 * (k - base) + 4 * g + r;
-            m = (c == 0 && b < n.L[i + 1]) ? n.boff[i] + b : -2;
-        }
-        base += T[i + 1];
-    }
-    imap[j] = m < 0 ? -1 : m;
+    if (j < slab) imap[j] = imap_at(n, pk.T, j);
 }
 
 __global__ void iota_kernel(int *v, int len, int valid) {
@@ -299,12 +343,12 @@ __global__ void to_f32_kernel(float *dst, const double *src, int len) {
 // Diagnostic build only (-DTRPO_STAMPS): s_memrealtime (100 MHz) stamps per block.
 // ---------------------------------------------------------------------------
 #ifdef TRPO_STAMPS
-__device__ unsigned long long g_stamps[1024 * 16];
+__device__ unsigned long long g_stamps[1024 * 32];
 #define STAMP(k)                                                                             \
     do {                                                                                     \
         if (threadIdx.x == 0 && blockIdx.x < 1024) {                                         \
-            g_stamps[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memrealtime();              \
-            g_stamps[blockIdx.x * 16 + 8 + (k)] = __builtin_amdgcn_s_memtime();              \
+            g_stamps[blockIdx.x * 32 + (k)] = __builtin_amdgcn_s_memrealtime();              \
+            g_stamps[blockIdx.x * 32 + 16 + (k)] = __builtin_amdgcn_s_memtime();             \
         }                                                                                    \
     } while (0)
 #else
@@ -348,20 +392,33 @@ struct FastCfg {
     static constexpr int SLAB = NACC * 64;
     // small nets: weights live in registers and 16 waves per block keep <= 1 tile per wave
     static constexpr bool REGW = T0 * T1 + T1 * T2 + T2 * T3 <= 3;
-    static constexpr int WAVES = 8;
+#ifndef TRPO_ARM_WAVES
+#define TRPO_ARM_WAVES 8
+#endif
+    // 12 waves (3 per SIMD) for the small nets: ~1 tile per wave at N = 50k, balanced SIMDs
+#ifndef TRPO_BIG_WAVES
+#define TRPO_BIG_WAVES 8
+#endif
+    static constexpr int WAVES = REGW ? TRPO_ARM_WAVES : TRPO_BIG_WAVES;
+    static constexpr int NT = 1;                   // tiles in flight per wave (2 measured no faster)
     static constexpr int THREADS = 64 * WAVES;
-    static constexpr int MAIN_BYTES = 4 * (TLEN + VLEN + WAVES * SCR);
+    static constexpr int PMAX = 256 * (T0 * T1 + T1 * T2 + T2 * T3) + 16 * (T1 + T2 + 2 * T3);
+    // tile scratch; also stages the fp64 direction of the fused CG update
+    static constexpr int SCRATCH = (WAVES * NT * SCR > 2 * PMAX) ? WAVES * NT * SCR : 2 * PMAX;
+    static constexpr int MAIN_BYTES = 4 * (TLEN + VLEN + SCRATCH);
     static constexpr int CAP = MAIN_BYTES > 131072 ? MAIN_BYTES : 131072;
     // waves combined per epilogue round (largest divisor of WAVES whose dumps fit)
-    static constexpr int RW = (WAVES * SLAB * 4 <= CAP) ? WAVES : (8 * SLAB * 4 <= CAP) ? 8 : (4 * SLAB * 4 <= CAP) ? 4
-                              : (2 * SLAB * 4 <= CAP) ? 2 : 1;
+    static constexpr int rw_pick(int w) {
+        return w < 1 ? 1 : ((WAVES % w == 0 && w * SLAB * 4 <= CAP) ? w : rw_pick(w - 1));
+    }
+    static constexpr int RW = rw_pick(WAVES);
     static constexpr int EPT = (SLAB / 4 + THREADS - 1) / THREADS;   // f4 slices per thread in the combine
     // fused CG update: natural P-vector elements per thread (upper bound from the padded shape)
-    static constexpr int PMAX = 256 * (T0 * T1 + T1 * T2 + T2 * T3) + 16 * (T1 + T2 + 2 * T3);
     static constexpr int EMAX = (PMAX + THREADS - 1) / THREADS;
     static constexpr int VEMAX = (VLEN + THREADS - 1) / THREADS;
     static constexpr int EMAX_REPLICAS = 4;        // atomic-replica reduction only for EMAX <= this
-    static_assert(2 * PMAX <= WAVES * SCR, "fp64 staging of p must fit the tile scratch");
+    static_assert(NT == 1 || NT == 2, "NT");
+    static_assert(WAVES % RW == 0, "RW");
     static int lds_bytes() {
         const int b = 4 * RW * SLAB;
         return MAIN_BYTES > b ? MAIN_BYTES : b;
@@ -395,14 +452,13 @@ template <int T0, int T1, int T2, int T3, int ACT>
 __global__ void __launch_bounds__((64 * FastCfg<T0, T1, T2, T3>::WAVES))
 fvp_mlp3_kernel(IterArgs A, Net net) {
     using C = FastCfg<T0, T1, T2, T3>;
-    (void)net;
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    __shared__ double sh64[32];
+    __shared__ double sh64[12 * C::WAVES];      // 1 + 2 DPP block sums, 4 rows per wave
     float *tw = lds;                                   // theta pack
     float *vw = lds + C::TLEN;                         // v pack (fragment order, fp32)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int c = lane & 15, g = lane >> 4;
-    float *scr = lds + C::TLEN + C::VLEN + wave * C::SCR;
+    float *scr = lds + C::TLEN + C::VLEN + wave * C::NT * C::SCR;
     const int nwaves = gridDim.x * C::WAVES;
     const int ntiles = A.ntiles, n = A.n;
     const f4 *obs4 = reinterpret_cast<const f4 *>(A.obs4);
@@ -433,18 +489,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
 #pragma unroll
         for (int kt = 0; kt < T0; ++kt) xn[kt] = obs4[(long)(tl * 16 + c) * (4 * T0) + kt * 4 + g];
     }
-    int im[C::EPT][4];
-    {
-        const int *imap = A.acc_out ? A.imap : A.skip;      // any valid pointer when unused
-#pragma unroll
-        for (int j = 0; j < C::EPT; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int e = 4 * (tid + j * C::THREADS) + r;
-                const int v = imap[A.acc_out ? min(e, C::SLAB - 1) : 0];
-                im[j][r] = e < C::SLAB ? v : -1;
-            }
-    }
+    constexpr int Tc[4] = {T0, T1, T2, T3};
     // CG state for the fused update (src/TRPO_CG.c:77-103), loaded in the same round
     double pv[C::EMAX], rv[C::EMAX], zv[C::EMAX], xv[C::EMAX];
     int vm[C::VEMAX];
@@ -469,8 +514,9 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
                 double za[8];
 #pragma unroll
                 for (int k = 0; k < 8; ++k) za[k] = A.acc_in[(long)min(k, A.R_in - 1) * A.P + qz];
+                z = za[0];                                // R_in >= 1: no select on the first term
 #pragma unroll
-                for (int k = 0; k < 8; ++k) z += k < A.R_in ? za[k] : 0.0;
+                for (int k = 1; k < 8; ++k) z += k < A.R_in ? za[k] : 0.0;
             } else {
                 z = A.acc_in[qz];                         // slab mode: one reduced vector
             }
@@ -480,11 +526,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
             zv[e] = q < A.nw ? z : 0.0;
         }
 #pragma unroll
-        for (int e = 0; e < C::VEMAX; ++e) {
-            const int ve = tid + e * C::THREADS;
-            const int v = A.vmap[min(ve, C::VLEN - 1)];
-            vm[e] = ve < C::VLEN ? v : -1;
-        }
+        for (int e = 0; e < C::VEMAX; ++e) vm[e] = vmap_at(net, Tc, tid + e * C::THREADS);
     }
     if (skipv) return;                                 // grid-uniform
     {
@@ -506,7 +548,11 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
             zv[e] = (q < A.nw ? zv[e] / cn : 2.0 * pv[e]) + clam * pv[e];
             pz += pv[e] * zv[e];
         }
-        const double alpha = sin.rdotr / block_sum(pz, sh64);
+        STAMP(8);
+        double red1[1] = {pz};
+        block_sums_dpp<1>(red1, sh64);
+        STAMP(9);
+        const double alpha = sin.rdotr / red1[0];
         double rr = 0.0, xx = 0.0;
 #pragma unroll
         for (int e = 0; e < C::EMAX; ++e) {
@@ -515,8 +561,10 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
             xv[e] += alpha * pv[e];
             xx += xv[e] * xv[e];
         }
-        double nr, xn2;
-        block_sum2(rr, xx, sh64, nr, xn2);
+        double red2[2] = {rr, xx};
+        block_sums_dpp<2>(red2, sh64 + 4 * C::WAVES);
+        const double nr = red2[0], xn2 = red2[1];
+        STAMP(10);
         const double beta = nr / sin.rdotr;
         double *stage = reinterpret_cast<double *>(lds + C::TLEN + C::VLEN);
 #pragma unroll
@@ -544,7 +592,9 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
             A.ctl->done = done;
         }
         if (done) return;                              // block-uniform (identical in every block)
+        STAMP(11);
         __syncthreads();
+        STAMP(12);
 #pragma unroll
         for (int e = 0; e < C::VEMAX; ++e) {
             const int ve = tid + e * C::THREADS;
@@ -598,96 +648,139 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
 #pragma unroll
     for (int a = 0; a < T3; ++a) sB3[a] = zero4;
 
-    for (; tile < ntiles; tile += nwaves) {
-        const int sample = tile * 16 + c;
-        // input tile: lane holds features 16kt+4g..+3 of its sample (D-layout rows);
-        // the next tile's observations are prefetched while this one computes
-        f4 x0[T0];
+    // NT independent tiles per loop trip (ILP: the scheduler interleaves their MFMA chains)
+    constexpr int NT = C::NT;
+    for (; tile < ntiles; tile += NT * nwaves) {
+        // input tiles: lane holds features 16kt+4g..+3 of its sample (D-layout rows)
+        f4 x0[NT][T0];
+        bool live[NT];
 #pragma unroll
-        for (int kt = 0; kt < T0; ++kt) x0[kt] = xn[kt];
-        {
-            const int tn = min(tile + nwaves, ntiles - 1);     // unconditional prefetch (clamped)
+        for (int t = 0; t < NT; ++t) {
+            const int tt = tile + t * nwaves;
+            live[t] = tt * 16 + c < n;
+            if (t == 0) {
+#pragma unroll
+                for (int kt = 0; kt < T0; ++kt) x0[0][kt] = xn[kt];
+            } else {
+                const int tc = min(tt, ntiles - 1);
+#pragma unroll
+                for (int kt = 0; kt < T0; ++kt) x0[t][kt] = obs4[(long)(tc * 16 + c) * (4 * T0) + kt * 4 + g];
+            }
+        }
+        {   // unconditional (clamped) prefetch of the next trip's first tile
+            const int tn = min(tile + NT * nwaves, ntiles - 1);
 #pragma unroll
             for (int kt = 0; kt < T0; ++kt) xn[kt] = obs4[(long)(tn * 16 + c) * (4 * T0) + kt * 4 + g];
         }
 
         // ---- layer 0: x1 = W0^T x0 + b0 ; Rx1 = VW0^T x0 + vb0 (Ry0 = 0) ----
-        f4 y1[T1], r1[T1];
+        f4 y1[NT][T1], r1[NT][T1];
 #pragma unroll
         for (int ot = 0; ot < T1; ++ot) {
-            f4 a = TW[C::BI0 / 4 + ot * 4 + g];
-            f4 ra = VW[C::VB0 / 4 + ot * 4 + g];
+            const f4 b0 = TW[C::BI0 / 4 + ot * 4 + g], vb0 = VW[C::VB0 / 4 + ot * 4 + g];
+            f4 a[NT], ra[NT];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                a[t] = b0;
+                ra[t] = vb0;
+            }
 #pragma unroll
             for (int kt = 0; kt < T0; ++kt) {
                 const f4 w = WLD(rFA0, TW[C::FA0 / 4 + (ot * T0 + kt) * 64 + lane]);
                 const f4 u = WLD(rVFA0, VW[C::VFA0 / 4 + (ot * T0 + kt) * 64 + lane]);
 #pragma unroll
-                for (int s = 0; s < 4; ++s) {
-                    a = MFMA(w[s], x0[kt][s], a);
-                    ra = MFMA(u[s], x0[kt][s], ra);
-                }
+                for (int s = 0; s < 4; ++s)
+#pragma unroll
+                    for (int t = 0; t < NT; ++t) {
+                        a[t] = MFMA(w[s], x0[t][kt][s], a[t]);
+                        ra[t] = MFMA(u[s], x0[t][kt][s], ra[t]);
+                    }
             }
-            y1[ot] = act_fwd(a1, a, ra, r1[ot]);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) y1[t][ot] = act_fwd(a1, a[t], ra[t], r1[t][ot]);
         }
         // ---- layer 1 ----
-        f4 y2[T2], r2[T2];
+        f4 y2[NT][T2], r2[NT][T2];
 #pragma unroll
         for (int ot = 0; ot < T2; ++ot) {
-            f4 a = TW[C::BI1 / 4 + ot * 4 + g];
-            f4 ra = VW[C::VB1 / 4 + ot * 4 + g];
-            f4 rb = zero4;                    // second chain: halves the dependent MFMA depth
+            const f4 b1 = TW[C::BI1 / 4 + ot * 4 + g], vb1 = VW[C::VB1 / 4 + ot * 4 + g];
+            f4 a[NT], ra[NT], rb[NT];                     // rb: second R chain, halves the depth
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                a[t] = b1;
+                ra[t] = vb1;
+                rb[t] = zero4;
+            }
 #pragma unroll
             for (int kt = 0; kt < T1; ++kt) {
                 const f4 w = WLD(rFA1, TW[C::FA1 / 4 + (ot * T1 + kt) * 64 + lane]);
                 const f4 u = WLD(rVFA1, VW[C::VFA1 / 4 + (ot * T1 + kt) * 64 + lane]);
 #pragma unroll
-                for (int s = 0; s < 4; ++s) {
-                    a = MFMA(w[s], y1[kt][s], a);
-                    ra = MFMA(w[s], r1[kt][s], ra);
-                    rb = MFMA(u[s], y1[kt][s], rb);
-                }
+                for (int s = 0; s < 4; ++s)
+#pragma unroll
+                    for (int t = 0; t < NT; ++t) {
+                        a[t] = MFMA(w[s], y1[t][kt][s], a[t]);
+                        ra[t] = MFMA(w[s], r1[t][kt][s], ra[t]);
+                        rb[t] = MFMA(u[s], y1[t][kt][s], rb[t]);
+                    }
             }
-            y2[ot] = act_fwd(a2, a, ra + rb, r2[ot]);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) y2[t][ot] = act_fwd(a2, a[t], ra[t] + rb[t], r2[t][ot]);
         }
         // ---- layer 2 (output) and G3 = act3'(Ry3 / sigma^2) ----
-        f4 g3[T3];
-        const bool live = sample < n;
+        f4 g3[NT][T3];
 #pragma unroll
         for (int ot = 0; ot < T3; ++ot) {
-            f4 a = TW[C::BI2 / 4 + ot * 4 + g];
-            f4 ra = VW[C::VB2 / 4 + ot * 4 + g];
-            f4 rb = zero4;
+            const f4 b2 = TW[C::BI2 / 4 + ot * 4 + g], vb2 = VW[C::VB2 / 4 + ot * 4 + g];
+            const f4 iv = TW[C::IV / 4 + ot * 4 + g];
+            f4 a[NT], ra[NT], rb[NT];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                a[t] = b2;
+                ra[t] = vb2;
+                rb[t] = zero4;
+            }
 #pragma unroll
             for (int kt = 0; kt < T2; ++kt) {
                 const f4 w = WLD(rFA2, TW[C::FA2 / 4 + (ot * T2 + kt) * 64 + lane]);
                 const f4 u = WLD(rVFA2, VW[C::VFA2 / 4 + (ot * T2 + kt) * 64 + lane]);
 #pragma unroll
-                for (int s = 0; s < 4; ++s) {
-                    if (y3_needed) a = MFMA(w[s], y2[kt][s], a);
-                    ra = MFMA(w[s], r2[kt][s], ra);
-                    rb = MFMA(u[s], y2[kt][s], rb);
-                }
+                for (int s = 0; s < 4; ++s)
+#pragma unroll
+                    for (int t = 0; t < NT; ++t) {
+                        if (y3_needed) a[t] = MFMA(w[s], y2[t][kt][s], a[t]);
+                        ra[t] = MFMA(w[s], r2[t][kt][s], ra[t]);
+                        rb[t] = MFMA(u[s], y2[t][kt][s], rb[t]);
+                    }
             }
-            f4 r3;
-            const f4 y3 = act_fwd(a3, a, ra + rb, r3);
-            const f4 iv = TW[C::IV / 4 + ot * 4 + g];
-            f4 gg = act_bwd(a3, y3, r3 * iv);
-            g3[ot] = live ? gg : zero4;
-            sB3[ot] += g3[ot];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                f4 r3;
+                const f4 y3 = act_fwd(a3, a[t], ra[t] + rb[t], r3);
+                const f4 gg = act_bwd(a3, y3, r3 * iv);
+                g3[t][ot] = live[t] ? gg : zero4;
+                sB3[ot] += g3[t][ot];
+            }
         }
         if (first_tile) STAMP(2);
-        // ---- contraction RGW2 += Y2 . G3^T (K = 16 samples) ----
+        // ---- contraction RGW2 += Y2 . G3^T (K = 16 samples per tile) ----
 #pragma unroll
-        for (int t = 0; t < T2; ++t) scr_put(scr, 16 * t, y2[t], c, g);
+        for (int t = 0; t < NT; ++t) {
+            float *sc = scr + t * C::SCR;
 #pragma unroll
-        for (int t = 0; t < T3; ++t) scr_put(scr, 16 * (T2 + t), g3[t], c, g);
-        {
+            for (int i = 0; i < T2; ++i) scr_put(sc, 16 * i, y2[t][i], c, g);
+#pragma unroll
+            for (int i = 0; i < T3; ++i) scr_put(sc, 16 * (T2 + i), g3[t][i], c, g);
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const float *sc = scr + t * C::SCR;
             f4 gb[T3];
 #pragma unroll
-            for (int t = 0; t < T3; ++t) gb[t] = scr_get(scr, 16 * (T2 + t), c, g);
+            for (int i = 0; i < T3; ++i) gb[i] = scr_get(sc, 16 * (T2 + i), c, g);
 #pragma unroll
             for (int at = 0; at < T2; ++at) {
-                const f4 ya = scr_get(scr, 16 * at, c, g);
+                const f4 ya = scr_get(sc, 16 * at, c, g);
 #pragma unroll
                 for (int bt = 0; bt < T3; ++bt)
 #pragma unroll
@@ -695,31 +788,44 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
             }
         }
         // ---- G2 = act2'(W2 G3) ----
-        f4 g2[T2];
+        f4 g2[NT][T2];
 #pragma unroll
         for (int it = 0; it < T2; ++it) {
-            f4 a = zero4;
+            f4 a[NT];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) a[t] = zero4;
 #pragma unroll
             for (int kt = 0; kt < T3; ++kt) {
                 const f4 w = WLD(rFB2, TW[C::FB2 / 4 + (it * T3 + kt) * 64 + lane]);
 #pragma unroll
-                for (int s = 0; s < 4; ++s) a = MFMA(w[s], g3[kt][s], a);
+                for (int s = 0; s < 4; ++s)
+#pragma unroll
+                    for (int t = 0; t < NT; ++t) a[t] = MFMA(w[s], g3[t][kt][s], a[t]);
             }
-            g2[it] = act_bwd(a2, y2[it], a);
-            sB2[it] += g2[it];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                g2[t][it] = act_bwd(a2, y2[t][it], a[t]);
+                sB2[it] += g2[t][it];
+            }
         }
         // ---- contraction RGW1 += Y1 . G2^T ----
 #pragma unroll
-        for (int t = 0; t < T1; ++t) scr_put(scr, 16 * t, y1[t], c, g);
+        for (int t = 0; t < NT; ++t) {
+            float *sc = scr + t * C::SCR;
 #pragma unroll
-        for (int t = 0; t < T2; ++t) scr_put(scr, 16 * (T1 + t), g2[t], c, g);
-        {
+            for (int i = 0; i < T1; ++i) scr_put(sc, 16 * i, y1[t][i], c, g);
+#pragma unroll
+            for (int i = 0; i < T2; ++i) scr_put(sc, 16 * (T1 + i), g2[t][i], c, g);
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const float *sc = scr + t * C::SCR;
             f4 gb[T2];
 #pragma unroll
-            for (int t = 0; t < T2; ++t) gb[t] = scr_get(scr, 16 * (T1 + t), c, g);
+            for (int i = 0; i < T2; ++i) gb[i] = scr_get(sc, 16 * (T1 + i), c, g);
 #pragma unroll
             for (int at = 0; at < T1; ++at) {
-                const f4 ya = scr_get(scr, 16 * at, c, g);
+                const f4 ya = scr_get(sc, 16 * at, c, g);
 #pragma unroll
                 for (int bt = 0; bt < T2; ++bt)
 #pragma unroll
@@ -727,31 +833,44 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
             }
         }
         // ---- G1 = act1'(W1 G2) ----
-        f4 g1[T1];
+        f4 g1[NT][T1];
 #pragma unroll
         for (int it = 0; it < T1; ++it) {
-            f4 a = zero4;
+            f4 a[NT];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) a[t] = zero4;
 #pragma unroll
             for (int kt = 0; kt < T2; ++kt) {
                 const f4 w = WLD(rFB1, TW[C::FB1 / 4 + (it * T2 + kt) * 64 + lane]);
 #pragma unroll
-                for (int s = 0; s < 4; ++s) a = MFMA(w[s], g2[kt][s], a);
+                for (int s = 0; s < 4; ++s)
+#pragma unroll
+                    for (int t = 0; t < NT; ++t) a[t] = MFMA(w[s], g2[t][kt][s], a[t]);
             }
-            g1[it] = act_bwd(a1, y1[it], a);
-            sB1[it] += g1[it];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                g1[t][it] = act_bwd(a1, y1[t][it], a[t]);
+                sB1[it] += g1[t][it];
+            }
         }
         // ---- contraction RGW0 += X0 . G1^T ----
 #pragma unroll
-        for (int t = 0; t < T0; ++t) scr_put(scr, 16 * t, x0[t], c, g);
+        for (int t = 0; t < NT; ++t) {
+            float *sc = scr + t * C::SCR;
 #pragma unroll
-        for (int t = 0; t < T1; ++t) scr_put(scr, 16 * (T0 + t), g1[t], c, g);
-        {
+            for (int i = 0; i < T0; ++i) scr_put(sc, 16 * i, x0[t][i], c, g);
+#pragma unroll
+            for (int i = 0; i < T1; ++i) scr_put(sc, 16 * (T0 + i), g1[t][i], c, g);
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const float *sc = scr + t * C::SCR;
             f4 gb[T1];
 #pragma unroll
-            for (int t = 0; t < T1; ++t) gb[t] = scr_get(scr, 16 * (T0 + t), c, g);
+            for (int i = 0; i < T1; ++i) gb[i] = scr_get(sc, 16 * (T0 + i), c, g);
 #pragma unroll
             for (int at = 0; at < T0; ++at) {
-                const f4 ya = scr_get(scr, 16 * at, c, g);
+                const f4 ya = scr_get(sc, 16 * at, c, g);
 #pragma unroll
                 for (int bt = 0; bt < T1; ++bt)
 #pragma unroll
@@ -833,8 +952,10 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
 #pragma unroll
         for (int j = 0; j < C::EPT; ++j)
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-                if (im[j][r] >= 0) unsafeAtomicAdd(dst + im[j][r], (double)part[j][r]);
+            for (int r = 0; r < 4; ++r) {
+                const int m = imap_at(net, Tc, 4 * (tid + j * C::THREADS) + r);
+                if (m >= 0) unsafeAtomicAdd(dst + m, (double)part[j][r]);
+            }
         if (blockIdx.x == 0)
             for (int e = tid; e < A.zero_len; e += C::THREADS) A.acc_zero[e] = 0.0;
     } else {
@@ -1316,7 +1437,12 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
         DMALLOC(d->pbuf[i], sizeof(double) * d->P);
         DMALLOC(d->rbuf[i], sizeof(double) * d->P);
     }
-    d->R = 8;
+    {
+        const char *er = getenv("TRPO_REPLICAS");
+        d->R = er ? atoi(er) : 8;
+        if (d->R < 1) d->R = 1;
+        if (d->R > 8) d->R = 8;
+    }
     DMALLOC(d->accbuf, sizeof(double) * 3 * d->R * d->P);
     if (d->fast) {
         Pack &pk = d->pack;
@@ -1840,7 +1966,7 @@ extern "C" const char *trpo_dev_kernel_name(const trpo_dev *d) { return d ? d->n
 // Diagnostic builds only: copy the per-block phase stamps (100 MHz ticks) to the host.
 extern "C" int trpo_dev_read_stamps(unsigned long long *out, int n) {
 #ifdef TRPO_STAMPS
-    if (n > 1024 * 16) n = 1024 * 16;
+    if (n > 1024 * 32) n = 1024 * 32;
     HCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * n, 0, hipMemcpyDeviceToHost));
     return n;
 #else
