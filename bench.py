@@ -193,6 +193,12 @@ def main():
     achieved_tflops = flops / (k_ms * 1e-3) / 1e12
     bytes_alg = bytes_per_fvp(ARM, n_local)
 
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "r01_fvp_traffic.json")
+    if os.path.exists(tpath) and dist.world == 1:
+        # HBM bytes per launch of this kernel at this workload, from the committed rocprofv3 PMC passes
+        traffic = json.load(open(tpath))["traffic_bytes"]
+
     result = {
         "metric": "FVP samples/sec + 10-iter CG wall time, armDOF_0 policy",
         "value": value,
@@ -213,7 +219,7 @@ def main():
         "cg_wall_ms": ms_per_step,
         "fvp_ms": fvp_ms,
         "roofline": {"bound": "mfma", "achieved": achieved_tflops, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved_tflops / PEAK_FP32_TFLOPS, "traffic": None,
+                     "frac": achieved_tflops / PEAK_FP32_TFLOPS, "traffic": traffic,
                      "kernel": "fvp_mlp3_kernel", "kernel_ms": k_ms, "flops_per_launch": flops,
                      "alg_bytes_per_launch": bytes_alg,
                      "hbm_gbs_algorithmic": bytes_alg / (k_ms * 1e-3) / 1e9,
