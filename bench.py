@@ -172,7 +172,7 @@ def main():
     dist = Dist()
     if dist.world != args.gpus and dist.rank == 0:
         print("warning: --gpus %d but WORLD_SIZE=%d" % (args.gpus, dist.world), file=sys.stderr)
-    device = dist.local_rank
+    device = int(os.environ.get("TRPO_BENCH_DEVICE", dist.local_rank))   # override: testing only
 
     ctx, theta, obs_all = make_ctx(ARM, N_TOTAL, dist, device)
     P = synth.num_params(ARM)

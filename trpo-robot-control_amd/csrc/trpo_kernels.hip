@@ -1312,6 +1312,7 @@ struct trpo_dev {
     double damping;
     // CG graph cache
     hipGraphExec_t cg_exec;
+    int no_graph;
     size_t cg_graph_iters;
     double cg_graph_resth;
     hipEvent_t ev0, ev1;
@@ -1886,22 +1887,32 @@ extern "C" int trpo_dev_cg(trpo_dev *d, size_t maxiter, double resth) {
     int rc = ensure_hist(d, maxiter);
     if (rc) return rc;
     const char *ng = getenv("TRPO_NO_GRAPH");
-    if (ng && atoi(ng)) return enqueue_cg_body(d, maxiter, resth);
+    if ((ng && atoi(ng)) || d->no_graph) return enqueue_cg_body(d, maxiter, resth);
     // the graph bakes (maxiter, resth) into cg_init's arguments: key on both
     if (!d->cg_exec || d->cg_graph_iters != maxiter || d->cg_graph_resth != resth) {
         if (d->cg_exec) {
             hipGraphExecDestroy(d->cg_exec);
             d->cg_exec = NULL;
         }
-        hipGraph_t graph;
-        HCHK(hipStreamBeginCapture(d->stream, hipStreamCaptureModeThreadLocal));
+        hipGraph_t graph = NULL;
+        // relaxed mode: RCCL may call non-stream APIs while its collective is being captured
+        HCHK(hipStreamBeginCapture(d->stream, d->comm ? hipStreamCaptureModeRelaxed : hipStreamCaptureModeThreadLocal));
         rc = enqueue_cg_body(d, maxiter, resth);
         hipError_t e = hipStreamEndCapture(d->stream, &graph);
-        if (rc) return rc;
-        HCHK(e);
-        e = hipGraphInstantiate(&d->cg_exec, graph, NULL, NULL, 0);
-        hipGraphDestroy(graph);
-        HCHK(e);
+        if (!rc && e == hipSuccess) {
+            e = hipGraphInstantiate(&d->cg_exec, graph, NULL, NULL, 0);
+        }
+        if (graph) hipGraphDestroy(graph);
+        if (rc || e != hipSuccess) {
+            // capture unsupported here (e.g. by the collective library): run the same sequence
+            // eagerly from now on -- identical kernels, only launch overhead differs
+            fprintf(stderr, "[trpo_mi355x] CG graph capture failed (%s, rc=%d); launching eagerly\n",
+                    hipGetErrorString(e), rc);
+            (void)hipGetLastError();
+            d->cg_exec = NULL;
+            d->no_graph = 1;
+            return enqueue_cg_body(d, maxiter, resth);
+        }
         d->cg_graph_iters = maxiter;
         d->cg_graph_resth = resth;
     }
