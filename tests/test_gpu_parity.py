@@ -161,3 +161,18 @@ def test_set_obs_and_damping_update():
         ctx.set_damping(0.25)
         ref, _ = oracle.fvp(layers, "lttl", th, obs2, np.ones(3), v, damping=0.25)
         assert cases.rel_l2(ctx.fvp(v), ref) <= FVP_TOL
+
+
+@pytest.mark.parametrize("layers,acts", [([15, 16, 16, 6], "lttl"), ([15, 16, 16, 4], "ltts"),
+                                         ([20, 32, 16, 1], "lstl")])
+def test_output_widths_and_activations_against_oracle(layers, acts):
+    import oracle
+    from trpo_amd import synth
+    n = 1500
+    th, obs = synth.make_theta(layers), synth.make_obs(n, layers[0])
+    std = np.linspace(0.7, 1.2, layers[-1])
+    v = synth.make_v(synth.num_params(layers))
+    ref, _ = oracle.fvp(layers, acts, th, obs, std, v)
+    with trpo_amd.Context(layers, acts, th, obs, std) as ctx:
+        assert ctx.kernel_name.startswith("mfma-mlp3")
+        assert cases.rel_l2(ctx.fvp(v), ref) <= FVP_TOL

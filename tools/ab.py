@@ -1,9 +1,12 @@
 """Interleaved A/B of library variants in ONE process (separate dlopen copies).
-usage: python tools/ab.py lib1.so lib2.so ...   (env SHAPES=arm,2x64 ROUNDS=5)"""
+usage: python tools/ab.py lib1.so lib2.so[:ENV=V,ENV2=W] ...   (env SHAPES=arm,2x64 ROUNDS=5)
+An optional ":ENV=V" suffix sets environment variables while that entry's contexts are created."""
 import ctypes as C, os, sys, importlib, numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "trpo-robot-control_amd")]
-libs = sys.argv[1:]
+specs = sys.argv[1:]
+libs = [sp.split(":")[0] for sp in specs]
+envs = [dict(kv.split("=") for kv in sp.split(":")[1].split(",")) if ":" in sp else {} for sp in specs]
 mods = []
 for i, path in enumerate(libs):
     os.environ["TRPO_LIB"] = path
@@ -19,8 +22,13 @@ for sname in os.environ.get("SHAPES", "arm,2x64").split(","):
     th, obs = synth.make_theta(L), synth.make_obs(n, 15)
     P = synth.num_params(L); b = synth.make_b(P); v = synth.make_v(P)
     ctxs = []
-    for m in mods:
+    for m, env in zip(mods, envs):
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
         c = m.Context(L, "lttl", th, obs, np.ones(3)); c.upload_b(b); c.upload_v(v); ctxs.append(c)
+        for k, val in old.items():
+            if val is None: os.environ.pop(k)
+            else: os.environ[k] = val
     res = {i: {"cg": [], "k": []} for i in range(len(mods))}
     xs = []
     for r in range(int(os.environ.get("ROUNDS", "5"))):
@@ -32,5 +40,5 @@ for sname in os.environ.get("SHAPES", "arm,2x64").split(","):
     for i, path in enumerate(libs):
         rel = np.linalg.norm(xs[i] - xs[0]) / np.linalg.norm(xs[0])
         print("%-5s %-40s cg10 med %.1f min %.1f us | fvp-kernel med %.2f us | x vs lib0 %.1e" % (
-            sname, os.path.basename(path), np.median(res[i]["cg"]), np.min(res[i]["cg"]), np.median(res[i]["k"]), rel), flush=True)
+            sname, os.path.basename(specs[i]), np.median(res[i]["cg"]), np.min(res[i]["cg"]), np.median(res[i]["k"]), rel), flush=True)
     for c in ctxs: c.close()

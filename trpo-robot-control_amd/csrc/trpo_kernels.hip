@@ -71,6 +71,7 @@ struct Ctl {                   // device-side control block of one context
 
 struct CgSt {                  // ping-ponged CG scalars (state k = before FVP k)
     double rdotr;
+    double xx;                 // |x|^2 (printed as the "Soln Norm")
     int iter;
     int pad;
 };
@@ -102,8 +103,6 @@ struct IterArgs {
 };
 
 // fixed-order block-wide fp64 sum (every thread gets the result)
-
-// fixed-order block-wide fp64 sum (every thread gets the result)
 __device__ double block_sum(double v, double *sh) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nwv = blockDim.x >> 6;
 #pragma unroll
@@ -130,8 +129,14 @@ __device__ __forceinline__ double rowsum16_f64(double v) {
     v += dpp64<0x128>(v);   // row_ror 8
     return v;
 }
-// block-wide fp64 sums of K values with ONE barrier: DPP row sums, then every thread adds the
-// (waves x 4 rows) partials from LDS in a fixed order.  sh must hold K * 4 * waves doubles and
+__device__ __forceinline__ double readlane64(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// block-wide fp64 sums of K values with ONE barrier: DPP row sums, the (waves x 4 rows) partials
+// through LDS, then every wave sums them again with DPP rows + 4 lane reads -- the same fixed
+// order in every wave and block.  Blocks of <= 16 waves.  sh must hold K * 4 * waves doubles and
 // must not be reused by another call before the block passes another barrier.
 template <int K>
 __device__ __forceinline__ void block_sums_dpp(double (&v)[K], double *sh) {
@@ -143,11 +148,13 @@ __device__ __forceinline__ void block_sums_dpp(double (&v)[K], double *sh) {
         for (int k = 0; k < K; ++k) sh[k * nr + w * 4 + (lane >> 4)] = v[k];
     }
     __syncthreads();
+    double t[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) t[k] = sh[k * nr + min(lane, nr - 1)];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        double t = 0.0;
-        for (int j = 0; j < nr; ++j) t += sh[k * nr + j];
-        v[k] = t;
+        const double u = rowsum16_f64(lane < nr ? t[k] : 0.0);
+        v[k] = (readlane64(u, 0) + readlane64(u, 16)) + (readlane64(u, 32) + readlane64(u, 48));
     }
 }
 
@@ -453,7 +460,7 @@ __global__ void __launch_bounds__((64 * FastCfg<T0, T1, T2, T3>::WAVES))
 fvp_mlp3_kernel(IterArgs A, Net net) {
     using C = FastCfg<T0, T1, T2, T3>;
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    __shared__ double sh64[12 * C::WAVES];      // 1 + 2 DPP block sums, 4 rows per wave
+    __shared__ double sh64[20 * C::WAVES];      // 5 DPP block sums, 4 rows per wave
     float *tw = lds;                                   // theta pack
     float *vw = lds + C::TLEN;                         // v pack (fragment order, fp32)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -493,7 +500,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
     // CG state for the fused update (src/TRPO_CG.c:77-103), loaded in the same round
     double pv[C::EMAX], rv[C::EMAX], zv[C::EMAX], xv[C::EMAX];
     int vm[C::VEMAX];
-    CgSt sin = {0.0, 0, 0};
+    CgSt sin = {0.0, 0.0, 0, 0};
     double cn = 1.0, clam = 0.0, cth = 0.0;
     int cmax = 0;
     if (upd) {
@@ -541,29 +548,30 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
     if (upd) {
         // every block runs the identical fp64 CG step (fixed-order sums => bitwise-equal
         // results in all blocks); block 0 publishes the new state
-        double pz = 0.0;
+        // ONE block reduction per step: p.z, r.z, z.z, x.p, p.p; then |r'|^2 = |r|^2 - 2a r.z + a^2 z.z
+        // and |x'|^2 = |x|^2 + 2a x.p + a^2 p.p in fp64 (algebraically the reference's r.r / x.x)
+        double red[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int e = 0; e < C::EMAX; ++e) {
             const int q = tid + e * C::THREADS;
             zv[e] = (q < A.nw ? zv[e] / cn : 2.0 * pv[e]) + clam * pv[e];
-            pz += pv[e] * zv[e];
+            red[0] += pv[e] * zv[e];
+            red[1] += rv[e] * zv[e];
+            red[2] += zv[e] * zv[e];
+            red[3] += xv[e] * pv[e];
+            red[4] += pv[e] * pv[e];
         }
         STAMP(8);
-        double red1[1] = {pz};
-        block_sums_dpp<1>(red1, sh64);
+        block_sums_dpp<5>(red, sh64);
         STAMP(9);
-        const double alpha = sin.rdotr / red1[0];
-        double rr = 0.0, xx = 0.0;
+        const double alpha = sin.rdotr / red[0];
 #pragma unroll
         for (int e = 0; e < C::EMAX; ++e) {
             rv[e] -= alpha * zv[e];
-            rr += rv[e] * rv[e];
             xv[e] += alpha * pv[e];
-            xx += xv[e] * xv[e];
         }
-        double red2[2] = {rr, xx};
-        block_sums_dpp<2>(red2, sh64 + 4 * C::WAVES);
-        const double nr = red2[0], xn2 = red2[1];
+        const double nr = sin.rdotr - 2.0 * alpha * red[1] + alpha * alpha * red[2];
+        const double xn2 = sin.xx + 2.0 * alpha * red[3] + alpha * alpha * red[4];
         STAMP(10);
         const double beta = nr / sin.rdotr;
         double *stage = reinterpret_cast<double *>(lds + C::TLEN + C::VLEN);
@@ -584,6 +592,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
         const int done = (nr < cth || it >= cmax) ? 1 : 0;
         if (blockIdx.x == 0 && tid == 0) {
             A.st_out->rdotr = nr;
+            A.st_out->xx = xn2;
             A.st_out->iter = it;
             A.hist[2 * it] = nr;
             A.hist[2 * it + 1] = sqrt(xn2);
@@ -1147,6 +1156,7 @@ cg_init_kernel(const double *__restrict__ b, double *x, double *r, double *p, in
         ctl->rdotr = rr;
         ctl->iter = 0;
         st->rdotr = rr;
+        st->xx = 0.0;
         st->iter = 0;
         hist[0] = rr;
         hist[1] = 0.0;
@@ -1214,6 +1224,7 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
     if (threadIdx.x == 0) {
         const int it = sin.iter + 1;
         st_out->rdotr = nr;
+        st_out->xx = xn;
         st_out->iter = it;
         ctl->iter = it;
         ctl->rdotr = nr;
