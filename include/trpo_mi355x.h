@@ -12,6 +12,8 @@
  *   CG             <- src/include/TRPO.h:96     (impl. src/TRPO_CG.c:11-113)
  *   FVP_FPGA       <- src/include/TRPO.h:98     (accelerator twin, same signature)
  *   CG_FPGA        <- src/include/TRPO.h:101    (accelerator twin, same signature)
+ *   TRPO_Update    <- src/include/TRPO.h:104    (impl. src/TRPO_Update.c:10-1011: policy
+ *                     gradient, CG step, FVP(x) step size, backtracking line search)
  *
  * Same prototypes, same by-value TRPOparam, same ownership (caller owns Input/b
  * and Result, fp64, length NumParamsCalc()), same return convention (elapsed
@@ -57,6 +59,7 @@ double FVPFast(TRPOparam param, double *Result, double *Input, size_t NumThreads
 double CG(TRPOparam param, double *Result, double *b, size_t MaxIter, double ResidualTh, size_t NumThreads);
 double FVP_FPGA(TRPOparam param, double *Result, double *Input);
 double CG_FPGA(TRPOparam param, double *Result, double *b, size_t MaxIter, double ResidualTh, size_t NumThreads);
+double TRPO_Update(TRPOparam param, double *Result, size_t NumThreads);
 #endif
 
 /* ------------------------------------------------------------------------- */
@@ -119,6 +122,32 @@ int trpo_ctx_synchronize(trpo_ctx *ctx);
 double trpo_ctx_time(trpo_ctx *ctx, int what, int reps, size_t max_iter, double residual_th);
 int trpo_ctx_download_x(trpo_ctx *ctx, double *x);
 int trpo_ctx_download_z(trpo_ctx *ctx, double *z);
+
+/* One TRPO policy update on the context's samples (src/TRPO_Update.c:254-1007):
+ * policy gradient b from the rollout, CG (F + damping I) x = b, shs = x.Fx / 2,
+ * lagrange = sqrt(shs / max_kl), fullstep = x / lagrange, backtracking line search
+ * over step fractions 0.5^k (k < max_backtracks) accepting the first with
+ * ratio > accept_ratio and positive improvement.  theta_out receives the new
+ * parameters -- or, as in the reference, the CG step direction x itself when no
+ * step fraction is accepted (src/TRPO_Update.c:850-852).  b_out / x_out / info may
+ * be NULL.  Requires trpo_ctx_set_rollout() for the current samples.  verbose != 0
+ * prints the reference's stdout lines (CG Iter, shs, lagrange multiplier, fval
+ * before, a/e/r).  Returns elapsed seconds or a negative error code. */
+#define TRPO_MAX_BACKTRACKS 32
+typedef struct {
+    double shs, lagrange, gnorm, fval_before, expected_improve_rate;
+    int evaluated;           /* step fractions evaluated (printed) */
+    int accepted;            /* accepted k (step fraction 0.5^k), or -1 */
+    double actual[TRPO_MAX_BACKTRACKS], expected[TRPO_MAX_BACKTRACKS], ratio[TRPO_MAX_BACKTRACKS];
+    size_t cg_iters;
+} trpo_update_info;
+
+/* Rollout of this rank's samples for the update: mean [n][A] (the policy mean the
+ * actions were drawn with), action [n][A], adv [n]. */
+int trpo_ctx_set_rollout(trpo_ctx *ctx, const double *mean, const double *action, const double *adv);
+double trpo_ctx_update(trpo_ctx *ctx, size_t cg_max_iter, double cg_residual_th, double max_kl,
+                       int max_backtracks, double accept_ratio, double *theta_out, double *b_out,
+                       double *x_out, trpo_update_info *info, int verbose);
 
 /* Introspection: which kernel family serves this context ("mfma-mlp3 T0xT1xT2xT3"
  * or "generic"), and the FVP launch geometry. */

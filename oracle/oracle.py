@@ -45,6 +45,17 @@ def lib():
         L.oracle_load_data.argtypes = [C.c_char_p, C.c_size_t, _sp, C.c_size_t, _dp, _dp, C.c_void_p]
         L.oracle_forward.restype = C.c_int
         L.oracle_forward.argtypes = [C.c_size_t, _sp, C.c_char_p, _dp, _dp, C.c_size_t, _dp]
+        L.oracle_policy_grad.restype = C.c_int
+        L.oracle_policy_grad.argtypes = [C.c_size_t, _sp, C.c_char_p, _dp, _dp, _dp, _dp, _dp, C.c_size_t, C.c_int,
+                                         _dp, C.POINTER(C.c_double)]
+        L.oracle_surrogate_sum.restype = C.c_double
+        L.oracle_surrogate_sum.argtypes = [C.c_size_t, _sp, C.c_char_p, _dp, _dp, _dp, _dp, _dp, _dp, C.c_size_t]
+        L.oracle_update.restype = C.c_double
+        L.oracle_update.argtypes = [C.c_size_t, _sp, C.c_char_p, _dp, _dp, _dp, _dp, _dp, _dp, C.c_size_t,
+                                    C.c_double, C.c_size_t, C.c_double, C.c_double, C.c_int, C.c_double,
+                                    _dp, _dp, _dp, _dp, _dp, C.POINTER(C.c_int), C.c_int]
+        L.oracle_load_rollout.restype = C.c_int
+        L.oracle_load_rollout.argtypes = [C.c_char_p, C.c_size_t, _sp, C.c_size_t, _dp, _dp, _dp, _dp, _dp]
         _lib = L
     return _lib
 
@@ -108,3 +119,54 @@ def forward(layers, acfunc, theta, obs):
     lib().oracle_forward(len(layers), _ls(layers), acfunc.encode(), np.ascontiguousarray(theta, np.float64), obs,
                          obs.shape[0], out)
     return out
+
+
+def _f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def policy_grad(layers, acfunc, theta, obs, mean, action, adv, normalise=True):
+    """src/TRPO_Update.c:254-378.  Returns (b, sum(adv))."""
+    obs = _f64(obs)
+    b = np.zeros(num_params(layers))
+    s = C.c_double(0.0)
+    lib().oracle_policy_grad(len(layers), _ls(layers), acfunc.encode(), _f64(theta), obs, _f64(mean), _f64(action),
+                             _f64(adv), obs.shape[0], 1 if normalise else 0, b, C.byref(s))
+    return b, s.value
+
+
+def surrogate_sum(layers, acfunc, theta_new, obs, mean, action, adv, std):
+    """sum_n Adv_n exp(LLD_n) (src/TRPO_Update.c:951-981)."""
+    obs = _f64(obs)
+    return lib().oracle_surrogate_sum(len(layers), _ls(layers), acfunc.encode(), _f64(theta_new), obs, _f64(mean),
+                                      _f64(action), _f64(adv), _f64(std), obs.shape[0])
+
+
+def update(layers, acfunc, theta, obs, mean, action, adv, std, damping=0.1, maxiter=10, resth=1e-10, max_kl=0.01,
+           max_bt=10, accept=0.1, verbose=False):
+    """One TRPO_Update (src/TRPO_Update.c:10-1011).  Returns a dict."""
+    obs = _f64(obs)
+    P = num_params(layers)
+    th, b, x = np.zeros(P), np.zeros(P), np.zeros(P)
+    scal = np.zeros(6)
+    are = np.zeros(3 * max(max_bt, 1))
+    ev = C.c_int(0)
+    t = lib().oracle_update(len(layers), _ls(layers), acfunc.encode(), _f64(theta), obs, _f64(mean), _f64(action),
+                            _f64(adv), _f64(std), obs.shape[0], damping, maxiter, resth, max_kl, max_bt, accept,
+                            th, b, x, scal, are, C.byref(ev), 1 if verbose else 0)
+    if t < 0:
+        raise RuntimeError("oracle_update failed")
+    k = ev.value
+    return dict(theta=th, b=b, x=x, shs=scal[0], lagrange=scal[1], gnorm=scal[2], fval=scal[3], rate=scal[4],
+                accepted=int(scal[5]), evaluated=k, actual=are[0:3 * k:3], expected=are[1:3 * k:3],
+                ratio=are[2:3 * k:3], seconds=t)
+
+
+def load_rollout(path, layers, n):
+    """Every column of a data file: (obs, std_of_last_line, mean, action, adv)."""
+    A = layers[-1]
+    obs, std = np.zeros((n, layers[0])), np.zeros(A)
+    mean, action, adv = np.zeros((n, A)), np.zeros((n, A)), np.zeros(n)
+    if lib().oracle_load_rollout(path.encode(), len(layers), _ls(layers), n, obs, std, mean, action, adv):
+        raise IOError(path)
+    return obs, std, mean, action, adv

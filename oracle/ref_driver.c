@@ -1,8 +1,8 @@
 /*
  * ref_driver.c -- TEST INFRASTRUCTURE ONLY (our own main, not reference code).
  *
- * Drives the reference's UNCHANGED src/TRPO_FVP.c, src/TRPO_CG.c and
- * src/TRPO_Util.c, compiled straight from /root/reference by oracle/Makefile
+ * Drives the reference's UNCHANGED src/TRPO_FVP.c, src/TRPO_CG.c,
+ * src/TRPO_Util.c and src/TRPO_Update.c, compiled straight from /root/reference by oracle/Makefile
  * into oracle/_ref/.  Used (a) by tests/golden/make_goldens.py to produce the
  * golden vectors committed under tests/golden/, and (b) by bench.py's
  * cpu_baseline leg ("kind": "reference") when oracle/_ref/ is present.
@@ -10,6 +10,7 @@
  *   ref_driver fvp  MODEL DATA N LAYERS ACFUNC DAMPING VIN  OUT [THREADS]
  *   ref_driver cg   MODEL DATA N LAYERS ACFUNC DAMPING BIN  MAXITER RESTH OUT [THREADS]
  *   ref_driver time MODEL DATA N LAYERS ACFUNC DAMPING BIN  MAXITER RESTH [THREADS]
+ *   ref_driver update MODEL DATA N LAYERS ACFUNC DAMPING OUT [THREADS]
  *
  * LAYERS is a comma list (e.g. 15,16,16,3); ACFUNC a string (e.g. lttl).
  * Vectors are text, one %.17g value per line.  The reference's own stdout
@@ -79,6 +80,12 @@ int main(int argc, char **argv) {
     prm.CG_Damping = atof(argv[7]);
     const size_t P = NumParamsCalc(ls, prm.NumLayers);
     double *in = calloc(P, sizeof(double)), *out = calloc(P, sizeof(double));
+    if (!strcmp(mode, "update")) {       /* TRPO_Update prints shs / lagrange / a/e/r itself */
+        size_t th = argc > 9 ? (size_t)atoi(argv[9]) : 1;
+        double t = TRPO_Update(prm, out, th);
+        if (t < 0) return 1;
+        return write_vec(argv[8], out, P) ? 1 : 0;
+    }
     if (read_vec(argv[8], in, P)) {
         fprintf(stderr, "cannot read %s\n", argv[8]);
         return 1;

@@ -25,6 +25,11 @@
  *   - CG loop, test at the top, <= MaxIter FVPs, prints rdotr/|x|
  *                                          src/TRPO_CG.c:11-113
  *   - NumParamsCalc                        src/TRPO_Util.c:7-17
+ *   - TRPO_Update: policy gradient         src/TRPO_Update.c:254-378
+ *                  CG (inlined copy)       src/TRPO_Update.c:383-628
+ *                  FVP(x), shs, lagrange   src/TRPO_Update.c:633-866
+ *                  line search             src/TRPO_Update.c:868-1007
+ *                  (theta starts as the CG step x: :850-852 quirk kept)
  */
 #include <math.h>
 #include <stdint.h>
@@ -335,4 +340,235 @@ int oracle_forward(size_t nl, const size_t *ls, const char *ac, const double *th
     free(a);
     free(b);
     return 0;
+}
+
+/* ------------------------------------------------------------------------- */
+/* TRPO_Update (src/TRPO_Update.c:10-1011)                                   */
+/* ------------------------------------------------------------------------- */
+static void or_layers(size_t nl, const size_t *ls, const double *theta, const double **W, const double **B,
+                      size_t *P) {
+    size_t pos = 0;
+    for (size_t i = 0; i + 1 < nl; ++i) {
+        W[i] = theta + pos;
+        pos += ls[i] * ls[i + 1];
+        B[i] = theta + pos;
+        pos += ls[i + 1];
+    }
+    *P = pos + ls[nl - 1];
+}
+
+/* y[i] = activations of layer i for one sample (src/TRPO_Update.c:262-293) */
+static void or_forward1(size_t nl, const size_t *ls, const char *ac, const double *const *W,
+                        const double *const *B, const double *x_in, double **y) {
+    for (size_t i = 0; i < ls[0]; ++i) y[0][i] = x_in[i];
+    for (size_t i = 0; i + 1 < nl; ++i) {
+        for (size_t j = 0; j < ls[i + 1]; ++j) {
+            double v = B[i][j];
+            for (size_t k = 0; k < ls[i]; ++k) v += y[i][k] * W[i][k * ls[i + 1] + j];
+            switch (ac[i + 1]) {
+            case 't': v = tanh(v); break;
+            case 'o': v = 0.1 * v; break;
+            case 's': v = 1.0 / (1 + exp(-v)); break;
+            default: break;
+            }
+            y[i + 1][j] = v;
+        }
+    }
+}
+
+/* Policy gradient (src/TRPO_Update.c:254-378).  Rollout: mean/action [n][A], adv [n].
+ * normalise != 0 divides by n like the reference; 0 leaves the plain sum (for sharded
+ * use).  adv_sum (may be NULL) receives sum(adv) in sample order. */
+int oracle_policy_grad(size_t nl, const size_t *ls, const char *ac, const double *theta, const double *obs,
+                       const double *mean, const double *action, const double *adv, size_t n, int normalise,
+                       double *b, double *adv_sum) {
+    if (nl < 2 || nl > OR_MAX_LAYERS) return -1;
+    const double *W[OR_MAX_LAYERS], *B[OR_MAX_LAYERS];
+    size_t P;
+    or_layers(nl, ls, theta, W, B, &P);
+    const size_t A = ls[nl - 1];
+    const double *logstd = theta + P - A;
+    size_t maxw = 0;
+    for (size_t i = 0; i < nl; ++i) maxw = ls[i] > maxw ? ls[i] : maxw;
+    double *buf = (double *)calloc(2 * nl * maxw + A, sizeof(double));
+    double *y[OR_MAX_LAYERS], *g[OR_MAX_LAYERS];
+    for (size_t i = 0; i < nl; ++i) {
+        y[i] = buf + (2 * i) * maxw;
+        g[i] = buf + (2 * i + 1) * maxw;
+    }
+    double *gls = buf + 2 * nl * maxw;
+    memset(b, 0, P * sizeof(double));
+    double as = 0;
+    for (size_t s = 0; s < n; ++s) {
+        or_forward1(nl, ls, ac, W, B, obs + s * ls[0], y);
+        for (size_t i = 0; i < A; ++i) {                             /* :297-303 */
+            double temp = (action[s * A + i] - mean[s * A + i]) / exp(logstd[i]);
+            g[nl - 1][i] = adv[s] * temp / exp(logstd[i]);
+            gls[i] = adv[s] * (temp * temp - 1);
+        }
+        size_t pos = P - A;
+        for (size_t i = nl - 1; i > 0; --i) {                        /* :305-357 */
+            for (size_t j = 0; j < ls[i]; ++j) {
+                switch (ac[i]) {
+                case 't': g[i][j] = g[i][j] * (1 - y[i][j] * y[i][j]); break;
+                case 'o': g[i][j] = 0.1 * g[i][j]; break;
+                case 's': g[i][j] = g[i][j] * y[i][j] * (1 - y[i][j]); break;
+                default: break;
+                }
+            }
+            /* accumulate GW[i-1], GB[i-1] at their flat positions (:361-372) */
+            pos -= ls[i - 1] * ls[i] + ls[i];
+            for (size_t j = 0; j < ls[i - 1]; ++j)
+                for (size_t k = 0; k < ls[i]; ++k) b[pos + j * ls[i] + k] += g[i][k] * y[i - 1][j];
+            for (size_t k = 0; k < ls[i]; ++k) b[pos + ls[i - 1] * ls[i] + k] += g[i][k];
+            for (size_t j = 0; j < ls[i - 1]; ++j) {
+                double t = 0;
+                for (size_t k = 0; k < ls[i]; ++k) t += g[i][k] * W[i - 1][j * ls[i] + k];
+                g[i - 1][j] = t;
+            }
+        }
+        for (size_t k = 0; k < A; ++k) b[P - A + k] += gls[k];
+        as += adv[s];
+    }
+    if (normalise)
+        for (size_t i = 0; i < P; ++i) b[i] = b[i] / (double)n;
+    if (adv_sum) *adv_sum = as;
+    free(buf);
+    return 0;
+}
+
+/* sum_n Adv_n exp(LLD_n) for parameters theta_new (src/TRPO_Update.c:951-981);
+ * stdv = the data file's Std. */
+double oracle_surrogate_sum(size_t nl, const size_t *ls, const char *ac, const double *theta_new,
+                            const double *obs, const double *mean, const double *action, const double *adv,
+                            const double *stdv, size_t n) {
+    const double *W[OR_MAX_LAYERS], *B[OR_MAX_LAYERS];
+    size_t P;
+    or_layers(nl, ls, theta_new, W, B, &P);
+    const size_t A = ls[nl - 1];
+    const double *logstd = theta_new + P - A;
+    size_t maxw = 0;
+    for (size_t i = 0; i < nl; ++i) maxw = ls[i] > maxw ? ls[i] : maxw;
+    double *buf = (double *)calloc(nl * maxw, sizeof(double));
+    double *y[OR_MAX_LAYERS];
+    for (size_t i = 0; i < nl; ++i) y[i] = buf + i * maxw;
+    double surr = 0;
+    for (size_t s = 0; s < n; ++s) {
+        or_forward1(nl, ls, ac, W, B, obs + s * ls[0], y);
+        double lld = 0;
+        for (size_t i = 0; i < A; ++i) {
+            double tx = (action[s * A + i] - mean[s * A + i]) / stdv[i];
+            double tn = (action[s * A + i] - y[nl - 1][i]) / exp(logstd[i]);
+            lld += tx * tx - tn * tn + log(stdv[i]) - logstd[i];
+        }
+        lld = lld * 0.5;
+        surr += exp(lld) * adv[s];
+    }
+    free(buf);
+    return surr;
+}
+
+/* One TRPO update (src/TRPO_Update.c:10-1011) with explicit settings (the reference
+ * hard-wires maxiter 10, resth 1e-10, max_kl 0.01, max_bt 10, accept 0.1).  Outputs:
+ * theta_out [P]; b_out / x_out [P] (policy gradient, CG step; may be NULL); scal[6] =
+ * {shs, lagrange, gnorm, fval_before, expected_improve_rate, accepted k or -1};
+ * are[3*max_bt] = actual/expected/ratio per evaluated backtrack; *evaluated. */
+double oracle_update(size_t nl, const size_t *ls, const char *ac, const double *theta, const double *obs,
+                     const double *mean, const double *action, const double *adv, const double *stdv, size_t n,
+                     double damping, size_t maxiter, double resth, double max_kl, int max_bt, double accept,
+                     double *theta_out, double *b_out, double *x_out, double *scal, double *are, int *evaluated,
+                     int verbose) {
+    const size_t P = oracle_num_params(ls, nl);
+    double *b = (double *)calloc(P, sizeof(double)), *x = (double *)calloc(P, sizeof(double));
+    double *z = (double *)calloc(P, sizeof(double)), *fullstep = (double *)calloc(P, sizeof(double));
+    double *xnew = (double *)calloc(P, sizeof(double));
+    double t0 = or_now(), adv_sum = 0;
+    oracle_policy_grad(nl, ls, ac, theta, obs, mean, action, adv, n, 1, b, &adv_sum);
+    if (oracle_cg(nl, ls, ac, theta, obs, n, stdv, damping, b, maxiter, resth, x, NULL, NULL, NULL, 1, verbose) < 0)
+        return -1;
+    oracle_fvp(nl, ls, ac, theta, obs, n, stdv, damping, x, z, 1);   /* :633-832 */
+    double shs = 0;
+    for (size_t i = 0; i < P; ++i) shs += z[i] * x[i];
+    shs = shs * 0.5;
+    if (verbose) printf("shs: %.14f\n", shs);
+    double lm = sqrt(shs / max_kl);
+    double gnorm = 0;
+    for (size_t i = 0; i < P; ++i) gnorm += b[i] * b[i];
+    gnorm = sqrt(gnorm);
+    if (verbose) printf("lagrange multiplier: %.14f, gnorm: %.14f\n", lm, gnorm);
+    for (size_t i = 0; i < P; ++i) fullstep[i] = x[i] / lm;
+    double neggdotstepdir = 0;
+    for (size_t i = 0; i < P; ++i) neggdotstepdir += b[i] * x[i];
+    for (size_t i = 0; i < P; ++i) theta_out[i] = x[i];
+    double rate = neggdotstepdir / lm;
+    double fval = -adv_sum / (double)n;
+    if (verbose) printf("fval before %.14e\n", fval);
+    int acc = -1, ev = 0;
+    for (int k = 0; k < max_bt; ++k) {
+        double stepfrac = pow(0.5, (double)k);
+        for (size_t i = 0; i < P; ++i) xnew[i] = theta[i] + stepfrac * fullstep[i];
+        double surr = oracle_surrogate_sum(nl, ls, ac, xnew, obs, mean, action, adv, stdv, n);
+        double newfval = -surr / (double)n;
+        double actual = fval - newfval, expected = rate * stepfrac, ratio = actual / expected;
+        if (verbose) printf("a/e/r %.14f / %.14f / %.14f\n", actual, expected, ratio);
+        if (are) {
+            are[3 * k] = actual;
+            are[3 * k + 1] = expected;
+            are[3 * k + 2] = ratio;
+        }
+        ev = k + 1;
+        if (ratio > accept && actual > 0) {
+            for (size_t i = 0; i < P; ++i) theta_out[i] = xnew[i];
+            acc = k;
+            break;
+        }
+    }
+    double t1 = or_now();
+    if (b_out) memcpy(b_out, b, P * sizeof(double));
+    if (x_out) memcpy(x_out, x, P * sizeof(double));
+    if (scal) {
+        scal[0] = shs;
+        scal[1] = lm;
+        scal[2] = gnorm;
+        scal[3] = fval;
+        scal[4] = rate;
+        scal[5] = acc;
+    }
+    if (evaluated) *evaluated = ev;
+    free(b); free(x); free(z); free(fullstep); free(xnew);
+    return t1 - t0;
+}
+
+/* Data file with every column (src/TRPO_Update.c:228-249); any output may be NULL. */
+int oracle_load_rollout(const char *path, size_t nl, const size_t *ls, size_t n, double *obs, double *stdv,
+                        double *mean, double *action, double *adv) {
+    FILE *f = fopen(path, "r");
+    if (!f) return -1;
+    const size_t O = ls[0], A = ls[nl - 1];
+    double tmp;
+    for (size_t s = 0; s < n; ++s) {
+        for (size_t j = 0; j < A; ++j) {
+            if (fscanf(f, "%lf", &tmp) != 1) goto bad;
+            if (mean) mean[s * A + j] = tmp;
+        }
+        for (size_t j = 0; j < A; ++j) {
+            if (fscanf(f, "%lf", &tmp) != 1) goto bad;
+            if (stdv) stdv[j] = tmp;
+        }
+        for (size_t j = 0; j < O; ++j) {
+            if (fscanf(f, "%lf", &tmp) != 1) goto bad;
+            if (obs) obs[s * O + j] = tmp;
+        }
+        for (size_t j = 0; j < A; ++j) {
+            if (fscanf(f, "%lf", &tmp) != 1) goto bad;
+            if (action) action[s * A + j] = tmp;
+        }
+        if (fscanf(f, "%lf", &tmp) != 1) goto bad;
+        if (adv) adv[s] = tmp;
+    }
+    fclose(f);
+    return 0;
+bad:
+    fclose(f);
+    return -1;
 }

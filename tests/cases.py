@@ -65,6 +65,33 @@ def inputs(c):
                 vin=synth.make_v(P) if c["vin"] == "v" else synth.make_b(P), damping=c["damping"])
 
 
+def synth_update_inputs(c):
+    """theta, obs, std, mean, action, adv of a synthetic TRPO_Update case."""
+    layers, acfunc, n = c["layers"], c["acfunc"], c["n"]
+    theta = synth.make_theta(layers)
+    theta[-layers[-1]:] = c["logstd"]
+    obs = synth.make_obs(n, layers[0])
+    std = np.asarray(c["std"], dtype=np.float64)
+    mean, action, adv = synth.make_rollout(layers, acfunc, theta, obs, std)
+    if c["adv"] == "neg_abs":
+        adv = -np.abs(adv)
+    return theta, obs, std, mean, action, adv
+
+
+def update_inputs(c):
+    """dict(layers, acfunc, theta, obs, std, mean, action, adv, damping) of an update case."""
+    if c["src"] == "fixture":
+        t = _read_table("ArmTestData.txt")[: c["n"]]
+        A, O = 3, 15
+        return dict(layers=ARM, acfunc="lttl", theta=fixture_model(), obs=np.ascontiguousarray(t[:, 2 * A:2 * A + O]),
+                    std=t[-1, A:2 * A].copy(), mean=np.ascontiguousarray(t[:, :A]),
+                    action=np.ascontiguousarray(t[:, 2 * A + O:3 * A + O]), adv=t[:, 3 * A + O].copy(),
+                    damping=c["damping"])
+    theta, obs, std, mean, action, adv = synth_update_inputs(c)
+    return dict(layers=c["layers"], acfunc=c["acfunc"], theta=theta, obs=obs, std=std, mean=mean, action=action,
+                adv=adv, damping=c["damping"])
+
+
 def expected(c):
     return np.loadtxt(os.path.join(GOLDEN, c["expected"]))
 

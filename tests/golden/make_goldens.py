@@ -2,7 +2,7 @@
 """Generate the golden vectors under tests/golden/ from the REFERENCE itself.
 
 Runs oracle/_ref/ref_driver -- the reference's unchanged src/TRPO_FVP.c,
-src/TRPO_CG.c and src/TRPO_Util.c compiled by oracle/Makefile (needs
+src/TRPO_CG.c, src/TRPO_Util.c and src/TRPO_Update.c compiled by oracle/Makefile (needs
 /root/reference; only ever run in the build container, never on the GPU box).
 
 Every case is described in manifest.json so that tests can rebuild the exact
@@ -26,11 +26,16 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, os.path.join(ROOT, "trpo-robot-control_amd"))
+sys.path.insert(0, os.path.dirname(HERE))
 from trpo_amd import synth  # noqa: E402
+from cases import synth_update_inputs  # noqa: E402
 
 DRIVER = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
 ARM = [15, 16, 16, 3]
 SIGMA3 = [0.6065306597126334, 0.8, 1.3]     # exp(-0.5) and two more, as exact literals
+# TRPO_Update with sigma != 1: model LogStd and the data file's Std (= exp(LogStd), literals)
+LOGSTD_U = [-0.5, 0.0, 0.25]
+SIGMA_U = [0.6065306597126334, 1.0, 1.2840254166877414]
 
 CASES = [
     # --- reference fixtures (build/ArmTest*.txt) ---
@@ -56,7 +61,19 @@ CASES = [
          std=[1.0, 1.0, 1.0], vin="b", maxiter=10, resth=0.0),
     dict(name="syn_2x64_cg_n50000", kind="cg", src="synth", layers=[15, 64, 64, 3], acfunc="lttl", n=50000,
          std=[1.0, 1.0, 1.0], vin="b", maxiter=10, resth=0.0),
+    # --- TRPO_Update (src/TRPO_Update.c; hard-wired CG 10 / 1e-10, MaxKL 0.01, 10 backtracks) ---
+    dict(name="fix_update_n3150", kind="update", src="fixture", n=3150),
+    dict(name="syn_update_arm_n20000", kind="update", src="synth", layers=ARM, acfunc="lttl", n=20000,
+         logstd=[0.0, 0.0, 0.0], std=[1.0, 1.0, 1.0], adv="normal"),
+    dict(name="syn_update_sigma_n5000", kind="update", src="synth", layers=ARM, acfunc="lttl", n=5000,
+         logstd=LOGSTD_U, std=SIGMA_U, adv="normal"),
+    dict(name="syn_update_2x64_n8192", kind="update", src="synth", layers=[15, 64, 64, 3], acfunc="lttl",
+         n=8192, logstd=[0.0, 0.0, 0.0], std=[1.0, 1.0, 1.0], adv="normal"),
+    # every backtrack rejected: the reference returns the CG step x itself (:850-852)
+    dict(name="syn_update_reject_n5000", kind="update", src="synth", layers=ARM, acfunc="lttl", n=5000,
+         logstd=[0.0, 0.0, 0.0], std=[1.0, 1.0, 1.0], adv="neg_abs"),
 ]
+
 
 
 def build_inputs(case, tmp):
@@ -79,7 +96,43 @@ def build_inputs(case, tmp):
     return model, data, layers, acfunc, vin
 
 
+def run_update_case(case, tmp):
+    if case["src"] == "fixture":
+        layers, acfunc = ARM, "lttl"
+        model, data = os.path.join(HERE, "ArmTestModel.txt"), os.path.join(HERE, "ArmTestData.txt")
+    else:
+        layers, acfunc = case["layers"], case["acfunc"]
+        theta, obs, std, mean, action, adv = synth_update_inputs(case)
+        model, data = os.path.join(tmp, case["name"] + ".model"), os.path.join(tmp, case["name"] + ".data")
+        synth.write_model_file(model, theta)
+        synth.write_data_file(data, obs, std, mean, action, adv)
+    out = os.path.join(HERE, case["name"] + ".txt")
+    lay = ",".join(str(x) for x in layers)
+    cmd = [DRIVER, "update", model, data, str(case["n"]), lay, acfunc, "0.1", out, "1"]
+    res = subprocess.run(cmd, capture_output=True, text=True, check=True)
+    rec = dict(case)
+    rec.update(layers=layers, acfunc=acfunc, damping=0.1, expected=os.path.basename(out))
+    hist = re.findall(r"CG Iter\[(\d+)\] Residual Norm=(\S+), Soln Norm=(\S+)", res.stdout)
+    rec["rdotr"] = [float(h[1]) for h in hist]
+    rec["iters"] = len(hist) - 1
+    rec["shs"] = float(re.search(r"shs: (\S+)", res.stdout).group(1))
+    m = re.search(r"lagrange multiplier: (\S+), gnorm: (\S+)", res.stdout)
+    rec["lagrange"], rec["gnorm"] = float(m.group(1)), float(m.group(2))
+    rec["fval"] = float(re.search(r"fval before (\S+)", res.stdout).group(1))
+    are = re.findall(r"a/e/r (\S+) / (\S+) / (\S+)", res.stdout)
+    rec["ratio"] = [float(a[2]) for a in are]
+    last_a, last_r = float(are[-1][0]), float(are[-1][2])
+    rec["accepted"] = len(are) - 1 if (last_r > 0.1 and last_a > 0) else -1
+    y = np.loadtxt(out)
+    rec["norm"] = float(np.linalg.norm(y))
+    print("%-24s P=%-5d |theta'|=%.15g accepted=%d" % (case["name"], len(y), rec["norm"], rec["accepted"]),
+          flush=True)
+    return rec
+
+
 def run_case(case, tmp):
+    if case["kind"] == "update":
+        return run_update_case(case, tmp)
     model, data, layers, acfunc, vin = build_inputs(case, tmp)
     vpath = os.path.join(tmp, case["name"] + ".in")
     synth.write_vector_file(vpath, vin)

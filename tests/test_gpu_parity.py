@@ -28,7 +28,7 @@ def _ctx(x, **kw):
     return trpo_amd.Context(x["layers"], x["acfunc"], x["theta"], x["obs"], x["std"], x["damping"], **kw)
 
 
-@pytest.mark.parametrize("name", [c["name"] for c in cases.manifest()])
+@pytest.mark.parametrize("name", [c["name"] for c in cases.manifest() if c["kind"] in ("fvp", "cg")])
 def test_context_matches_reference_golden(name):
     c = cases.case(name)
     x = cases.inputs(c)

@@ -1,0 +1,61 @@
+/*
+ * trpo_common.h -- definitions shared by the device translation units
+ * (trpo_kernels.hip: FVP / CG;  trpo_update.hip: the TRPO_Update path).
+ * Internal to libtrpo_mi355x.so; the public ABI is include/trpo_mi355x.h.
+ */
+#ifndef TRPO_COMMON_H
+#define TRPO_COMMON_H
+
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+
+#include "trpo_dev.h"
+
+#define MAXL 8
+
+enum { ACT_L = 0, ACT_T = 1, ACT_O = 2, ACT_S = 3 };
+
+// Network description in the reference's flat parameter layout
+// (src/TRPO_FVP.c:194-215): W[i] row-major [in][out] at woff[i], B[i] at boff[i],
+// LogStd[A] at P - A.
+struct Net {
+    int nl;
+    int L[MAXL];
+    int act[MAXL];
+    int P;
+    int woff[MAXL], boff[MAXL];
+    int A;
+};
+
+#define HCHK(x)                                                                            \
+    do {                                                                                   \
+        hipError_t e_ = (x);                                                               \
+        if (e_ != hipSuccess) {                                                            \
+            fprintf(stderr, "[trpo_mi355x] HIP error %s at %s:%d\n", hipGetErrorString(e_), \
+                    __FILE__, __LINE__);                                                   \
+            return -2;                                                                     \
+        }                                                                                  \
+    } while (0)
+
+static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+// What the TRPO_Update translation unit may see of a device context.
+struct trpo_dev_view {
+    int device;
+    hipStream_t stream;
+    Net net;
+    const double *theta64;     // natural theta (W, B, ..., LogStd), fp64
+    const double *std64;       // the data file's Std (FVP sigma), fp64 [A]
+    const double *obs64;       // local observations [n][L0], fp64
+    size_t n;                  // local samples
+    double n_total;            // global samples (all ranks)
+    double *vec_b;             // CG right-hand side slot (TRPO_VEC_B)
+};
+void trpo_dev_get_view(trpo_dev *d, trpo_dev_view *v);
+// in-place fp64 sum over the attached RCCL communicator (no-op without one)
+int trpo_dev_allreduce64(trpo_dev *d, double *buf, size_t count);
+// per-context storage of the update path (owned by trpo_update.hip)
+void **trpo_dev_update_state(trpo_dev *d);
+void trpo_update_state_free(void *state);
+
+#endif

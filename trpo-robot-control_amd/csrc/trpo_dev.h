@@ -42,9 +42,18 @@ int trpo_dev_sync(trpo_dev *d);
 /* what: 0 FVP kernel, 1 full FVP, 2 CG(maxiter) -- average ms over reps */
 double trpo_dev_time(trpo_dev *d, int what, int reps, size_t maxiter, double resth);
 
+/* TRPO_Update path (src/TRPO_Update.c), fp64.  Rollout = per local sample Mean[A],
+ * Action[A], Adv.  policy_gradient leaves b in slot B (and copies it / the global
+ * sum of Adv to the host when non-NULL); surrogate returns the global sums
+ * sum_n Adv exp(LLD) for candidates theta + 2^-k fullstep, k = k0 .. k0+nk-1. */
+int trpo_dev_set_rollout(trpo_dev *d, const double *mean, const double *action, const double *adv, size_t n);
+int trpo_dev_policy_gradient(trpo_dev *d, double *b_host, double *adv_sum);
+int trpo_dev_surrogate(trpo_dev *d, const double *fullstep, int k0, int nk, double *surr_host);
+
 const char *trpo_dev_kernel_name(const trpo_dev *d);
 int trpo_dev_geometry(const trpo_dev *d, int *blocks, int *threads, int *lds_bytes);
 size_t trpo_dev_num_params(const trpo_dev *d);
+double trpo_dev_n_total(const trpo_dev *d);    /* global sample count (all ranks) */
 
 #ifdef __cplusplus
 }

@@ -62,6 +62,8 @@ struct trpo_ctx {
     size_t P;
     size_t n;
     double damping;
+    double *theta;             /* host copy of the current parameters (line search base) */
+    int have_roll;             /* rollout uploaded for the current samples */
 };
 
 static int check_shape(size_t nl, const size_t *ls, const char *ac) {
@@ -98,6 +100,13 @@ trpo_ctx *trpo_ctx_create(size_t num_layers, const size_t *layer_size, const cha
         free(c);
         return NULL;
     }
+    c->theta = (double *)calloc(c->P, sizeof(double));
+    if (!c->theta) {
+        trpo_dev_destroy(c->dev);
+        free(c);
+        return NULL;
+    }
+    if (theta) memcpy(c->theta, theta, c->P * sizeof(double));
     if ((theta && trpo_dev_set_theta(c->dev, theta)) || (stdv && trpo_dev_set_std(c->dev, stdv)) ||
         ((obs || n == 0) && trpo_dev_set_obs(c->dev, obs, n)) || trpo_dev_set_damping(c->dev, cg_damping)) {
         set_err("device initialisation failed (theta/std/obs upload)");
@@ -112,17 +121,21 @@ trpo_ctx *trpo_ctx_create(size_t num_layers, const size_t *layer_size, const cha
 void trpo_ctx_destroy(trpo_ctx *c) {
     if (!c) return;
     trpo_dev_destroy(c->dev);
+    free(c->theta);
     free(c);
 }
 
 int trpo_ctx_set_theta(trpo_ctx *c, const double *theta) {
     if (!c || !theta) return TRPO_E_INVALID;
-    return trpo_dev_set_theta(c->dev, theta);
+    int rc = trpo_dev_set_theta(c->dev, theta);
+    if (!rc) memcpy(c->theta, theta, c->P * sizeof(double));
+    return rc;
 }
 int trpo_ctx_set_obs(trpo_ctx *c, const double *obs, size_t n) {
     if (!c || (!obs && n)) return TRPO_E_INVALID;
     int rc = trpo_dev_set_obs(c->dev, obs, n);
     if (!rc) c->n = n;
+    c->have_roll = 0;                  /* a rollout belongs to one set of samples */
     return rc;
 }
 int trpo_ctx_set_std(trpo_ctx *c, const double *stdv) {
@@ -189,6 +202,125 @@ int trpo_ctx_cg_history(const trpo_ctx *c, double *rdotr, double *xnorm, size_t 
     return trpo_dev_cg_history(c->dev, rdotr, xnorm, cap, iters);
 }
 
+/* ------------------------------------------------------------------------- */
+/* one TRPO policy update (src/TRPO_Update.c:254-1007)                       */
+/* ------------------------------------------------------------------------- */
+int trpo_ctx_set_rollout(trpo_ctx *c, const double *mean, const double *action, const double *adv) {
+    if (!c || (c->n && (!mean || !action || !adv))) return TRPO_E_INVALID;
+    int rc = trpo_dev_set_rollout(c->dev, mean, action, adv, c->n);
+    c->have_roll = rc == 0;
+    if (rc) set_err("rollout upload failed (code %d)", rc);
+    return rc;
+}
+
+static void print_cg_lines(trpo_ctx *c, size_t max_iter, size_t *iters_out) {
+    size_t iters = 0;
+    double *rr = (double *)malloc(sizeof(double) * (max_iter + 1));
+    double *xn = (double *)malloc(sizeof(double) * (max_iter + 1));
+    if (rr && xn && !trpo_dev_cg_history(c->dev, rr, xn, max_iter + 1, &iters)) {
+        for (size_t i = 0; i <= iters; ++i)
+            printf("CG Iter[%zu] Residual Norm=%.12e, Soln Norm=%.12e\n", i, rr[i], xn[i]);
+    }
+    if (iters_out) *iters_out = iters;
+    free(rr);
+    free(xn);
+}
+
+double trpo_ctx_update(trpo_ctx *c, size_t max_iter, double resth, double max_kl, int max_bt, double accept,
+                       double *theta_out, double *b_out, double *x_out, trpo_update_info *info, int verbose) {
+    if (!c || !theta_out || max_bt < 0 || max_bt > TRPO_MAX_BACKTRACKS || !(max_kl > 0)) return TRPO_E_INVALID;
+    if (!c->have_roll) {
+        set_err("trpo_ctx_update: no rollout for the current samples (trpo_ctx_set_rollout)");
+        return TRPO_E_INVALID;
+    }
+    const size_t P = c->P;
+    double *b = (double *)malloc(sizeof(double) * P), *x = (double *)malloc(sizeof(double) * P);
+    double *z = (double *)malloc(sizeof(double) * P), *fullstep = (double *)malloc(sizeof(double) * P);
+    trpo_update_info inf;
+    memset(&inf, 0, sizeof inf);
+    inf.accepted = -1;
+    double ret = TRPO_E_NOMEM;
+    if (!b || !x || !z || !fullstep) goto out;
+    const double t0 = now_s();
+    double adv_sum = 0.0;
+    int rc = trpo_dev_policy_gradient(c->dev, b, &adv_sum);                    /* :254-378 */
+    if (!rc) rc = trpo_dev_cg(c->dev, max_iter, resth);                         /* :383-628 */
+    if (!rc) rc = trpo_dev_download(c->dev, TRPO_VEC_X, x);
+    if (!rc && verbose) print_cg_lines(c, max_iter, &inf.cg_iters);
+    else if (!rc) trpo_dev_cg_history(c->dev, NULL, NULL, 0, &inf.cg_iters);
+    if (!rc) rc = trpo_dev_upload(c->dev, TRPO_VEC_V, x);                      /* :633-832 */
+    if (!rc) rc = trpo_dev_fvp(c->dev);
+    if (!rc) rc = trpo_dev_download(c->dev, TRPO_VEC_Z, z);
+    if (rc) {
+        set_err("TRPO update failed on the device (code %d)", rc);
+        ret = rc < 0 ? rc : TRPO_E_DEVICE;
+        goto out;
+    }
+    /* step size (src/TRPO_Update.c:834-868), fp64 on the host, reference order */
+    double shs = 0;
+    for (size_t i = 0; i < P; ++i) shs += z[i] * x[i];
+    shs = shs * 0.5;
+    if (verbose) printf("shs: %.14f\n", shs);
+    const double lm = sqrt(shs / max_kl);
+    double gnorm = 0;
+    for (size_t i = 0; i < P; ++i) gnorm += b[i] * b[i];
+    gnorm = sqrt(gnorm);
+    if (verbose) printf("lagrange multiplier: %.14f, gnorm: %.14f\n", lm, gnorm);
+    for (size_t i = 0; i < P; ++i) fullstep[i] = x[i] / lm;
+    double neggdotstepdir = 0;
+    for (size_t i = 0; i < P; ++i) neggdotstepdir += b[i] * x[i];
+    memcpy(theta_out, x, P * sizeof(double));        /* reference quirk: theta starts as x */
+    const double rate = neggdotstepdir / lm;
+    const double N = trpo_dev_n_total(c->dev);
+    const double fval = -adv_sum / N;
+    if (verbose) printf("fval before %.14e\n", fval);
+    inf.shs = shs;
+    inf.lagrange = lm;
+    inf.gnorm = gnorm;
+    inf.fval_before = fval;
+    inf.expected_improve_rate = rate;
+    /* backtracking line search (src/TRPO_Update.c:884-1007): fraction 1 alone first
+     * (the usual outcome), then every remaining fraction in one launch; the accepted
+     * one is the first in order, exactly as the sequential reference loop finds it */
+    for (int k0 = 0; k0 < max_bt && inf.accepted < 0;) {
+        const int nk = k0 == 0 ? 1 : max_bt - k0;
+        double surr[TRPO_MAX_BACKTRACKS];
+        rc = trpo_dev_surrogate(c->dev, fullstep, k0, nk, surr);
+        if (rc) {
+            set_err("line search failed on the device (code %d)", rc);
+            ret = rc < 0 ? rc : TRPO_E_DEVICE;
+            goto out;
+        }
+        for (int j = 0; j < nk; ++j) {
+            const int k = k0 + j;
+            const double stepfrac = pow(0.5, (double)k);
+            const double newfval = -surr[j] / N;
+            const double actual = fval - newfval, expected = rate * stepfrac, ratio = actual / expected;
+            if (verbose) printf("a/e/r %.14f / %.14f / %.14f\n", actual, expected, ratio);
+            inf.actual[k] = actual;
+            inf.expected[k] = expected;
+            inf.ratio[k] = ratio;
+            inf.evaluated = k + 1;
+            if (ratio > accept && actual > 0) {
+                for (size_t i = 0; i < P; ++i) theta_out[i] = c->theta[i] + stepfrac * fullstep[i];
+                inf.accepted = k;
+                break;
+            }
+        }
+        k0 += nk;
+    }
+    ret = now_s() - t0;
+    if (b_out) memcpy(b_out, b, P * sizeof(double));
+    if (x_out) memcpy(x_out, x, P * sizeof(double));
+    if (info) *info = inf;
+out:
+    free(b);
+    free(x);
+    free(z);
+    free(fullstep);
+    return ret;
+}
+
 int trpo_ctx_upload_b(trpo_ctx *c, const double *b) { return c ? trpo_dev_upload(c->dev, TRPO_VEC_B, b) : -1; }
 int trpo_ctx_upload_v(trpo_ctx *c, const double *v) { return c ? trpo_dev_upload(c->dev, TRPO_VEC_V, v) : -1; }
 int trpo_ctx_enqueue_fvp(trpo_ctx *c) { return c ? trpo_dev_fvp(c->dev) : -1; }
@@ -252,9 +384,11 @@ static int load_model(const char *path, size_t P, double *theta) {
     return 0;
 }
 
-/* Data file (src/TRPO_FVP.c:731-762): per sample Mean[A] Std[A] Obs[O] Action[A] Adv.
- * Keeps Obs, the Std of the last parsed line and (optionally) Mean. */
-static int load_data(const char *path, size_t O, size_t A, size_t n, double *obs, double *stdv, double *mean) {
+/* Data file (src/TRPO_FVP.c:731-762, src/TRPO_Update.c:228-249): per sample
+ * Mean[A] Std[A] Obs[O] Action[A] Adv.  Keeps Obs, the Std of the last parsed line
+ * and (each optionally) Mean, Action and Adv. */
+static int load_data(const char *path, size_t O, size_t A, size_t n, double *obs, double *stdv, double *mean,
+                     double *action, double *adv) {
     char *t = slurp(path, NULL);
     if (!t) {
         fprintf(stderr, "[ERROR] Cannot open Data File [%s]. \n", path);
@@ -280,6 +414,8 @@ static int load_data(const char *path, size_t O, size_t A, size_t n, double *obs
         if (mean) memcpy(mean + s * A, tmp, A * sizeof(double));
         memcpy(stdv, tmp + A, A * sizeof(double));
         memcpy(obs + s * O, tmp + 2 * A, O * sizeof(double));
+        if (action) memcpy(action + s * A, tmp + 2 * A + O, A * sizeof(double));
+        if (adv) adv[s] = tmp[3 * A + O];
     }
     free(tmp);
     free(t);
@@ -335,6 +471,7 @@ typedef struct {
     size_t nsamples, nl, ls[MAX_LAYERS];
     char ac[MAX_LAYERS + 1];
     trpo_ctx *ctx;
+    int has_roll;              /* Mean/Action/Adv uploaded (TRPO_Update) */
 } cache_entry;
 
 static cache_entry g_cache[CACHE_SLOTS];
@@ -357,9 +494,28 @@ void trpo_cache_clear(void) {
 
 static int same_ts(struct timespec a, struct timespec b) { return a.tv_sec == b.tv_sec && a.tv_nsec == b.tv_nsec; }
 
+/* Upload Mean/Action/Adv of the data file into a cached context (TRPO_Update). */
+static int load_rollout(cache_entry *e, const TRPOparam *prm) {
+    const size_t nl = prm->NumLayers, O = prm->LayerSize[0], A = prm->LayerSize[nl - 1], n = prm->NumSamples;
+    double *obs = (double *)calloc(n * O + 1, sizeof(double)), *stdv = (double *)calloc(A, sizeof(double));
+    double *mean = (double *)calloc(n * A + 1, sizeof(double)), *act = (double *)calloc(n * A + 1, sizeof(double));
+    double *adv = (double *)calloc(n + 1, sizeof(double));
+    int rc = -1;
+    if (obs && stdv && mean && act && adv && !load_data(prm->DataFile, O, A, n, obs, stdv, mean, act, adv))
+        rc = trpo_ctx_set_rollout(e->ctx, mean, act, adv);
+    if (!rc) e->has_roll = 1;
+    free(obs);
+    free(stdv);
+    free(mean);
+    free(act);
+    free(adv);
+    return rc;
+}
+
 /* Returns a context for param (parsing + uploading on a miss), or NULL with the
- * reference's "[ERROR] Cannot open ..." message on stderr. */
-static trpo_ctx *ctx_for_param(const TRPOparam *prm) {
+ * reference's "[ERROR] Cannot open ..." message on stderr.  need_roll: also make
+ * sure the rollout columns are on the device (TRPO_Update). */
+static trpo_ctx *ctx_for_param(const TRPOparam *prm, int need_roll) {
     if (!prm->ModelFile || !prm->DataFile) {
         fprintf(stderr, "[ERROR] Model/Data file name missing.\n");
         return NULL;
@@ -398,6 +554,7 @@ static trpo_ctx *ctx_for_param(const TRPOparam *prm) {
     }
     if (hit) {
         hit->stamp = ++g_clock;
+        if (need_roll && !hit->has_roll && load_rollout(hit, prm)) return NULL;
         return hit->ctx;
     }
     /* miss: parse both files, upload, replace the LRU slot */
@@ -414,7 +571,7 @@ static trpo_ctx *ctx_for_param(const TRPOparam *prm) {
     if (load_model(prm->ModelFile, P, theta)) goto out;
     /* FVPFast reads "LogStd" from the model into Std; the data file overwrites it */
     for (size_t k = 0; k < A; ++k) stdv[k] = theta[P - A + k];
-    if (load_data(prm->DataFile, O, A, n, obs, stdv, mean)) goto out;
+    if (load_data(prm->DataFile, O, A, n, obs, stdv, mean, NULL, NULL)) goto out;
     ctx = trpo_ctx_create(nl, prm->LayerSize, prm->AcFunc, theta, obs, n, stdv, prm->CG_Damping, -1);
     if (!ctx) {
         fprintf(stderr, "[ERROR] %s\n", g_err);
@@ -436,6 +593,8 @@ static trpo_ctx *ctx_for_param(const TRPOparam *prm) {
     memset(victim->ac, 0, sizeof victim->ac);
     memcpy(victim->ac, prm->AcFunc, nl);
     victim->ctx = ctx;
+    victim->has_roll = 0;
+    if (need_roll && load_rollout(victim, prm)) ctx = NULL;
 out:
     free(theta);
     free(obs);
@@ -454,7 +613,7 @@ double FVPFast(TRPOparam param, double *Result, double *Input, size_t NumThreads
     (void)NumThreads;
     if (!Result || !Input) return -1;
     pthread_mutex_lock(&g_lock);
-    trpo_ctx *c = ctx_for_param(&param);
+    trpo_ctx *c = ctx_for_param(&param, 0);
     double t = -1;
     if (c) {
         if (c->damping != param.CG_Damping) trpo_ctx_set_damping(c, param.CG_Damping);
@@ -482,7 +641,7 @@ double CG(TRPOparam param, double *Result, double *b, size_t MaxIter, double Res
     (void)NumThreads;
     if (!Result || !b) return -1;
     pthread_mutex_lock(&g_lock);
-    trpo_ctx *c = ctx_for_param(&param);
+    trpo_ctx *c = ctx_for_param(&param, 0);
     double t = -1;
     if (c) {
         if (c->damping != param.CG_Damping) trpo_ctx_set_damping(c, param.CG_Damping);
@@ -505,4 +664,28 @@ double FVP_FPGA(TRPOparam param, double *Result, double *Input) { return FVPFast
 
 double CG_FPGA(TRPOparam param, double *Result, double *b, size_t MaxIter, double ResidualTh, size_t NumThreads) {
     return CG(param, Result, b, MaxIter, ResidualTh, NumThreads);
+}
+
+/* src/TRPO_Update.c:10-1011 with its hard-wired settings: CG MaxIter 10 and
+ * ResidualTh 1e-10, MaxKL 0.01, 10 backtracks, AcceptRatio 0.1.  Result receives
+ * the updated parameters (or the CG step direction if no backtrack is accepted,
+ * like the reference).  The Std of the data file's last line is the FVP sigma;
+ * exp(LogStd) of the model is the policy sigma of the gradient and line search. */
+double TRPO_Update(TRPOparam param, double *Result, size_t NumThreads) {
+    (void)NumThreads;
+    if (!Result) return -1;
+    pthread_mutex_lock(&g_lock);
+    trpo_ctx *c = ctx_for_param(&param, 1);
+    double t = -1;
+    if (c) {
+        if (c->damping != param.CG_Damping) trpo_ctx_set_damping(c, param.CG_Damping);
+        t = trpo_ctx_update(c, 10, 1e-10, 0.01, 10, 0.1, Result, NULL, NULL, NULL, 1);
+        if (t < 0) {
+            fprintf(stderr, "[ERROR] %s\n", g_err);
+            t = -1;
+        }
+    }
+    fflush(stdout);
+    pthread_mutex_unlock(&g_lock);
+    return t;
 }

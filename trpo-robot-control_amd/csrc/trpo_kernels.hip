@@ -33,23 +33,12 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include "trpo_common.h"
 #include "trpo_dev.h"
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-#define MAXL 8
 #define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b), (c), 0, 0, 0)
-
-enum { ACT_L = 0, ACT_T = 1, ACT_O = 2, ACT_S = 3 };
-
-struct Net {
-    int nl;
-    int L[MAXL];
-    int act[MAXL];
-    int P;
-    int woff[MAXL], boff[MAXL];
-    int A;
-};
 
 // Fragment-order pack layout for the 3-weight-layer fast path (offsets in floats).
 struct Pack {
@@ -612,7 +601,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
     }
     __syncthreads();
     STAMP(1);
-    bool first_tile = true;
+    [[maybe_unused]] bool first_tile = true;
 
     const int a1 = ACT >= 0 ? (ACT & 3) : net.act[1];
     const int a2 = ACT >= 0 ? ((ACT >> 2) & 3) : net.act[2];
@@ -708,6 +697,12 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
 #pragma unroll
             for (int t = 0; t < NT; ++t) y1[t][ot] = act_fwd(a1, a[t], ra[t], r1[t][ot]);
         }
+#ifdef TRPO_STAMPS
+        if (first_tile) {
+            asm volatile("" ::"v"(y1[0][0]));
+            STAMP(13);
+        }
+#endif
         // ---- layer 1 ----
         f4 y2[NT][T2], r2[NT][T2];
 #pragma unroll
@@ -736,6 +731,12 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
 #pragma unroll
             for (int t = 0; t < NT; ++t) y2[t][ot] = act_fwd(a2, a[t], ra[t] + rb[t], r2[t][ot]);
         }
+#ifdef TRPO_STAMPS
+        if (first_tile) {
+            asm volatile("" ::"v"(y2[0][0]));
+            STAMP(14);
+        }
+#endif
         // ---- layer 2 (output) and G3 = act3'(Ry3 / sigma^2) ----
         f4 g3[NT][T3];
 #pragma unroll
@@ -771,7 +772,12 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
                 sB3[ot] += g3[t][ot];
             }
         }
-        if (first_tile) STAMP(2);
+#ifdef TRPO_STAMPS
+        if (first_tile) {
+            asm volatile("" ::"v"(g3[0][0]));
+            STAMP(2);
+        }
+#endif
         // ---- contraction RGW2 += Y2 . G3^T (K = 16 samples per tile) ----
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
@@ -817,6 +823,12 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
                 sB2[it] += g2[t][it];
             }
         }
+#ifdef TRPO_STAMPS
+        if (first_tile) {
+            asm volatile("" ::"v"(g2[0][0]));
+            STAMP(15);
+        }
+#endif
         // ---- contraction RGW1 += Y1 . G2^T ----
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
@@ -1304,6 +1316,8 @@ struct trpo_dev {
     size_t scratch_blocks;
     // common
     double *theta64;            // natural theta (device, fp64)
+    double *obs64;              // local observations [n][L0], fp64 (TRPO_Update path)
+    void *upd;                  // TRPO_Update path state (trpo_update.hip)
     double *std64;
     double *vec[5];             // V, Z, X, B, P
     double *r, *zacc;
@@ -1343,17 +1357,7 @@ static int act_code(char a) {
     }
 }
 
-#define HCHK(x)                                                                            \
-    do {                                                                                   \
-        hipError_t e_ = (x);                                                               \
-        if (e_ != hipSuccess) {                                                            \
-            fprintf(stderr, "[trpo_mi355x] HIP error %s at %s:%d\n", hipGetErrorString(e_), \
-                    __FILE__, __LINE__);                                                   \
-            return -2;                                                                     \
-        }                                                                                  \
-    } while (0)
 
-static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 extern "C" size_t trpo_dev_num_params(const trpo_dev *d) { return d ? (size_t)d->P : 0; }
 
@@ -1523,7 +1527,8 @@ extern "C" void trpo_dev_destroy(trpo_dev *d) {
     if (d->stream) hipStreamSynchronize(d->stream);
     if (d->cg_exec) hipGraphExecDestroy(d->cg_exec);
     if (d->comm) ncclCommDestroy(d->comm);
-    void *ptrs[] = {d->st, d->pbuf[0], d->pbuf[1], d->rbuf[0], d->rbuf[1], d->accbuf, d->imap, d->tpack, d->vpack, d->tmap, d->vmap, d->obs4, d->th32, d->v32, d->iv32, d->obs32, d->scratch,
+    trpo_update_state_free(d->upd);
+    void *ptrs[] = {d->obs64, d->st, d->pbuf[0], d->pbuf[1], d->rbuf[0], d->rbuf[1], d->accbuf, d->imap, d->tpack, d->vpack, d->tmap, d->vmap, d->obs4, d->th32, d->v32, d->iv32, d->obs32, d->scratch,
                     d->theta64, d->std64, d->r, d->zacc, d->slabs, d->ctl, d->hist};
     for (void *p : ptrs)
         if (p) hipFree(p);
@@ -1661,7 +1666,8 @@ extern "C" int trpo_dev_set_obs(trpo_dev *d, const double *obs, size_t n) {
     }
     HCHK(hipGetLastError());
     HCHK(hipStreamSynchronize(d->stream));
-    if (tmp) hipFree(tmp);
+    if (d->obs64) hipFree(d->obs64);
+    d->obs64 = tmp;                                    // kept in fp64 for the TRPO_Update path
     if (d->cg_exec) {     // geometry may have changed: recapture next time
         hipGraphExecDestroy(d->cg_exec);
         d->cg_exec = NULL;
@@ -2005,3 +2011,24 @@ extern "C" int trpo_dev_geometry(const trpo_dev *d, int *blocks, int *threads, i
     if (lds_bytes) *lds_bytes = d->fast ? d->fast->lds : 0;
     return 0;
 }
+
+// ---------------------------------------------------------------------------
+// internal accessors for trpo_update.hip (trpo_common.h)
+// ---------------------------------------------------------------------------
+void trpo_dev_get_view(trpo_dev *d, trpo_dev_view *v) {
+    v->device = d->device;
+    v->stream = d->stream;
+    v->net = d->net;
+    v->theta64 = d->theta64;
+    v->std64 = d->std64;
+    v->obs64 = d->obs64;
+    v->n = d->n;
+    v->n_total = d->n_total;
+    v->vec_b = d->vec[TRPO_VEC_B];
+}
+
+int trpo_dev_allreduce64(trpo_dev *d, double *buf, size_t count) { return allreduce(d, buf, count); }
+
+void **trpo_dev_update_state(trpo_dev *d) { return &d->upd; }
+
+extern "C" double trpo_dev_n_total(const trpo_dev *d) { return d ? d->n_total : 0.0; }

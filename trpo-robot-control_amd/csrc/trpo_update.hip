@@ -1,0 +1,372 @@
+// trpo_update.hip -- gfx950 kernels for the rest of one TRPO policy update
+// (reference src/TRPO_Update.c), around the FVP/CG solve of trpo_kernels.hip:
+//
+//   * policy gradient b = (1/N) sum_n grad_theta [ Adv_n * loglik ]   (:254-378)
+//       output seed  G = Adv (Action - Mean) / sigma^2,  sigma = exp(LogStd)
+//       LogStd part  Adv ((Action - Mean)^2 / sigma^2 - 1)
+//       then ordinary backprop through the policy MLP;
+//   * surrogate sums for the backtracking line search               (:951-981)
+//       surr_k = sum_n Adv_n exp(0.5 sum_i [tx^2 - tn^2 + log Std_i - LogStd'_i])
+//       for candidates theta_k = theta + 2^-k fullstep, several k per launch.
+//
+// Both run once per update (not per CG iteration), so they are written for
+// fidelity first: fp64 throughout, one sample per lane, 64-sample passes per
+// one-wave workgroup, the pass's activations staged in LDS ([row][64], up to
+// 160 KB; a global scratch beyond that), weights read with wave-uniform scalar
+// loads.  Cross-sample sums are fixed-order (lane order within a pass, block
+// order across blocks), so results are deterministic; multi-GPU ranks add their
+// shard sums with one RCCL all-reduce.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "trpo_common.h"
+
+constexpr int UT = 64;                     // samples per pass == threads per workgroup
+constexpr int LDS_CAP = 160 * 1024;        // gfx950 LDS per workgroup
+
+struct UpdState {
+    double *roll = nullptr;                // [n][2A+1]: Mean[A], Action[A], Adv
+    size_t roll_cap = 0, roll_n = 0;
+    int have_roll = 0;
+    double *ws = nullptr;                  // global activation scratch (big nets only)
+    size_t ws_cap = 0;
+    double *slabs = nullptr;               // per-block partial sums
+    size_t slab_cap = 0;
+    double *sum = nullptr;                 // [P + 1]
+    double *fs = nullptr;                  // fullstep [P]
+    double *sums = nullptr;                // [64]
+    int lds_set = 0;
+};
+
+void trpo_update_state_free(void *state) {
+    UpdState *u = (UpdState *)state;
+    if (!u) return;
+    void *ptrs[] = {u->roll, u->ws, u->slabs, u->sum, u->fs, u->sums};
+    for (void *p : ptrs)
+        if (p) hipFree(p);
+    delete u;
+}
+
+__device__ __forceinline__ double act_y64(int a, double x) {
+    switch (a) {
+    case ACT_T: return tanh(x);
+    case ACT_O: return 0.1 * x;
+    case ACT_S: return 1.0 / (1.0 + exp(-x));
+    default: return x;
+    }
+}
+// d(act)/dx applied to an upstream gradient, expressed through y = act(x)
+__device__ __forceinline__ double act_d64(int a, double y, double g) {
+    switch (a) {
+    case ACT_T: return g * (1.0 - y * y);
+    case ACT_O: return 0.1 * g;
+    case ACT_S: return g * y * (1.0 - y);
+    default: return g;
+    }
+}
+
+// Plain parameters, or the line-search candidate theta + sf * fullstep (sf = 2^-k, so
+// sf * fullstep is exact and the sum rounds once, as xnew[i] = x[i] + stepfrac*fullstep[i]).
+struct ThetaPlain {
+    const double *__restrict__ t;
+    __device__ double operator[](int i) const { return t[i]; }
+};
+struct ThetaStep {
+    const double *__restrict__ t;
+    const double *__restrict__ f;
+    double sf;
+    __device__ double operator[](int i) const { return t[i] + sf * f[i]; }
+};
+
+// forward pass of sample s into Y rows [row][UT] (rows of layer i start at roff[i]);
+// src/TRPO_Update.c:262-293 / :954-976
+template <class TH>
+__device__ void forward64(const Net &net, const TH &th, const double *__restrict__ obs, int s, bool live,
+                          double *Y, const int *roff, int tid) {
+    const int L0 = net.L[0];
+    for (int k = 0; k < L0; ++k) Y[k * UT + tid] = live ? obs[(long)s * L0 + k] : 0.0;
+    for (int i = 0; i + 1 < net.nl; ++i) {
+        const int in = net.L[i], out = net.L[i + 1], a = net.act[i + 1];
+        const int wo = net.woff[i], bo = net.boff[i];
+        for (int j = 0; j < out; ++j) {
+            double x = th[bo + j];
+            for (int k = 0; k < in; ++k) x += Y[(roff[i] + k) * UT + tid] * th[wo + k * out + j];
+            Y[(roff[i + 1] + j) * UT + tid] = act_y64(a, x);
+        }
+    }
+}
+
+__device__ __forceinline__ void row_offsets(const Net &net, int *roff) {
+    roff[0] = 0;
+    for (int i = 0; i < net.nl; ++i) roff[i + 1] = roff[i] + net.L[i];
+}
+
+// Policy gradient partial sums: block b accumulates, over its 64-sample passes, the
+// unnormalised gradient [GW, GB per layer, GLogStd] (src/TRPO_Update.c:295-378) plus
+// sum(Adv) at index P, into slabs[b][P + 1].
+__global__ void __launch_bounds__(UT)
+pg_kernel(Net net, const double *__restrict__ th, const double *__restrict__ obs, const double *__restrict__ roll,
+          int n, double *ws, int rows, int use_lds, double *__restrict__ slabs) {
+    extern __shared__ double lds64[];
+    const int tid = threadIdx.x;
+    double *Y = use_lds ? lds64 : ws + (long)blockIdx.x * rows * UT;
+    int roff[MAXL + 1];
+    row_offsets(net, roff);
+    const int tot = roff[net.nl], P = net.P, A = net.A, last = net.nl - 1;
+    double *G = Y + (long)tot * UT;            // gradient w.r.t. pre-activations, same rows as Y
+    double *GL = G + (long)tot * UT;           // A rows of per-sample GLogStd, then one row of Adv
+    double *slab = slabs + (long)blockIdx.x * (P + 1);
+    const ThetaPlain T{th};
+    for (int q = tid; q <= P; q += UT) slab[q] = 0.0;
+    const int npass = (n + UT - 1) / UT;
+    for (int pass = blockIdx.x; pass < npass; pass += gridDim.x) {
+        const int s = pass * UT + tid;
+        const bool live = s < n;
+        forward64(net, T, obs, s, live, Y, roff, tid);
+        const double *rw = roll + (long)(live ? s : 0) * (2 * A + 1);
+        const double adv = live ? rw[2 * A] : 0.0;
+        // output seed (src/TRPO_Update.c:297-303)
+        for (int i = 0; i < A; ++i) {
+            const double es = exp(th[P - A + i]);
+            const double temp = (rw[A + i] - rw[i]) / es;
+            G[(roff[last] + i) * UT + tid] = live ? adv * temp / es : 0.0;
+            GL[i * UT + tid] = live ? adv * (temp * temp - 1.0) : 0.0;
+        }
+        GL[A * UT + tid] = adv;
+        // backprop (src/TRPO_Update.c:305-357); the unused input-layer gradient is skipped
+        for (int i = last; i >= 1; --i) {
+            const int cur = net.L[i], a = net.act[i];
+            for (int j = 0; j < cur; ++j) {
+                const int e = (roff[i] + j) * UT + tid;
+                G[e] = act_d64(a, Y[e], G[e]);
+            }
+            if (i >= 2) {
+                const int prev = net.L[i - 1], wo = net.woff[i - 1];
+                for (int j = 0; j < prev; ++j) {
+                    double t = 0.0;
+                    for (int k = 0; k < cur; ++k) t += G[(roff[i] + k) * UT + tid] * th[wo + j * cur + k];
+                    G[(roff[i - 1] + j) * UT + tid] = t;
+                }
+            }
+        }
+        __syncthreads();
+        // contraction over the pass's 64 samples, one parameter per thread (fixed order)
+        for (int q = tid; q <= P; q += UT) {
+            const double *u = nullptr, *w = nullptr;
+            if (q >= P - A) {
+                w = GL + (long)(q - (P - A)) * UT;     // GLogStd rows, then the Adv row at q == P
+            } else {
+                int i = 0;
+                while (i + 2 < net.nl && q >= net.woff[i + 1]) ++i;
+                const int in = net.L[i], out = net.L[i + 1], local = q - net.woff[i];
+                if (local < in * out) {
+                    u = Y + (long)(roff[i] + local / out) * UT;
+                    w = G + (long)(roff[i + 1] + local % out) * UT;
+                } else {
+                    w = G + (long)(roff[i + 1] + local - in * out) * UT;
+                }
+            }
+            double acc = 0.0;
+            if (u) {
+                for (int t = 0; t < UT; ++t) acc += u[t] * w[t];
+            } else {
+                for (int t = 0; t < UT; ++t) acc += w[t];
+            }
+            slab[q] += acc;
+        }
+        __syncthreads();
+    }
+}
+
+// Line-search surrogate: block (bx, k) sums Adv * exp(LLD) over its passes for candidate
+// theta + 2^-(k0+k) fullstep (src/TRPO_Update.c:951-981); parts[bx][k].
+__global__ void __launch_bounds__(UT)
+surr_kernel(Net net, const double *__restrict__ th0, const double *__restrict__ fs, int k0,
+            const double *__restrict__ obs, const double *__restrict__ roll, const double *__restrict__ stdv, int n,
+            double *ws, int rows, int use_lds, double *__restrict__ parts) {
+    extern __shared__ double lds64[];
+    const int tid = threadIdx.x, k = blockIdx.y, nk = gridDim.y;
+    double *Y = use_lds ? lds64 : ws + ((long)k * gridDim.x + blockIdx.x) * rows * UT;
+    int roff[MAXL + 1];
+    row_offsets(net, roff);
+    const int P = net.P, A = net.A, last = net.nl - 1;
+    const ThetaStep T{th0, fs, ldexp(1.0, -(k0 + k))};   // pow(0.5, k) exactly
+    double acc = 0.0;
+    const int npass = (n + UT - 1) / UT;
+    for (int pass = blockIdx.x; pass < npass; pass += gridDim.x) {
+        const int s = pass * UT + tid;
+        const bool live = s < n;
+        forward64(net, T, obs, s, live, Y, roff, tid);
+        if (live) {
+            const double *rw = roll + (long)s * (2 * A + 1);
+            double lld = 0.0;
+            for (int i = 0; i < A; ++i) {
+                const double ls = T[P - A + i];
+                const double tx = (rw[A + i] - rw[i]) / stdv[i];
+                const double tn = (rw[A + i] - Y[(roff[last] + i) * UT + tid]) / exp(ls);
+                lld += tx * tx - tn * tn + log(stdv[i]) - ls;
+            }
+            lld = lld * 0.5;
+            acc += exp(lld) * rw[2 * A];
+        }
+    }
+    // fixed-order wave tree
+    for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if (tid == 0) parts[(long)blockIdx.x * nk + k] = acc;
+}
+
+// out[q] = sum_b slabs[b][q] for q < len, in a fixed order (16 strided chains, then in order)
+__global__ void __launch_bounds__(256)
+sum_slabs64_kernel(const double *__restrict__ slabs, int G, int len, double *__restrict__ out) {
+    __shared__ double part[16][17];
+    const int tq = threadIdx.x & 15, tj = threadIdx.x >> 4;
+    const int q = blockIdx.x * 16 + tq;
+    double s = 0.0;
+    if (q < len)
+        for (int b = tj; b < G; b += 16) s += slabs[(long)b * len + q];
+    part[tj][tq] = s;
+    __syncthreads();
+    if (tj == 0 && q < len) {
+        double t = 0.0;
+        for (int j = 0; j < 16; ++j) t += part[j][tq];
+        out[q] = t;
+    }
+}
+
+// b = sum / N into the CG right-hand side (src/TRPO_Update.c:374-378)
+__global__ void pg_finish_kernel(const double *__restrict__ sum, double n_total, int P, double *__restrict__ b) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < P) b[q] = sum[q] / n_total;
+}
+
+// ---------------------------------------------------------------------------
+// device-layer entry points (trpo_dev.h)
+// ---------------------------------------------------------------------------
+static UpdState *state(trpo_dev *d) {
+    void **slot = trpo_dev_update_state(d);
+    if (!*slot) *slot = new UpdState();
+    return (UpdState *)*slot;
+}
+
+static int ensure(double **p, size_t *cap, size_t count, hipStream_t st) {
+    if (count <= *cap && *p) return 0;
+    if (*p) hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    HCHK(hipMalloc((void **)p, sizeof(double) * (count ? count : 1)));
+    HCHK(hipMemsetAsync(*p, 0, sizeof(double) * (count ? count : 1), st));
+    *cap = count;
+    return 0;
+}
+
+static int rows_for(const Net &net, bool grads) {
+    int tot = 0;
+    for (int i = 0; i < net.nl; ++i) tot += net.L[i];
+    return grads ? 2 * tot + net.A + 1 : tot;
+}
+
+// activation storage for `blocks` workgroups of `rows` rows: LDS when it fits (returns the
+// dynamic LDS bytes), else a global scratch (returns 0)
+static int act_storage(UpdState *u, const Net &net, int rows, long blocks, hipStream_t st, int *use_lds) {
+    const size_t bytes = sizeof(double) * (size_t)rows * UT;
+    if (bytes <= (size_t)LDS_CAP) {
+        if (!u->lds_set) {
+            HCHK(hipFuncSetAttribute((const void *)pg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_CAP));
+            HCHK(hipFuncSetAttribute((const void *)surr_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_CAP));
+            u->lds_set = 1;
+        }
+        *use_lds = 1;
+        return (int)bytes;
+    }
+    (void)net;
+    *use_lds = 0;
+    if (ensure(&u->ws, &u->ws_cap, (size_t)rows * UT * blocks, st)) return -1;
+    return 0;
+}
+
+extern "C" int trpo_dev_set_rollout(trpo_dev *d, const double *mean, const double *action, const double *adv,
+                                    size_t n) {
+    if (!d || (n && (!mean || !action || !adv))) return -1;
+    trpo_dev_view v;
+    trpo_dev_get_view(d, &v);
+    if (n != v.n) return -1;
+    HCHK(hipSetDevice(v.device));
+    UpdState *u = state(d);
+    const int A = v.net.A, W = 2 * A + 1;
+    double *h = (double *)malloc(sizeof(double) * (n * W + 1));
+    if (!h) return -1;
+    for (size_t s = 0; s < n; ++s) {
+        memcpy(h + s * W, mean + s * A, sizeof(double) * A);
+        memcpy(h + s * W + A, action + s * A, sizeof(double) * A);
+        h[s * W + 2 * A] = adv[s];
+    }
+    int rc = ensure(&u->roll, &u->roll_cap, n * W, v.stream);
+    if (!rc && n) rc = hipMemcpyAsync(u->roll, h, sizeof(double) * n * W, hipMemcpyHostToDevice, v.stream) ? -2 : 0;
+    if (!rc) rc = hipStreamSynchronize(v.stream) ? -2 : 0;
+    free(h);
+    if (rc) return rc;
+    u->roll_n = n;
+    u->have_roll = 1;
+    return 0;
+}
+
+extern "C" int trpo_dev_policy_gradient(trpo_dev *d, double *b_host, double *adv_sum) {
+    if (!d) return -1;
+    trpo_dev_view v;
+    trpo_dev_get_view(d, &v);
+    UpdState *u = state(d);
+    if (!u->have_roll || u->roll_n != v.n) return -3;       // rollout missing / stale for this obs
+    HCHK(hipSetDevice(v.device));
+    const Net &net = v.net;
+    const int P = net.P, n = (int)v.n;
+    const int G = n ? (cdiv(n, UT) < 2048 ? cdiv(n, UT) : 2048) : 1;
+    const int rows = rows_for(net, true);
+    int use_lds = 0;
+    const int lds = act_storage(u, net, rows, G, v.stream, &use_lds);
+    if (lds < 0) return -2;
+    if (ensure(&u->slabs, &u->slab_cap, (size_t)G * (P + 1), v.stream)) return -2;
+    if (!u->sum) HCHK(hipMalloc((void **)&u->sum, sizeof(double) * (P + 1)));
+    hipLaunchKernelGGL(pg_kernel, dim3(G), dim3(UT), lds, v.stream, net, v.theta64, v.obs64, u->roll, n, u->ws, rows,
+                       use_lds, u->slabs);
+    hipLaunchKernelGGL(sum_slabs64_kernel, dim3(cdiv(P + 1, 16)), dim3(256), 0, v.stream, u->slabs, G, P + 1, u->sum);
+    HCHK(hipGetLastError());
+    if (trpo_dev_allreduce64(d, u->sum, (size_t)P + 1)) return -4;
+    hipLaunchKernelGGL(pg_finish_kernel, dim3(cdiv(P, 256)), dim3(256), 0, v.stream, u->sum, v.n_total, P, v.vec_b);
+    HCHK(hipGetLastError());
+    if (b_host) HCHK(hipMemcpyAsync(b_host, v.vec_b, sizeof(double) * P, hipMemcpyDeviceToHost, v.stream));
+    if (adv_sum) HCHK(hipMemcpyAsync(adv_sum, u->sum + P, sizeof(double), hipMemcpyDeviceToHost, v.stream));
+    HCHK(hipStreamSynchronize(v.stream));
+    return 0;
+}
+
+extern "C" int trpo_dev_surrogate(trpo_dev *d, const double *fullstep, int k0, int nk, double *surr_host) {
+    if (!d || !fullstep || !surr_host || k0 < 0 || nk < 1 || nk > 64 || k0 + nk > 1074) return -1;
+    trpo_dev_view v;
+    trpo_dev_get_view(d, &v);
+    UpdState *u = state(d);
+    if (!u->have_roll || u->roll_n != v.n) return -3;
+    HCHK(hipSetDevice(v.device));
+    const Net &net = v.net;
+    const int P = net.P, n = (int)v.n;
+    const int cap = 2048 / nk > 0 ? 2048 / nk : 1;
+    const int Gs = n ? (cdiv(n, UT) < cap ? cdiv(n, UT) : cap) : 1;
+    const int rows = rows_for(net, false);
+    int use_lds = 0;
+    const int lds = act_storage(u, net, rows, (long)Gs * nk, v.stream, &use_lds);
+    if (lds < 0) return -2;
+    if (!u->fs) HCHK(hipMalloc((void **)&u->fs, sizeof(double) * P));
+    if (ensure(&u->slabs, &u->slab_cap, (size_t)Gs * nk, v.stream)) return -2;
+    if (!u->sums) HCHK(hipMalloc((void **)&u->sums, sizeof(double) * 64));
+    HCHK(hipMemcpyAsync(u->fs, fullstep, sizeof(double) * P, hipMemcpyHostToDevice, v.stream));
+    hipLaunchKernelGGL(surr_kernel, dim3(Gs, nk), dim3(UT), lds, v.stream, net, v.theta64, u->fs, k0, v.obs64,
+                       u->roll, v.std64, n, u->ws, rows, use_lds, u->slabs);
+    hipLaunchKernelGGL(sum_slabs64_kernel, dim3(cdiv(nk, 16)), dim3(256), 0, v.stream, u->slabs, Gs, nk, u->sums);
+    HCHK(hipGetLastError());
+    if (trpo_dev_allreduce64(d, u->sums, (size_t)nk)) return -4;
+    HCHK(hipMemcpyAsync(surr_host, u->sums, sizeof(double) * nk, hipMemcpyDeviceToHost, v.stream));
+    HCHK(hipStreamSynchronize(v.stream));
+    return 0;
+}

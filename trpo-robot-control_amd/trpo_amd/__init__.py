@@ -108,12 +108,30 @@ def lib():
     L.trpo_ctx_kernel_name.argtypes = [C.c_void_p]
     L.trpo_ctx_launch_geometry.restype = C.c_int
     L.trpo_ctx_launch_geometry.argtypes = [C.c_void_p, P(C.c_int), P(C.c_int), P(C.c_int)]
+    L.TRPO_Update.restype = C.c_double
+    L.TRPO_Update.argtypes = [TRPOparam, _dp, sz]
+    L.trpo_ctx_set_rollout.restype = C.c_int
+    L.trpo_ctx_set_rollout.argtypes = [C.c_void_p, _dp, _dp, _dp]
+    L.trpo_ctx_update.restype = C.c_double
+    L.trpo_ctx_update.argtypes = [C.c_void_p, sz, C.c_double, C.c_double, C.c_int, C.c_double, _dp, _dp, _dp,
+                                  P(UpdateInfo), C.c_int]
     L.trpo_last_error.restype = C.c_char_p
     L.trpo_last_error.argtypes = []
     L.trpo_cache_clear.restype = None
     L.trpo_cache_clear.argtypes = []
     _lib = L
     return L
+
+
+MAX_BACKTRACKS = 32
+
+
+class UpdateInfo(C.Structure):
+    """trpo_update_info (include/trpo_mi355x.h)."""
+    _fields_ = [("shs", C.c_double), ("lagrange", C.c_double), ("gnorm", C.c_double), ("fval_before", C.c_double),
+                ("expected_improve_rate", C.c_double), ("evaluated", C.c_int), ("accepted", C.c_int),
+                ("actual", C.c_double * MAX_BACKTRACKS), ("expected", C.c_double * MAX_BACKTRACKS),
+                ("ratio", C.c_double * MAX_BACKTRACKS), ("cg_iters", C.c_size_t)]
 
 
 def last_error() -> str:
@@ -157,6 +175,11 @@ def FVP(param: TRPOparam, result: np.ndarray, inp: np.ndarray) -> float:
 def CG(param: TRPOparam, result: np.ndarray, b: np.ndarray, max_iter: int = 10, residual_th: float = 1e-10,
        num_threads: int = 1) -> float:
     return float(lib().CG(param, result, b, max_iter, residual_th, num_threads))
+
+
+def TRPO_Update(param: TRPOparam, result: np.ndarray, num_threads: int = 1) -> float:
+    """src/TRPO_Update.c:10-1011: result <- updated policy parameters."""
+    return float(lib().TRPO_Update(param, result, num_threads))
 
 
 def FVP_FPGA(param: TRPOparam, result: np.ndarray, inp: np.ndarray) -> float:
@@ -248,6 +271,30 @@ class Context:
         self._chk(lib().trpo_ctx_cg_history(self._h, rr, xn, cap, C.byref(it)), "cg_history")
         n = it.value + 1
         return rr[:n], xn[:n], it.value
+
+    def set_rollout(self, mean, action, adv):
+        """Mean [n][A], Action [n][A], Advantage [n] of this context's samples (TRPO_Update)."""
+        A = self.layers[-1]
+        mean = np.ascontiguousarray(mean, np.float64)
+        action = np.ascontiguousarray(action, np.float64)
+        adv = np.ascontiguousarray(adv, np.float64)
+        if mean.size != self.n * A or action.size != self.n * A or adv.size != self.n:
+            raise ValueError("rollout shape mismatch for n=%d A=%d" % (self.n, A))
+        self._chk(lib().trpo_ctx_set_rollout(self._h, mean, action, adv), "set_rollout")
+
+    def update(self, max_iter=10, residual_th=1e-10, max_kl=0.01, max_backtracks=10, accept_ratio=0.1,
+               verbose=False):
+        """One TRPO policy update (src/TRPO_Update.c:254-1007).  Returns a dict with the new
+        parameters, the policy gradient b, the CG step x and the step-size / line-search values."""
+        th, b, x = np.zeros(self.P), np.zeros(self.P), np.zeros(self.P)
+        info = UpdateInfo()
+        t = self._chk(lib().trpo_ctx_update(self._h, max_iter, residual_th, max_kl, max_backtracks, accept_ratio,
+                                            th, b, x, C.byref(info), 1 if verbose else 0), "update")
+        k = info.evaluated
+        return dict(theta=th, b=b, x=x, shs=info.shs, lagrange=info.lagrange, gnorm=info.gnorm,
+                    fval=info.fval_before, rate=info.expected_improve_rate, accepted=info.accepted, evaluated=k,
+                    actual=np.array(info.actual[:k]), expected=np.array(info.expected[:k]),
+                    ratio=np.array(info.ratio[:k]), cg_iters=info.cg_iters, seconds=t)
 
     # device-resident hooks used by bench.py
     def upload_b(self, b):

@@ -9,6 +9,10 @@ Distributions:
   * W ~ N(0, 1/fan_in)   via Irwin-Hall(12) - 6, b = 0, logstd = 0
   * v ~ U[0, 1)          (as ArmTestFVP.txt column 1)
   * CG right-hand side b ~ N(0, 1e-2^2)
+  * TRPO_Update rollouts: Mean = the policy's own output on the observations,
+    Action = Mean + Std * N(0, 1), Advantage ~ N(0, 1).  The policy mean uses
+    tanh through Lambert's continued fraction (exact IEEE +,-,*,/ only), so it
+    is still bit-identical on every host.
 """
 from __future__ import annotations
 
@@ -20,7 +24,7 @@ _M1 = np.uint64(0xBF58476D1CE4E5B9)
 _M2 = np.uint64(0x94D049BB133111EB)
 
 # stream ids keep the different inputs independent
-STREAM_OBS, STREAM_W, STREAM_V, STREAM_B = 1, 2, 3, 4
+STREAM_OBS, STREAM_W, STREAM_V, STREAM_B, STREAM_ACT, STREAM_ADV = 1, 2, 3, 4, 5, 6
 
 
 def _splitmix(seed: int, stream: int, count: int, offset: int = 0) -> np.ndarray:
@@ -80,6 +84,50 @@ def make_b(P: int, seed: int = SEED) -> np.ndarray:
     return normal(seed, STREAM_B, P, sigma=1e-2)
 
 
+def tanh_cf(x: np.ndarray, depth: int = 24) -> np.ndarray:
+    """tanh via Lambert's continued fraction x / (1 + x^2 / (3 + x^2 / (5 + ...))),
+    exact arithmetic only; agrees with libm tanh to ~1 ulp for |x| < 4."""
+    x = np.asarray(x, dtype=np.float64)
+    x2 = x * x
+    t = np.full_like(x, 2.0 * depth + 1.0)
+    for k in range(depth, 0, -1):
+        t = (2.0 * k - 1.0) + x2 / t
+    return x / t
+
+
+def policy_mean(layers, acfunc: str, theta: np.ndarray, obs: np.ndarray) -> np.ndarray:
+    """Forward pass of the policy MLP (src/TRPO_Update.c:262-293), fixed-order sums,
+    no BLAS, so the result does not depend on the host."""
+    y = np.asarray(obs, dtype=np.float64)
+    pos = 0
+    for i in range(len(layers) - 1):
+        fin, out = layers[i], layers[i + 1]
+        W = theta[pos:pos + fin * out].reshape(fin, out)
+        B = theta[pos + fin * out:pos + fin * out + out]
+        pos += fin * out + out
+        x = np.broadcast_to(B, (y.shape[0], out)).copy()
+        for k in range(fin):
+            x = x + y[:, k:k + 1] * W[k:k + 1, :]
+        a = acfunc[i + 1]
+        if a == "t":
+            x = tanh_cf(x)
+        elif a == "o":
+            x = 0.1 * x
+        elif a == "s":
+            x = 0.5 + 0.5 * tanh_cf(0.5 * x)
+        y = x
+    return y
+
+
+def make_rollout(layers, acfunc: str, theta: np.ndarray, obs: np.ndarray, std, seed: int = SEED):
+    """(mean [n][A], action [n][A], advantage [n]) for a TRPO_Update data file."""
+    n, A = obs.shape[0], layers[-1]
+    mean = policy_mean(layers, acfunc, theta, obs)
+    action = mean + np.asarray(std, dtype=np.float64) * normal(seed, STREAM_ACT, n * A).reshape(n, A)
+    adv = normal(seed, STREAM_ADV, n)
+    return mean, action, adv
+
+
 def write_model_file(path: str, theta: np.ndarray) -> None:
     """One value per line (src/TRPO_FVP.c:670-699)."""
     with open(path, "w") as f:
@@ -87,15 +135,17 @@ def write_model_file(path: str, theta: np.ndarray) -> None:
         f.write("\n")
 
 
-def write_data_file(path: str, obs: np.ndarray, std: np.ndarray, mean: np.ndarray | None = None) -> None:
+def write_data_file(path: str, obs: np.ndarray, std: np.ndarray, mean: np.ndarray | None = None,
+                    action: np.ndarray | None = None, adv: np.ndarray | None = None) -> None:
     """Per sample: Mean[A] Std[A] Obs[O] Action[A] Adv (src/TRPO_FVP.c:731-762).
-    Action and Advantage are zero: the FVP/CG path never reads them."""
+    Missing Mean / Action / Advantage columns are written as zeros (the FVP/CG path
+    never reads them; TRPO_Update does)."""
     n, _ = obs.shape
     A = len(std)
-    if mean is None:
-        mean = np.zeros((n, A))
-    zeros = np.zeros((n, A + 1))
-    table = np.concatenate([mean, np.broadcast_to(std, (n, A)), obs, zeros], axis=1)
+    mean = np.zeros((n, A)) if mean is None else mean
+    action = np.zeros((n, A)) if action is None else action
+    adv = np.zeros(n) if adv is None else adv
+    table = np.concatenate([mean, np.broadcast_to(std, (n, A)), obs, action, adv[:, None]], axis=1)
     np.savetxt(path, table, fmt="%.17g")
 
 
