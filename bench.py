@@ -160,6 +160,45 @@ def cpu_baseline(theta, obs_all, b, gpu_x):
     return res, rel
 
 
+def bench_update(device, n=N_TOTAL, reps=20):
+    """One full TRPO policy update (src/TRPO_Update.c: policy gradient, 10-iteration CG, FVP(x),
+    line search) on a synthetic armDOF_0 rollout, host-visible wall time per update (includes the
+    host round trips of x / z / the line-search scalars); CPU reference TRPO_Update timed beside it."""
+    import oracle
+    L = ARM
+    theta = synth.make_theta(L)
+    obs = synth.make_obs(n, L[0])
+    std = np.ones(L[-1])
+    mean, action, adv = synth.make_rollout(L, "lttl", theta, obs, std)
+    ctx = trpo_amd.Context(L, "lttl", theta, obs, std, DAMPING, device=device)
+    ctx.set_rollout(mean, action, adv)
+    r = ctx.update()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        r = ctx.update()
+    wall = (time.perf_counter() - t0) / reps
+    ctx.close()
+    out = {"update_ms": 1e3 * wall, "accepted": r["accepted"], "cg_iters": int(r["cg_iters"]),
+           "samples": n, "what": "policy gradient + CG(10, 1e-10) + FVP(x) + line search, fp64 PG/line search"}
+    if os.path.exists(oracle.REF_DRIVER_FAST):
+        with tempfile.TemporaryDirectory() as tmp:
+            mf, df, of = (os.path.join(tmp, f) for f in ("m.txt", "d.txt", "o.txt"))
+            synth.write_model_file(mf, theta)
+            synth.write_data_file(df, obs, std, mean, action, adv)
+            cmd = [oracle.REF_DRIVER_FAST, "update", mf, df, str(n), ",".join(map(str, L)), "lttl", str(DAMPING),
+                   of, "1"]
+            w0 = time.perf_counter()
+            p = subprocess.run(cmd, capture_output=True, text=True)
+            if p.returncode == 0:
+                ref = np.loadtxt(of)
+                tj = json.loads(p.stderr.strip().splitlines()[-1])
+                out["cpu_reference_compute_s_1core"] = tj["compute_s"]
+                out["cpu_reference_wall_s_1core_incl_parse"] = time.perf_counter() - w0
+                out["theta_update_relL2_vs_cpu"] = float(np.linalg.norm((r["theta"] - theta) - (ref - theta))
+                                                         / np.linalg.norm(ref - theta))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -243,6 +282,7 @@ def main():
                                         "kernel_ms": k3,
                                         "kernel_tflops": flops_per_sample(L2) * N_TOTAL / (k3 * 1e-3) / 1e12}
         c3.close()
+        extra["C5_update_armDOF_0_N50000"] = bench_update(device)
         result["extra"] = extra
 
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:

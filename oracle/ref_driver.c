@@ -82,8 +82,11 @@ int main(int argc, char **argv) {
     double *in = calloc(P, sizeof(double)), *out = calloc(P, sizeof(double));
     if (!strcmp(mode, "update")) {       /* TRPO_Update prints shs / lagrange / a/e/r itself */
         size_t th = argc > 9 ? (size_t)atoi(argv[9]) : 1;
+        double w0 = wall();
         double t = TRPO_Update(prm, out, th);
+        double w1 = wall();
         if (t < 0) return 1;
+        fprintf(stderr, "{\"compute_s\": %.9f, \"wall_s\": %.9f, \"threads\": %zu}\n", t, w1 - w0, th);
         return write_vec(argv[8], out, P) ? 1 : 0;
     }
     if (read_vec(argv[8], in, P)) {

@@ -1,7 +1,10 @@
 """MI355X parity of the TRPO_Update path (src/TRPO_Update.c:10-1011) through the C ABI.
 
 Tolerances (stated):
-  * policy gradient b: fp64 on the device, only the summation order differs -> relL2 <= 1e-12
+  * policy gradient b: weights/biases by the fp32 MFMA tile kernel (fp64 cross-tile sums),
+    LogStd part and sum(Adv) in fp64 -> relL2 <= 2e-6 (numpy emulation of fp32 per-sample math:
+    1.2e-7, which moves the CG step by 4e-7); the generic fp64 kernel (TRPO_UPDATE_GENERIC=1,
+    used for shapes without a tile kernel) -> relL2 <= 1e-12
   * CG step x: fp32 FVP inside the solve -> relL2 <= 1e-4 (as the CG tests) for armDOF_0;
     2e-3 for the 2x64 policy.  Why: the fp32 rounding of each CG direction p (and the
     p-proportional rounding of the R-chain) is noise that CG amplifies by the condition
@@ -26,6 +29,8 @@ pytestmark = pytest.mark.gpu
 
 UPDATE = [c["name"] for c in cases.manifest() if c["kind"] == "update"]
 TOL = {"syn_update_2x64_n8192": 2e-3}
+B_TOL = 2e-6            # fp32 tile-kernel policy gradient
+B_TOL_GENERIC = 1e-12   # fp64 generic kernel
 
 
 def _ctx(x):
@@ -40,16 +45,19 @@ def _oracle_update(x, **kw):
                          x["std"], x["damping"], **kw)
 
 
+@pytest.mark.parametrize("generic", [False, True])
 @pytest.mark.parametrize("name", UPDATE)
-def test_update_matches_reference_golden(name):
+def test_update_matches_reference_golden(name, generic, monkeypatch):
     import oracle
+    if generic:
+        monkeypatch.setenv("TRPO_UPDATE_GENERIC", "1")
     c = cases.case(name)
     x = cases.update_inputs(c)
     with _ctx(x) as ctx:
         r = ctx.update()
     b_ref, _ = oracle.policy_grad(x["layers"], x["acfunc"], x["theta"], x["obs"], x["mean"], x["action"], x["adv"])
-    assert cases.rel_l2(r["b"], b_ref) <= 1e-12
-    assert abs(r["gnorm"] - c["gnorm"]) <= 1e-12 * c["gnorm"]
+    assert cases.rel_l2(r["b"], b_ref) <= (B_TOL_GENERIC if generic else B_TOL)
+    assert abs(r["gnorm"] - c["gnorm"]) <= (B_TOL_GENERIC if generic else B_TOL) * c["gnorm"]
     assert abs(r["fval"] - c["fval"]) <= 1e-12
     tol = TOL.get(name, 1e-4)
     ref = _oracle_update(x)
@@ -80,9 +88,13 @@ def test_trpo_update_file_entry_point(capfd):
     assert cases.rel_l2(res - th, cases.expected(c) - th) <= 1e-4
     out = capfd.readouterr().out
     assert out.count("CG Iter[") in (9, 10)            # 8 FVPs in fp64; fp32 may need one more
-    assert "shs: 0.0029493" in out
-    assert "lagrange multiplier: 0.54307" in out and "gnorm: 0.09516276863626" in out
-    assert out.count("a/e/r ") == 1 and "/ 0.9129" in out
+    import re
+    shs = float(re.search(r"shs: (\S+)", out).group(1))
+    lm, gn = map(float, re.search(r"lagrange multiplier: (\S+), gnorm: (\S+)", out).groups())
+    are = re.findall(r"a/e/r (\S+) / (\S+) / (\S+)", out)
+    assert abs(shs - c["shs"]) <= 1e-4 * c["shs"] and abs(lm - c["lagrange"]) <= 1e-4 * c["lagrange"]
+    assert abs(gn - c["gnorm"]) <= B_TOL * c["gnorm"]
+    assert len(are) == 1 and abs(float(are[0][2]) - c["ratio"][0]) <= 1e-3 * c["ratio"][0]
     # a second call hits the device cache (rollout already resident): same answer
     res2 = np.zeros(582)
     assert trpo_amd.TRPO_Update(prm, res2, 1) >= 0
@@ -122,7 +134,7 @@ def test_update_ragged_sample_counts(n):
     b_ref, s_ref = oracle.policy_grad(L, "lttl", th, obs, mean, action, adv)
     with _ctx(x) as ctx:
         r = ctx.update()
-    assert cases.rel_l2(r["b"], b_ref) <= 1e-12
+    assert cases.rel_l2(r["b"], b_ref) <= B_TOL
     assert abs(r["fval"] + s_ref / n) <= 1e-12 * max(1.0, abs(s_ref / n))
 
 

@@ -89,6 +89,11 @@ struct IterArgs {
     Ctl *ctl;
     double *hist;
     const int *vmap;
+    // policy-gradient mode (MODE == 1, src/TRPO_Update.c:254-378): per padded sample the
+    // fp32 (Action - Mean) rows [16 T3] and Adv, and 1/sigma^2 with sigma = exp(LogStd)
+    const float4 *pg_d4;
+    const float *pg_adv;
+    const float4 *pg_iv4;
 };
 
 // fixed-order block-wide fp64 sum (every thread gets the result)
@@ -444,9 +449,13 @@ __device__ __forceinline__ f4 scr_get(const float *scr, int row0, int c, int g) 
 
 // ACT >= 0: activations of layers 1..3 fixed at compile time (a1 | a2 << 2 | a3 << 4);
 // ACT == -1: read from net.act at run time (wave-uniform branches).
-template <int T0, int T1, int T2, int T3, int ACT>
+// MODE 0: Fisher-vector product (R-forward + Pearlmutter backward, optionally fused with the
+// CG step).  MODE 1: policy gradient of TRPO_Update (plain forward, output seed
+// Adv (Action - Mean) / sigma^2, the same backward and contractions; no R chains).
+template <int T0, int T1, int T2, int T3, int ACT, int MODE>
 __global__ void __launch_bounds__((64 * FastCfg<T0, T1, T2, T3>::WAVES))
 fvp_mlp3_kernel(IterArgs A, Net net) {
+    constexpr bool FV = MODE == 0;
     using C = FastCfg<T0, T1, T2, T3>;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ double sh64[20 * C::WAVES];      // 5 DPP block sums, 4 rows per wave
@@ -685,13 +694,13 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
 #pragma unroll
             for (int kt = 0; kt < T0; ++kt) {
                 const f4 w = WLD(rFA0, TW[C::FA0 / 4 + (ot * T0 + kt) * 64 + lane]);
-                const f4 u = WLD(rVFA0, VW[C::VFA0 / 4 + (ot * T0 + kt) * 64 + lane]);
+                const f4 u = FV ? WLD(rVFA0, VW[C::VFA0 / 4 + (ot * T0 + kt) * 64 + lane]) : zero4;
 #pragma unroll
                 for (int s = 0; s < 4; ++s)
 #pragma unroll
                     for (int t = 0; t < NT; ++t) {
                         a[t] = MFMA(w[s], x0[t][kt][s], a[t]);
-                        ra[t] = MFMA(u[s], x0[t][kt][s], ra[t]);
+                        if constexpr (FV) ra[t] = MFMA(u[s], x0[t][kt][s], ra[t]);
                     }
             }
 #pragma unroll
@@ -718,14 +727,16 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
 #pragma unroll
             for (int kt = 0; kt < T1; ++kt) {
                 const f4 w = WLD(rFA1, TW[C::FA1 / 4 + (ot * T1 + kt) * 64 + lane]);
-                const f4 u = WLD(rVFA1, VW[C::VFA1 / 4 + (ot * T1 + kt) * 64 + lane]);
+                const f4 u = FV ? WLD(rVFA1, VW[C::VFA1 / 4 + (ot * T1 + kt) * 64 + lane]) : zero4;
 #pragma unroll
                 for (int s = 0; s < 4; ++s)
 #pragma unroll
                     for (int t = 0; t < NT; ++t) {
                         a[t] = MFMA(w[s], y1[t][kt][s], a[t]);
-                        ra[t] = MFMA(w[s], r1[t][kt][s], ra[t]);
-                        rb[t] = MFMA(u[s], y1[t][kt][s], rb[t]);
+                        if constexpr (FV) {
+                            ra[t] = MFMA(w[s], r1[t][kt][s], ra[t]);
+                            rb[t] = MFMA(u[s], y1[t][kt][s], rb[t]);
+                        }
                     }
             }
 #pragma unroll
@@ -753,21 +764,31 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
 #pragma unroll
             for (int kt = 0; kt < T2; ++kt) {
                 const f4 w = WLD(rFA2, TW[C::FA2 / 4 + (ot * T2 + kt) * 64 + lane]);
-                const f4 u = WLD(rVFA2, VW[C::VFA2 / 4 + (ot * T2 + kt) * 64 + lane]);
+                const f4 u = FV ? WLD(rVFA2, VW[C::VFA2 / 4 + (ot * T2 + kt) * 64 + lane]) : zero4;
 #pragma unroll
                 for (int s = 0; s < 4; ++s)
 #pragma unroll
                     for (int t = 0; t < NT; ++t) {
                         if (y3_needed) a[t] = MFMA(w[s], y2[t][kt][s], a[t]);
-                        ra[t] = MFMA(w[s], r2[t][kt][s], ra[t]);
-                        rb[t] = MFMA(u[s], y2[t][kt][s], rb[t]);
+                        if constexpr (FV) {
+                            ra[t] = MFMA(w[s], r2[t][kt][s], ra[t]);
+                            rb[t] = MFMA(u[s], y2[t][kt][s], rb[t]);
+                        }
                     }
             }
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
-                f4 r3;
+                f4 r3, gg;
                 const f4 y3 = act_fwd(a3, a[t], ra[t] + rb[t], r3);
-                const f4 gg = act_bwd(a3, y3, r3 * iv);
+                if constexpr (FV) {
+                    gg = act_bwd(a3, y3, r3 * iv);
+                } else {
+                    // seed of the policy gradient (src/TRPO_Update.c:297-303), lane = (sample c, outputs 4g+r)
+                    const int tt = min(tile + t * nwaves, ntiles - 1);
+                    const f4 dm = reinterpret_cast<const f4 *>(A.pg_d4)[(long)(tt * 16 + c) * (4 * T3) + ot * 4 + g];
+                    const float adv = A.pg_adv[tt * 16 + c];
+                    gg = act_bwd(a3, y3, (adv * dm) * reinterpret_cast<const f4 *>(A.pg_iv4)[ot * 4 + g]);
+                }
                 g3[t][ot] = live[t] ? gg : zero4;
                 sB3[ot] += g3[t][ot];
             }
@@ -1251,9 +1272,9 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
 // ===========================================================================
 typedef void (*fast_launch_fn)(dim3, int, hipStream_t, const IterArgs &, const Net &);
 
-template <int T0, int T1, int T2, int T3, int ACT>
+template <int T0, int T1, int T2, int T3, int ACT, int MODE>
 static void fast_launch(dim3 g, int lds, hipStream_t st, const IterArgs &a, const Net &net) {
-    hipLaunchKernelGGL((fvp_mlp3_kernel<T0, T1, T2, T3, ACT>), g, dim3(64 * FastCfg<T0, T1, T2, T3>::WAVES), lds,
+    hipLaunchKernelGGL((fvp_mlp3_kernel<T0, T1, T2, T3, ACT, MODE>), g, dim3(64 * FastCfg<T0, T1, T2, T3>::WAVES), lds,
                        st, a, net);
 }
 
@@ -1273,7 +1294,10 @@ static int cg_E(int P) {
     }
 template <int T0, int T1, int T2, int T3, int ACT>
 static hipError_t fast_attr(int lds) {
-    return hipFuncSetAttribute((const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT>,
+    hipError_t e = hipFuncSetAttribute((const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 0>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute((const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 1>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 }
 
@@ -1281,13 +1305,15 @@ struct FastEntry {
     int T[4];
     int act;                     // -1: run-time activations
     fast_launch_fn launch;
+    fast_launch_fn launch_pg;    // MODE 1: policy gradient
     hipError_t (*attr)(int);
     int lds, tlen, vlen, slab, emax, waves;
 };
 
 #define ACT_TTL (ACT_T | (ACT_T << 2) | (ACT_L << 4))
 #define FAST_ENTRY(a, b, c, d, act)                                                                               \
-    {{a, b, c, d}, act, fast_launch<a, b, c, d, act>, fast_attr<a, b, c, d, act>,                                 \
+    {{a, b, c, d}, act, fast_launch<a, b, c, d, act, 0>, fast_launch<a, b, c, d, act, 1>,                         \
+     fast_attr<a, b, c, d, act>,                                                                                  \
      FastCfg<a, b, c, d>::lds_bytes(), FastCfg<a, b, c, d>::TLEN, FastCfg<a, b, c, d>::VLEN,                      \
      FastCfg<a, b, c, d>::SLAB, FastCfg<a, b, c, d>::EMAX, FastCfg<a, b, c, d>::WAVES}
 #define FAST_SHAPE(a, b, c, d) FAST_ENTRY(a, b, c, d, ACT_TTL), FAST_ENTRY(a, b, c, d, -1)
@@ -1317,6 +1343,8 @@ struct trpo_dev {
     // common
     double *theta64;            // natural theta (device, fp64)
     double *obs64;              // local observations [n][L0], fp64 (TRPO_Update path)
+    float *pg_d, *pg_adv, *pg_iv;   // policy-gradient mode inputs (fp32, padded like obs4)
+    size_t pg_cap;
     void *upd;                  // TRPO_Update path state (trpo_update.hip)
     double *std64;
     double *vec[5];             // V, Z, X, B, P
@@ -1528,7 +1556,7 @@ extern "C" void trpo_dev_destroy(trpo_dev *d) {
     if (d->cg_exec) hipGraphExecDestroy(d->cg_exec);
     if (d->comm) ncclCommDestroy(d->comm);
     trpo_update_state_free(d->upd);
-    void *ptrs[] = {d->obs64, d->st, d->pbuf[0], d->pbuf[1], d->rbuf[0], d->rbuf[1], d->accbuf, d->imap, d->tpack, d->vpack, d->tmap, d->vmap, d->obs4, d->th32, d->v32, d->iv32, d->obs32, d->scratch,
+    void *ptrs[] = {d->obs64, d->pg_d, d->pg_adv, d->pg_iv, d->st, d->pbuf[0], d->pbuf[1], d->rbuf[0], d->rbuf[1], d->accbuf, d->imap, d->tpack, d->vpack, d->tmap, d->vmap, d->obs4, d->th32, d->v32, d->iv32, d->obs32, d->scratch,
                     d->theta64, d->std64, d->r, d->zacc, d->slabs, d->ctl, d->hist};
     for (void *p : ptrs)
         if (p) hipFree(p);
@@ -2032,3 +2060,58 @@ int trpo_dev_allreduce64(trpo_dev *d, double *buf, size_t count) { return allred
 void **trpo_dev_update_state(trpo_dev *d) { return &d->upd; }
 
 extern "C" double trpo_dev_n_total(const trpo_dev *d) { return d ? d->n_total : 0.0; }
+
+// ---------------------------------------------------------------------------
+// policy gradient through the MFMA tile kernel (MODE 1) -- TRPO_Update path
+// ---------------------------------------------------------------------------
+// (Action - Mean) rows [npad][ld] in fp32 (difference taken in fp64) and Adv [npad]
+__global__ void pg_prep_kernel(const double *__restrict__ roll, int n, int npad, int A, int ld,
+                               float *__restrict__ dm, float *__restrict__ adv) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (long)npad * ld) return;
+    const int s = (int)(e / ld), j = (int)(e % ld), W = 2 * A + 1;
+    dm[e] = (s < n && j < A) ? (float)(roll[(long)s * W + A + j] - roll[(long)s * W + j]) : 0.0f;
+    if (j == 0) adv[s] = s < n ? (float)roll[(long)s * W + 2 * A] : 0.0f;
+}
+
+// 1 / sigma^2 with sigma = exp(LogStd) of the current parameters
+__global__ void pg_iv_kernel(const double *__restrict__ theta, int P, int A, int len, float *__restrict__ iv) {
+    const int j = threadIdx.x;
+    if (j < len) {
+        const double es = j < A ? exp(theta[P - A + j]) : 1.0;
+        iv[j] = j < A ? (float)(1.0 / (es * es)) : 0.0f;
+    }
+}
+
+int trpo_dev_pg_sums_fast(trpo_dev *d, const double *roll64, const double **zacc) {
+    if (!d->fast) return 1;
+    HCHK(hipSetDevice(d->device));
+    const int ld = 16 * d->pack.T[3];
+    const size_t npad = (size_t)cdiv((long)d->n, 16) * 16 + 16;
+    if (npad > d->pg_cap) {
+        if (d->pg_d) hipFree(d->pg_d);
+        if (d->pg_adv) hipFree(d->pg_adv);
+        d->pg_d = d->pg_adv = NULL;
+        d->pg_cap = 0;
+        HCHK(hipMalloc((void **)&d->pg_d, sizeof(float) * npad * ld));
+        HCHK(hipMalloc((void **)&d->pg_adv, sizeof(float) * npad));
+        d->pg_cap = npad;
+    }
+    if (!d->pg_iv) HCHK(hipMalloc((void **)&d->pg_iv, sizeof(float) * ld));
+    hipLaunchKernelGGL(pg_prep_kernel, dim3(cdiv((long)npad * ld, 256)), dim3(256), 0, d->stream, roll64,
+                       (int)d->n, (int)npad, d->net.A, ld, d->pg_d, d->pg_adv);
+    hipLaunchKernelGGL(pg_iv_kernel, dim3(1), dim3(cdiv(ld, 64) * 64), 0, d->stream, d->theta64, d->P, d->net.A, ld,
+                       d->pg_iv);
+    IterArgs a = plain_args(d, &d->ctl->zero);
+    a.pg_d4 = reinterpret_cast<const float4 *>(d->pg_d);
+    a.pg_adv = d->pg_adv;
+    a.pg_iv4 = reinterpret_cast<const float4 *>(d->pg_iv);
+    d->fast->launch_pg(dim3(d->grid), d->fast->lds, d->stream, a, d->net);
+    HCHK(hipGetLastError());
+    hipLaunchKernelGGL(reduce_slabs_kernel, dim3(cdiv(d->slab, 64)), dim3(1024), 0, d->stream, d->slabs, d->grid,
+                       d->slab, d->imap, d->zacc, &d->ctl->zero);
+    HCHK(hipGetLastError());
+    if (allreduce(d, d->zacc, d->nw)) return -4;
+    *zacc = d->zacc;
+    return 0;
+}

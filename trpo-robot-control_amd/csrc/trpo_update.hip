@@ -38,13 +38,15 @@ struct UpdState {
     double *sum = nullptr;                 // [P + 1]
     double *fs = nullptr;                  // fullstep [P]
     double *sums = nullptr;                // [64]
+    double *tpad = nullptr;                // register path: padded parameters [nk][PADW]
+    size_t tpad_cap = 0;
     int lds_set = 0;
 };
 
 void trpo_update_state_free(void *state) {
     UpdState *u = (UpdState *)state;
     if (!u) return;
-    void *ptrs[] = {u->roll, u->ws, u->slabs, u->sum, u->fs, u->sums};
+    void *ptrs[] = {u->roll, u->ws, u->slabs, u->sum, u->fs, u->sums, u->tpad};
     for (void *p : ptrs)
         if (p) hipFree(p);
     delete u;
@@ -81,20 +83,25 @@ struct ThetaStep {
     __device__ double operator[](int i) const { return t[i] + sf * f[i]; }
 };
 
-// forward pass of sample s into Y rows [row][UT] (rows of layer i start at roff[i]);
+// LDS / scratch activation rows are [row][RS]: the odd stride puts the rows a wave reads at
+// the same sample index in different banks during the contraction
+constexpr int RS = UT + 1;
+
+// forward pass of sample s into Y rows (rows of layer i start at roff[i]);
 // src/TRPO_Update.c:262-293 / :954-976
 template <class TH>
 __device__ void forward64(const Net &net, const TH &th, const double *__restrict__ obs, int s, bool live,
                           double *Y, const int *roff, int tid) {
     const int L0 = net.L[0];
-    for (int k = 0; k < L0; ++k) Y[k * UT + tid] = live ? obs[(long)s * L0 + k] : 0.0;
+    for (int k = 0; k < L0; ++k) Y[k * RS + tid] = live ? obs[(long)s * L0 + k] : 0.0;
     for (int i = 0; i + 1 < net.nl; ++i) {
         const int in = net.L[i], out = net.L[i + 1], a = net.act[i + 1];
         const int wo = net.woff[i], bo = net.boff[i];
         for (int j = 0; j < out; ++j) {
             double x = th[bo + j];
-            for (int k = 0; k < in; ++k) x += Y[(roff[i] + k) * UT + tid] * th[wo + k * out + j];
-            Y[(roff[i + 1] + j) * UT + tid] = act_y64(a, x);
+#pragma unroll 4
+            for (int k = 0; k < in; ++k) x += Y[(roff[i] + k) * RS + tid] * th[wo + k * out + j];
+            Y[(roff[i + 1] + j) * RS + tid] = act_y64(a, x);
         }
     }
 }
@@ -104,20 +111,65 @@ __device__ __forceinline__ void row_offsets(const Net &net, int *roff) {
     for (int i = 0; i < net.nl; ++i) roff[i + 1] = roff[i] + net.L[i];
 }
 
-// Policy gradient partial sums: block b accumulates, over its 64-sample passes, the
-// unnormalised gradient [GW, GB per layer, GLogStd] (src/TRPO_Update.c:295-378) plus
-// sum(Adv) at index P, into slabs[b][P + 1].
+// Sum over the pass's UT samples of every gradient entry, one parameter per thread, added into
+// the block's slab (fixed order).  yoff[i]: first row of layer i's outputs y_i (i < nl-1);
+// goff[i]: first row of the pre-activation gradient of layer i+1; gl: first of the A GLogStd
+// rows, followed by the Adv row (slab index P).
+__device__ void contract_pass(const Net &net, const double *Y, const int *yoff, const int *goff, int gl,
+                              double *__restrict__ slab, int tid) {
+    const int P = net.P, A = net.A;
+    for (int q = tid; q <= P; q += UT) {
+        const double *u = nullptr, *w = nullptr;
+        if (q >= P - A) {
+            w = Y + (long)(gl + q - (P - A)) * RS;
+        } else {
+            int i = 0;
+            while (i + 2 < net.nl && q >= net.woff[i + 1]) ++i;
+            const int in = net.L[i], out = net.L[i + 1], local = q - net.woff[i];
+            if (local < in * out) {
+                u = Y + (long)(yoff[i] + local / out) * RS;
+                w = Y + (long)(goff[i] + local % out) * RS;
+            } else {
+                w = Y + (long)(goff[i] + local - in * out) * RS;
+            }
+        }
+        double acc = 0.0;
+        if (u) {
+#pragma unroll 16
+            for (int t = 0; t < UT; ++t) acc += u[t] * w[t];
+        } else {
+#pragma unroll 16
+            for (int t = 0; t < UT; ++t) acc += w[t];
+        }
+        slab[q] += acc;
+    }
+}
+
+// Output seed of the policy gradient for one sample (src/TRPO_Update.c:297-303):
+// g = Adv (Action - Mean) / sigma^2 and the LogStd term, sigma = exp(LogStd).
+__device__ __forceinline__ void pg_seed(const double *rw, int A, int i, double logstd, double adv, double &g,
+                                        double &gls) {
+    const double es = exp(logstd);
+    const double temp = (rw[A + i] - rw[i]) / es;
+    g = adv * temp / es;
+    gls = adv * (temp * temp - 1.0);
+}
+
+// Policy gradient partial sums, any depth / widths: block b accumulates, over its 64-sample
+// passes, the unnormalised gradient [GW, GB per layer, GLogStd] (src/TRPO_Update.c:295-378)
+// plus sum(Adv) at index P, into slabs[b][P + 1].  Activations in Y rows (LDS or scratch).
 __global__ void __launch_bounds__(UT)
 pg_kernel(Net net, const double *__restrict__ th, const double *__restrict__ obs, const double *__restrict__ roll,
           int n, double *ws, int rows, int use_lds, double *__restrict__ slabs) {
     extern __shared__ double lds64[];
     const int tid = threadIdx.x;
-    double *Y = use_lds ? lds64 : ws + (long)blockIdx.x * rows * UT;
+    double *Y = use_lds ? lds64 : ws + (long)blockIdx.x * rows * RS;
     int roff[MAXL + 1];
     row_offsets(net, roff);
     const int tot = roff[net.nl], P = net.P, A = net.A, last = net.nl - 1;
-    double *G = Y + (long)tot * UT;            // gradient w.r.t. pre-activations, same rows as Y
-    double *GL = G + (long)tot * UT;           // A rows of per-sample GLogStd, then one row of Adv
+    const int G0 = tot, GL = 2 * tot;          // gradient rows mirror Y's; then GLogStd rows + Adv row
+    int goff[MAXL];
+    for (int i = 0; i + 1 < net.nl; ++i) goff[i] = G0 + roff[i + 1];
     double *slab = slabs + (long)blockIdx.x * (P + 1);
     const ThetaPlain T{th};
     for (int q = tid; q <= P; q += UT) slab[q] = 0.0;
@@ -128,57 +180,123 @@ pg_kernel(Net net, const double *__restrict__ th, const double *__restrict__ obs
         forward64(net, T, obs, s, live, Y, roff, tid);
         const double *rw = roll + (long)(live ? s : 0) * (2 * A + 1);
         const double adv = live ? rw[2 * A] : 0.0;
-        // output seed (src/TRPO_Update.c:297-303)
         for (int i = 0; i < A; ++i) {
-            const double es = exp(th[P - A + i]);
-            const double temp = (rw[A + i] - rw[i]) / es;
-            G[(roff[last] + i) * UT + tid] = live ? adv * temp / es : 0.0;
-            GL[i * UT + tid] = live ? adv * (temp * temp - 1.0) : 0.0;
+            double g, gls;
+            pg_seed(rw, A, i, th[P - A + i], adv, g, gls);
+            Y[(G0 + roff[last] + i) * RS + tid] = live ? g : 0.0;
+            Y[(GL + i) * RS + tid] = live ? gls : 0.0;
         }
-        GL[A * UT + tid] = adv;
+        Y[(GL + A) * RS + tid] = adv;
         // backprop (src/TRPO_Update.c:305-357); the unused input-layer gradient is skipped
         for (int i = last; i >= 1; --i) {
             const int cur = net.L[i], a = net.act[i];
             for (int j = 0; j < cur; ++j) {
-                const int e = (roff[i] + j) * UT + tid;
-                G[e] = act_d64(a, Y[e], G[e]);
+                const int e = (roff[i] + j) * RS + tid;
+                Y[G0 * RS + e] = act_d64(a, Y[e], Y[G0 * RS + e]);
             }
             if (i >= 2) {
                 const int prev = net.L[i - 1], wo = net.woff[i - 1];
                 for (int j = 0; j < prev; ++j) {
                     double t = 0.0;
-                    for (int k = 0; k < cur; ++k) t += G[(roff[i] + k) * UT + tid] * th[wo + j * cur + k];
-                    G[(roff[i - 1] + j) * UT + tid] = t;
+#pragma unroll 4
+                    for (int k = 0; k < cur; ++k) t += Y[(G0 + roff[i] + k) * RS + tid] * th[wo + j * cur + k];
+                    Y[(G0 + roff[i - 1] + j) * RS + tid] = t;
                 }
             }
         }
         __syncthreads();
-        // contraction over the pass's 64 samples, one parameter per thread (fixed order)
-        for (int q = tid; q <= P; q += UT) {
-            const double *u = nullptr, *w = nullptr;
-            if (q >= P - A) {
-                w = GL + (long)(q - (P - A)) * UT;     // GLogStd rows, then the Adv row at q == P
-            } else {
-                int i = 0;
-                while (i + 2 < net.nl && q >= net.woff[i + 1]) ++i;
-                const int in = net.L[i], out = net.L[i + 1], local = q - net.woff[i];
-                if (local < in * out) {
-                    u = Y + (long)(roff[i] + local / out) * UT;
-                    w = G + (long)(roff[i + 1] + local % out) * UT;
-                } else {
-                    w = G + (long)(roff[i + 1] + local - in * out) * UT;
-                }
-            }
-            double acc = 0.0;
-            if (u) {
-                for (int t = 0; t < UT; ++t) acc += u[t] * w[t];
-            } else {
-                for (int t = 0; t < UT; ++t) acc += w[t];
-            }
-            slab[q] += acc;
-        }
+        contract_pass(net, Y, roff, goff, GL, slab, tid);
         __syncthreads();
     }
+}
+
+// ---------------------------------------------------------------------------
+// Register path: 3 weight layers, every width <= RW.  Each lane keeps its sample's
+// activations and gradients in registers (fully unrolled over a zero-padded [RW][RW]
+// copy of the weights, read with scalar loads); only the rows the contraction needs go
+// through LDS.  Padding adds exact zeros, so the sums equal the unpadded ones.
+// ---------------------------------------------------------------------------
+constexpr int RW = 16;
+constexpr int PADL = RW * RW + RW;               // one padded layer: W [RW][RW] (in, out), B [RW]
+constexpr int PADW = 3 * PADL + RW;              // three layers, then LogStd [RW]
+
+// padded parameters theta + sf * fullstep (fs == nullptr: theta itself); blockIdx.y = candidate k
+__global__ void pad_theta_kernel(Net net, const double *__restrict__ th, const double *__restrict__ fs, int k0,
+                                 double *__restrict__ out) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= PADW) return;
+    const double sf = ldexp(1.0, -(k0 + (int)blockIdx.y));
+    int m = -1;
+    if (e < 3 * PADL) {
+        const int i = e / PADL, r = e % PADL;
+        const int in = net.L[i], out = net.L[i + 1];
+        if (r < RW * RW) {
+            const int k = r / RW, j = r % RW;
+            if (k < in && j < out) m = net.woff[i] + k * out + j;
+        } else if (r - RW * RW < out) {
+            m = net.boff[i] + r - RW * RW;
+        }
+    } else if (e - 3 * PADL < net.A) {
+        m = net.P - net.A + e - 3 * PADL;
+    }
+    out[(long)blockIdx.y * PADW + e] = m < 0 ? 0.0 : (fs ? th[m] + sf * fs[m] : th[m]);
+}
+
+__device__ __forceinline__ void act_vec(int a, double (&v)[RW]) {
+    if (a == ACT_T) {
+#pragma unroll
+        for (int j = 0; j < RW; ++j) v[j] = tanh(v[j]);
+    } else if (a == ACT_S) {
+#pragma unroll
+        for (int j = 0; j < RW; ++j) v[j] = 1.0 / (1.0 + exp(-v[j]));
+    } else if (a == ACT_O) {
+#pragma unroll
+        for (int j = 0; j < RW; ++j) v[j] = 0.1 * v[j];
+    }
+}
+__device__ __forceinline__ void actd_vec(int a, const double (&y)[RW], double (&g)[RW]) {
+#pragma unroll
+    for (int j = 0; j < RW; ++j) g[j] = act_d64(a, y[j], g[j]);
+}
+// dst = act(W^T src + B), W [RW][RW] (in, out) -- src/TRPO_Update.c:266-290 order per output
+__device__ __forceinline__ void layer_reg(const double *__restrict__ L, int a, const double (&src)[RW],
+                                          double (&dst)[RW]) {
+#pragma unroll
+    for (int j = 0; j < RW; ++j) {
+        double x = L[RW * RW + j];
+#pragma unroll
+        for (int k = 0; k < RW; ++k) x += src[k] * L[k * RW + j];
+        dst[j] = x;
+    }
+    act_vec(a, dst);
+}
+// dst[k] = sum_j src[j] W[k][j]  (gradient w.r.t. the layer's inputs, :351-356)
+__device__ __forceinline__ void back_reg(const double *__restrict__ L, const double (&src)[RW], double (&dst)[RW]) {
+#pragma unroll
+    for (int k = 0; k < RW; ++k) {
+        double t = 0.0;
+#pragma unroll
+        for (int j = 0; j < RW; ++j) t += src[j] * L[k * RW + j];
+        dst[k] = t;
+    }
+}
+
+__device__ __forceinline__ void forward_reg(const Net &net, const double *__restrict__ tp,
+                                            const double *__restrict__ obs, int s, bool live, double (&y0)[RW],
+                                            double (&y1)[RW], double (&y2)[RW], double (&y3)[RW]) {
+    const int L0 = net.L[0];
+#pragma unroll
+    for (int k = 0; k < RW; ++k) y0[k] = (live && k < L0) ? obs[(long)s * L0 + k] : 0.0;
+    layer_reg(tp, net.act[1], y0, y1);
+    layer_reg(tp + PADL, net.act[2], y1, y2);
+    layer_reg(tp + 2 * PADL, net.act[3], y2, y3);
+}
+
+__device__ __forceinline__ double lld_term(const double *rw, int A, int i, double mean_new, double logstd,
+                                           double stdv) {
+    const double tx = (rw[A + i] - rw[i]) / stdv;
+    const double tn = (rw[A + i] - mean_new) / exp(logstd);
+    return tx * tx - tn * tn + log(stdv) - logstd;
 }
 
 // Line-search surrogate: block (bx, k) sums Adv * exp(LLD) over its passes for candidate
@@ -189,7 +307,7 @@ surr_kernel(Net net, const double *__restrict__ th0, const double *__restrict__ 
             double *ws, int rows, int use_lds, double *__restrict__ parts) {
     extern __shared__ double lds64[];
     const int tid = threadIdx.x, k = blockIdx.y, nk = gridDim.y;
-    double *Y = use_lds ? lds64 : ws + ((long)k * gridDim.x + blockIdx.x) * rows * UT;
+    double *Y = use_lds ? lds64 : ws + ((long)k * gridDim.x + blockIdx.x) * rows * RS;
     int roff[MAXL + 1];
     row_offsets(net, roff);
     const int P = net.P, A = net.A, last = net.nl - 1;
@@ -203,17 +321,45 @@ surr_kernel(Net net, const double *__restrict__ th0, const double *__restrict__ 
         if (live) {
             const double *rw = roll + (long)s * (2 * A + 1);
             double lld = 0.0;
-            for (int i = 0; i < A; ++i) {
-                const double ls = T[P - A + i];
-                const double tx = (rw[A + i] - rw[i]) / stdv[i];
-                const double tn = (rw[A + i] - Y[(roff[last] + i) * UT + tid]) / exp(ls);
-                lld += tx * tx - tn * tn + log(stdv[i]) - ls;
-            }
+            for (int i = 0; i < A; ++i) lld += lld_term(rw, A, i, Y[(roff[last] + i) * RS + tid], T[P - A + i], stdv[i]);
             lld = lld * 0.5;
             acc += exp(lld) * rw[2 * A];
         }
     }
     // fixed-order wave tree
+    for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if (tid == 0) parts[(long)blockIdx.x * nk + k] = acc;
+}
+
+// Line-search surrogate, register path; tp = the nk padded candidates [nk][PADW].
+__global__ void __launch_bounds__(UT)
+surr_reg_kernel(Net net, const double *__restrict__ tpk, const double *__restrict__ obs,
+                const double *__restrict__ roll, const double *__restrict__ stdv, int n,
+                double *__restrict__ parts) {
+    const int tid = threadIdx.x, k = blockIdx.y, nk = gridDim.y, A = net.A;
+    __shared__ double tpw[PADW];
+    for (int e = tid; e < PADW; e += UT) tpw[e] = tpk[(long)k * PADW + e];
+    __syncthreads();
+    double acc = 0.0;
+    const int npass = (n + UT - 1) / UT;
+    for (int pass = blockIdx.x; pass < npass; pass += gridDim.x) {
+        const int s = pass * UT + tid;
+        const bool live = s < n;
+        int wb = 0;
+        asm volatile("" : "+s"(wb));
+        const double *tpl = tpw + wb;
+        double y0[RW], y1[RW], y2[RW], y3[RW];
+        forward_reg(net, tpl, obs, s, live, y0, y1, y2, y3);
+        if (live) {
+            const double *rw = roll + (long)s * (2 * A + 1);
+            double lld = 0.0;
+#pragma unroll
+            for (int i = 0; i < RW; ++i)
+                if (i < A) lld += lld_term(rw, A, i, y3[i], tpl[3 * PADL + i], stdv[i]);
+            lld = lld * 0.5;
+            acc += exp(lld) * rw[2 * A];
+        }
+    }
     for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
     if (tid == 0) parts[(long)blockIdx.x * nk + k] = acc;
 }
@@ -225,8 +371,10 @@ sum_slabs64_kernel(const double *__restrict__ slabs, int G, int len, double *__r
     const int tq = threadIdx.x & 15, tj = threadIdx.x >> 4;
     const int q = blockIdx.x * 16 + tq;
     double s = 0.0;
-    if (q < len)
+    if (q < len) {
+#pragma unroll 8
         for (int b = tj; b < G; b += 16) s += slabs[(long)b * len + q];
+    }
     part[tj][tq] = s;
     __syncthreads();
     if (tj == 0 && q < len) {
@@ -240,6 +388,42 @@ sum_slabs64_kernel(const double *__restrict__ slabs, int G, int len, double *__r
 __global__ void pg_finish_kernel(const double *__restrict__ sum, double n_total, int P, double *__restrict__ b) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q < P) b[q] = sum[q] / n_total;
+}
+
+// same, with the weight/bias sums from the tile kernel (wsum, P - A entries) and the LogStd
+// sums (lsum, A entries) kept apart
+__global__ void pg_finish2_kernel(const double *__restrict__ wsum, const double *__restrict__ lsum, double n_total,
+                                  int P, int A, double *__restrict__ b) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < P) b[q] = (q < P - A ? wsum[q] : lsum[q - (P - A)]) / n_total;
+}
+
+// LogStd part of the policy gradient and sum(Adv), fp64: block b writes
+// slabs[b][i] = sum over its samples of Adv ((Action - Mean)^2 / sigma^2 - 1)  (i < A),
+// slabs[b][A] = sum of Adv  (src/TRPO_Update.c:297-303, :372)
+__global__ void __launch_bounds__(UT)
+pg_logstd_kernel(const double *__restrict__ th, int P, int A, const double *__restrict__ roll, int n,
+                 double *__restrict__ slabs) {
+    const int tid = threadIdx.x, W = 2 * A + 1;
+    const int npass = (n + UT - 1) / UT;
+    for (int i = 0; i <= A; ++i) {
+        const double es = i < A ? exp(th[P - A + i]) : 1.0;
+        double acc = 0.0;
+        for (int pass = blockIdx.x; pass < npass; pass += gridDim.x) {
+            const int s = pass * UT + tid;
+            if (s < n) {
+                const double *rw = roll + (long)s * W;
+                if (i < A) {
+                    const double temp = (rw[A + i] - rw[i]) / es;
+                    acc += rw[2 * A] * (temp * temp - 1.0);
+                } else {
+                    acc += rw[2 * A];
+                }
+            }
+        }
+        for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+        if (tid == 0) slabs[(long)blockIdx.x * (A + 1) + i] = acc;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -268,22 +452,35 @@ static int rows_for(const Net &net, bool grads) {
     return grads ? 2 * tot + net.A + 1 : tot;
 }
 
+// register path: 3 weight layers, all widths <= RW (env TRPO_UPDATE_GENERIC=1 forces the other)
+static bool reg_path(const Net &net) {
+    const char *e = getenv("TRPO_UPDATE_GENERIC");
+    if (e && atoi(e)) return false;
+    if (net.nl != 4) return false;
+    for (int i = 0; i < 4; ++i)
+        if (net.L[i] > RW) return false;
+    return true;
+}
+
+static int set_lds_attrs(UpdState *u) {
+    if (u->lds_set) return 0;
+    HCHK(hipFuncSetAttribute((const void *)pg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_CAP));
+    HCHK(hipFuncSetAttribute((const void *)surr_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_CAP));
+    u->lds_set = 1;
+    return 0;
+}
+
 // activation storage for `blocks` workgroups of `rows` rows: LDS when it fits (returns the
 // dynamic LDS bytes), else a global scratch (returns 0)
-static int act_storage(UpdState *u, const Net &net, int rows, long blocks, hipStream_t st, int *use_lds) {
-    const size_t bytes = sizeof(double) * (size_t)rows * UT;
+static int act_storage(UpdState *u, int rows, long blocks, hipStream_t st, int *use_lds) {
+    const size_t bytes = sizeof(double) * (size_t)rows * RS;
+    if (set_lds_attrs(u)) return -1;
     if (bytes <= (size_t)LDS_CAP) {
-        if (!u->lds_set) {
-            HCHK(hipFuncSetAttribute((const void *)pg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_CAP));
-            HCHK(hipFuncSetAttribute((const void *)surr_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_CAP));
-            u->lds_set = 1;
-        }
         *use_lds = 1;
         return (int)bytes;
     }
-    (void)net;
     *use_lds = 0;
-    if (ensure(&u->ws, &u->ws_cap, (size_t)rows * UT * blocks, st)) return -1;
+    if (ensure(&u->ws, &u->ws_cap, (size_t)rows * RS * blocks, st)) return -1;
     return 0;
 }
 
@@ -322,15 +519,37 @@ extern "C" int trpo_dev_policy_gradient(trpo_dev *d, double *b_host, double *adv
     HCHK(hipSetDevice(v.device));
     const Net &net = v.net;
     const int P = net.P, n = (int)v.n;
-    const int G = n ? (cdiv(n, UT) < 2048 ? cdiv(n, UT) : 2048) : 1;
-    const int rows = rows_for(net, true);
-    int use_lds = 0;
-    const int lds = act_storage(u, net, rows, G, v.stream, &use_lds);
-    if (lds < 0) return -2;
+    const int G = n ? (cdiv(n, UT) < 1024 ? cdiv(n, UT) : 1024) : 1;
     if (ensure(&u->slabs, &u->slab_cap, (size_t)G * (P + 1), v.stream)) return -2;
     if (!u->sum) HCHK(hipMalloc((void **)&u->sum, sizeof(double) * (P + 1)));
-    hipLaunchKernelGGL(pg_kernel, dim3(G), dim3(UT), lds, v.stream, net, v.theta64, v.obs64, u->roll, n, u->ws, rows,
-                       use_lds, u->slabs);
+    const char *eg = getenv("TRPO_UPDATE_GENERIC");
+    const double *wsum = nullptr;
+    int fast = (eg && atoi(eg)) ? 1 : trpo_dev_pg_sums_fast(d, u->roll, &wsum);
+    if (fast < 0) return fast;
+    if (fast == 0) {
+        // weights / biases by the MFMA tile kernel (fp32 per sample, fp64 sums); LogStd + Adv in fp64
+        const int A = net.A;
+        hipLaunchKernelGGL(pg_logstd_kernel, dim3(G), dim3(UT), 0, v.stream, v.theta64, P, A, u->roll, n, u->slabs);
+        hipLaunchKernelGGL(sum_slabs64_kernel, dim3(cdiv(A + 1, 16)), dim3(256), 0, v.stream, u->slabs, G, A + 1,
+                           u->sum);
+        HCHK(hipGetLastError());
+        if (trpo_dev_allreduce64(d, u->sum, (size_t)A + 1)) return -4;
+        hipLaunchKernelGGL(pg_finish2_kernel, dim3(cdiv(P, 256)), dim3(256), 0, v.stream, wsum, u->sum, v.n_total,
+                           P, A, v.vec_b);
+        HCHK(hipGetLastError());
+        if (b_host) HCHK(hipMemcpyAsync(b_host, v.vec_b, sizeof(double) * P, hipMemcpyDeviceToHost, v.stream));
+        if (adv_sum) HCHK(hipMemcpyAsync(adv_sum, u->sum + A, sizeof(double), hipMemcpyDeviceToHost, v.stream));
+        HCHK(hipStreamSynchronize(v.stream));
+        return 0;
+    }
+    {
+        const int rows = rows_for(net, true);
+        int use_lds = 0;
+        const int lds = act_storage(u, rows, G, v.stream, &use_lds);
+        if (lds < 0) return -2;
+        hipLaunchKernelGGL(pg_kernel, dim3(G), dim3(UT), lds, v.stream, net, v.theta64, v.obs64, u->roll, n, u->ws,
+                           rows, use_lds, u->slabs);
+    }
     hipLaunchKernelGGL(sum_slabs64_kernel, dim3(cdiv(P + 1, 16)), dim3(256), 0, v.stream, u->slabs, G, P + 1, u->sum);
     HCHK(hipGetLastError());
     if (trpo_dev_allreduce64(d, u->sum, (size_t)P + 1)) return -4;
@@ -353,16 +572,24 @@ extern "C" int trpo_dev_surrogate(trpo_dev *d, const double *fullstep, int k0, i
     const int P = net.P, n = (int)v.n;
     const int cap = 2048 / nk > 0 ? 2048 / nk : 1;
     const int Gs = n ? (cdiv(n, UT) < cap ? cdiv(n, UT) : cap) : 1;
-    const int rows = rows_for(net, false);
-    int use_lds = 0;
-    const int lds = act_storage(u, net, rows, (long)Gs * nk, v.stream, &use_lds);
-    if (lds < 0) return -2;
     if (!u->fs) HCHK(hipMalloc((void **)&u->fs, sizeof(double) * P));
     if (ensure(&u->slabs, &u->slab_cap, (size_t)Gs * nk, v.stream)) return -2;
     if (!u->sums) HCHK(hipMalloc((void **)&u->sums, sizeof(double) * 64));
     HCHK(hipMemcpyAsync(u->fs, fullstep, sizeof(double) * P, hipMemcpyHostToDevice, v.stream));
-    hipLaunchKernelGGL(surr_kernel, dim3(Gs, nk), dim3(UT), lds, v.stream, net, v.theta64, u->fs, k0, v.obs64,
-                       u->roll, v.std64, n, u->ws, rows, use_lds, u->slabs);
+    if (reg_path(net)) {
+        if (ensure(&u->tpad, &u->tpad_cap, (size_t)PADW * nk, v.stream)) return -2;
+        hipLaunchKernelGGL(pad_theta_kernel, dim3(cdiv(PADW, 256), nk), dim3(256), 0, v.stream, net, v.theta64,
+                           (const double *)u->fs, k0, u->tpad);
+        hipLaunchKernelGGL(surr_reg_kernel, dim3(Gs, nk), dim3(UT), 0, v.stream, net, (const double *)u->tpad,
+                           v.obs64, u->roll, v.std64, n, u->slabs);
+    } else {
+        const int rows = rows_for(net, false);
+        int use_lds = 0;
+        const int lds = act_storage(u, rows, (long)Gs * nk, v.stream, &use_lds);
+        if (lds < 0) return -2;
+        hipLaunchKernelGGL(surr_kernel, dim3(Gs, nk), dim3(UT), lds, v.stream, net, v.theta64, u->fs, k0, v.obs64,
+                           u->roll, v.std64, n, u->ws, rows, use_lds, u->slabs);
+    }
     hipLaunchKernelGGL(sum_slabs64_kernel, dim3(cdiv(nk, 16)), dim3(256), 0, v.stream, u->slabs, Gs, nk, u->sums);
     HCHK(hipGetLastError());
     if (trpo_dev_allreduce64(d, u->sums, (size_t)nk)) return -4;
