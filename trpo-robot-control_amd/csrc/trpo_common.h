@@ -50,6 +50,7 @@ struct trpo_dev_view {
     size_t n;                  // local samples
     double n_total;            // global samples (all ranks)
     double *vec_b;             // CG right-hand side slot (TRPO_VEC_B)
+    double *vec_x, *vec_v, *vec_z;
 };
 void trpo_dev_get_view(trpo_dev *d, trpo_dev_view *v);
 // in-place fp64 sum over the attached RCCL communicator (no-op without one)

@@ -49,6 +49,10 @@ double trpo_dev_time(trpo_dev *d, int what, int reps, size_t maxiter, double res
 int trpo_dev_set_rollout(trpo_dev *d, const double *mean, const double *action, const double *adv, size_t n);
 int trpo_dev_policy_gradient(trpo_dev *d, double *b_host, double *adv_sum);
 int trpo_dev_surrogate(trpo_dev *d, const double *fullstep, int k0, int nk, double *surr_host);
+/* The device phase of one update with ONE host synchronisation: policy gradient -> slot B,
+ * CG(maxiter, resth) -> slot X, FVP(x) -> slot Z; then b, x, z and sum(Adv) to the host. */
+int trpo_dev_update_solve(trpo_dev *d, size_t maxiter, double resth, double *b, double *x, double *z,
+                          double *adv_sum);
 
 const char *trpo_dev_kernel_name(const trpo_dev *d);
 int trpo_dev_geometry(const trpo_dev *d, int *blocks, int *threads, int *lds_bytes);

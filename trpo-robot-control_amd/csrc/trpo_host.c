@@ -243,14 +243,10 @@ double trpo_ctx_update(trpo_ctx *c, size_t max_iter, double resth, double max_kl
     if (!b || !x || !z || !fullstep) goto out;
     const double t0 = now_s();
     double adv_sum = 0.0;
-    int rc = trpo_dev_policy_gradient(c->dev, b, &adv_sum);                    /* :254-378 */
-    if (!rc) rc = trpo_dev_cg(c->dev, max_iter, resth);                         /* :383-628 */
-    if (!rc) rc = trpo_dev_download(c->dev, TRPO_VEC_X, x);
+    /* policy gradient (:254-378), CG (:383-628) and FVP(x) (:633-832) on the device, one sync */
+    int rc = trpo_dev_update_solve(c->dev, max_iter, resth, b, x, z, &adv_sum);
     if (!rc && verbose) print_cg_lines(c, max_iter, &inf.cg_iters);
-    else if (!rc) trpo_dev_cg_history(c->dev, NULL, NULL, 0, &inf.cg_iters);
-    if (!rc) rc = trpo_dev_upload(c->dev, TRPO_VEC_V, x);                      /* :633-832 */
-    if (!rc) rc = trpo_dev_fvp(c->dev);
-    if (!rc) rc = trpo_dev_download(c->dev, TRPO_VEC_Z, z);
+    else if (!rc && info) trpo_dev_cg_history(c->dev, NULL, NULL, 0, &inf.cg_iters);
     if (rc) {
         set_err("TRPO update failed on the device (code %d)", rc);
         ret = rc < 0 ? rc : TRPO_E_DEVICE;

@@ -2053,6 +2053,9 @@ void trpo_dev_get_view(trpo_dev *d, trpo_dev_view *v) {
     v->n = d->n;
     v->n_total = d->n_total;
     v->vec_b = d->vec[TRPO_VEC_B];
+    v->vec_x = d->vec[TRPO_VEC_X];
+    v->vec_v = d->vec[TRPO_VEC_V];
+    v->vec_z = d->vec[TRPO_VEC_Z];
 }
 
 int trpo_dev_allreduce64(trpo_dev *d, double *buf, size_t count) { return allreduce(d, buf, count); }

@@ -510,7 +510,8 @@ extern "C" int trpo_dev_set_rollout(trpo_dev *d, const double *mean, const doubl
     return 0;
 }
 
-extern "C" int trpo_dev_policy_gradient(trpo_dev *d, double *b_host, double *adv_sum) {
+// enqueue the policy gradient into slot B; *adv_dev = device address of the global sum(Adv)
+static int enqueue_policy_gradient(trpo_dev *d, const double **adv_dev) {
     if (!d) return -1;
     trpo_dev_view v;
     trpo_dev_get_view(d, &v);
@@ -537,9 +538,7 @@ extern "C" int trpo_dev_policy_gradient(trpo_dev *d, double *b_host, double *adv
         hipLaunchKernelGGL(pg_finish2_kernel, dim3(cdiv(P, 256)), dim3(256), 0, v.stream, wsum, u->sum, v.n_total,
                            P, A, v.vec_b);
         HCHK(hipGetLastError());
-        if (b_host) HCHK(hipMemcpyAsync(b_host, v.vec_b, sizeof(double) * P, hipMemcpyDeviceToHost, v.stream));
-        if (adv_sum) HCHK(hipMemcpyAsync(adv_sum, u->sum + A, sizeof(double), hipMemcpyDeviceToHost, v.stream));
-        HCHK(hipStreamSynchronize(v.stream));
+        *adv_dev = u->sum + A;
         return 0;
     }
     {
@@ -555,8 +554,39 @@ extern "C" int trpo_dev_policy_gradient(trpo_dev *d, double *b_host, double *adv
     if (trpo_dev_allreduce64(d, u->sum, (size_t)P + 1)) return -4;
     hipLaunchKernelGGL(pg_finish_kernel, dim3(cdiv(P, 256)), dim3(256), 0, v.stream, u->sum, v.n_total, P, v.vec_b);
     HCHK(hipGetLastError());
-    if (b_host) HCHK(hipMemcpyAsync(b_host, v.vec_b, sizeof(double) * P, hipMemcpyDeviceToHost, v.stream));
-    if (adv_sum) HCHK(hipMemcpyAsync(adv_sum, u->sum + P, sizeof(double), hipMemcpyDeviceToHost, v.stream));
+    *adv_dev = u->sum + P;
+    return 0;
+}
+
+extern "C" int trpo_dev_policy_gradient(trpo_dev *d, double *b_host, double *adv_sum) {
+    const double *adv_dev = nullptr;
+    int rc = enqueue_policy_gradient(d, &adv_dev);
+    if (rc) return rc;
+    trpo_dev_view v;
+    trpo_dev_get_view(d, &v);
+    if (b_host) HCHK(hipMemcpyAsync(b_host, v.vec_b, sizeof(double) * v.net.P, hipMemcpyDeviceToHost, v.stream));
+    if (adv_sum) HCHK(hipMemcpyAsync(adv_sum, adv_dev, sizeof(double), hipMemcpyDeviceToHost, v.stream));
+    HCHK(hipStreamSynchronize(v.stream));
+    return 0;
+}
+
+extern "C" int trpo_dev_update_solve(trpo_dev *d, size_t maxiter, double resth, double *b, double *x, double *z,
+                                     double *adv_sum) {
+    if (!d || !b || !x || !z || !adv_sum) return -1;
+    const double *adv_dev = nullptr;
+    int rc = enqueue_policy_gradient(d, &adv_dev);            // :254-378
+    if (!rc) rc = trpo_dev_cg(d, maxiter, resth);              // :383-628 (graph replay)
+    if (rc) return rc;
+    trpo_dev_view v;
+    trpo_dev_get_view(d, &v);
+    const size_t bytes = sizeof(double) * v.net.P;
+    HCHK(hipMemcpyAsync(v.vec_v, v.vec_x, bytes, hipMemcpyDeviceToDevice, v.stream));
+    rc = trpo_dev_fvp(d);                                       // :633-832, z = F x
+    if (rc) return rc;
+    HCHK(hipMemcpyAsync(b, v.vec_b, bytes, hipMemcpyDeviceToHost, v.stream));
+    HCHK(hipMemcpyAsync(x, v.vec_x, bytes, hipMemcpyDeviceToHost, v.stream));
+    HCHK(hipMemcpyAsync(z, v.vec_z, bytes, hipMemcpyDeviceToHost, v.stream));
+    HCHK(hipMemcpyAsync(adv_sum, adv_dev, sizeof(double), hipMemcpyDeviceToHost, v.stream));
     HCHK(hipStreamSynchronize(v.stream));
     return 0;
 }
