@@ -178,6 +178,26 @@ __device__ void block_sum2(double a, double b, double *sh, double &sa, double &s
 // ---------------------------------------------------------------------------
 // activation helpers (reference src/TRPO_FVP.c:810-834 and :866-882)
 // ---------------------------------------------------------------------------
+// fp32 tanh for the tile kernel: |x| < 0.625 odd polynomial x(1 + x^2 Q(x^2)) (Chebyshev-node
+// least squares, degree 4), else 1 - 2 / (e^{2|x|} + 1) with the hardware exp2 / rcp.  Max
+// relative error 1.5e-7 (tools/fit_tanh.py), 14 VALU ops against ~22 for the libm tanhf; the tile
+// loop is VALU+MFMA issue bound, so this is time.  Same function in every FVP => the small
+// deviation from tanhf is a fixed perturbation of F, not noise across CG iterations.
+__device__ __forceinline__ float tanh_fast(float x) {
+    const float ax = fabsf(x), u = x * x;
+    float q = fmaf(u, -0.006104945205152035f, 0.021003639325499535f);
+    q = fmaf(u, q, -0.05385249853134155f);
+    q = fmaf(u, q, 0.13332782685756683f);
+    q = fmaf(u, q, -0.333333283662796f);
+    const float ts = fmaf(ax * u, q, ax);
+    const float e = __builtin_amdgcn_exp2f(ax * 2.8853900817779268f);      // e^{2|x|}
+    const float tb = fmaf(-2.0f, __builtin_amdgcn_rcpf(e + 1.0f), 1.0f);
+    return copysignf(ax < 0.625f ? ts : tb, x);
+}
+// fp32 logistic 1 / (1 + e^{-x}) with the hardware exp2 / rcp
+__device__ __forceinline__ float sigmoid_fast(float x) {
+    return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
+}
 __device__ __forceinline__ float act_y(int a, float x) {
     switch (a) {
     case ACT_T: return tanhf(x);
@@ -200,13 +220,13 @@ __device__ __forceinline__ f4 act_fwd(int a, f4 x, f4 rx, f4 &ry) {
     if (a == ACT_T) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            y[r] = tanhf(x[r]);
+            y[r] = tanh_fast(x[r]);
             ry[r] = rx[r] * (1.0f - y[r] * y[r]);
         }
     } else if (a == ACT_S) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            y[r] = 1.0f / (1.0f + expf(-x[r]));
+            y[r] = sigmoid_fast(x[r]);
             ry[r] = rx[r] * y[r] * (1.0f - y[r]);
         }
     } else if (a == ACT_O) {
