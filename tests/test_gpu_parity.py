@@ -176,3 +176,30 @@ def test_output_widths_and_activations_against_oracle(layers, acts):
     with trpo_amd.Context(layers, acts, th, obs, std) as ctx:
         assert ctx.kernel_name.startswith("mfma-mlp3")
         assert cases.rel_l2(ctx.fvp(v), ref) <= FVP_TOL
+
+
+@pytest.mark.parametrize("layers", [[15, 32, 32, 3], [20, 32, 32, 2], [30, 64, 64, 4], [15, 64, 64, 3]])
+@pytest.mark.parametrize("coop", ["1", "0"])
+def test_cooperative_kernel_shapes_against_oracle(layers, coop, monkeypatch):
+    """Wide hidden layers run the cooperative tile kernel (TRPO_COOP=0: the one-wave-per-tile
+    kernel); FVP, CG and the policy gradient against the oracle."""
+    import oracle
+    from trpo_amd import synth
+    monkeypatch.setenv("TRPO_COOP", coop)
+    n = 2345
+    th, obs = synth.make_theta(layers), synth.make_obs(n, layers[0])
+    std = np.linspace(0.8, 1.1, layers[-1])
+    P = synth.num_params(layers)
+    v, b = synth.make_v(P), synth.make_b(P)
+    ref, _ = oracle.fvp(layers, "lttl", th, obs, std, v)
+    with trpo_amd.Context(layers, "lttl", th, obs, std) as ctx:
+        assert ctx.kernel_name.endswith(" coop") == (coop == "1")
+        assert cases.rel_l2(ctx.fvp(v), ref) <= FVP_TOL
+        x = ctx.cg(b, 10, 0.0)
+        xr = oracle.cg(layers, "lttl", th, obs, std, b, 10, 0.0)["x"]
+        assert cases.rel_l2(x, xr) <= 2e-3          # fp32 FVP in an ill-conditioned 10-step CG (DESIGN §3)
+        mean, action, adv = synth.make_rollout(layers, "lttl", th, obs, std)
+        ctx.set_rollout(mean, action, adv)
+        r = ctx.update()
+        bref, _ = oracle.policy_grad(layers, "lttl", th, obs, mean, action, adv)
+        assert cases.rel_l2(r["b"], bref) <= 2e-6

@@ -1033,6 +1033,295 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
 }
 
 // ---------------------------------------------------------------------------
+// Cooperative tile kernel for wide hidden layers (T1 == T2 == TH in {2, 4}, T3 == 1, e.g. the
+// 2x64-tanh policy): the TH waves of a GROUP process one 16-sample tile together, wave w owning
+// hidden row tile w of layers 1 and 2.  Per tile a wave issues 1/TH of the MFMAs, holds only its
+// own weight fragments (in registers) and its own slice of the gradient accumulators, and the
+// block's 8 waves are NG = 8 / TH groups -- so the end-of-block combine is NG-way instead of
+// 8-way and the per-tile latency is ~1/TH of the one-wave-per-tile kernel.  Exchanges through
+// LDS (double-buffered by tile parity): y1/Ry1 after layer 0, the layer-2 partial products over
+// the row tiles, and G2.  MODE 0: FVP; MODE 1: policy gradient (as fvp_mlp3_kernel).
+// ---------------------------------------------------------------------------
+template <int T0, int TH>
+struct CoopCfg {
+    static constexpr int WAVES = 8, GW = TH, NG = WAVES / GW, THREADS = 64 * WAVES;
+    static constexpr int NW = T0 + TH + 4;                 // accumulator f4 per lane per wave
+    static constexpr int SLAB = TH * NW * 256;             // floats per block partial
+    // LDS, f4 units: exchange buffers [parity][group][row tile][...][lane]
+    static constexpr int XB = 0, XB_N = 2 * NG * TH * 2 * 64;
+    static constexpr int PB = XB + XB_N, PB_N = 2 * NG * TH * 2 * 64;
+    static constexpr int GB = PB + PB_N, GB_N = 2 * NG * TH * 64;
+    static constexpr int EX_F4 = GB + GB_N;
+    static constexpr int SROWS = 16 * (TH + 1 > T0 + 1 ? TH + 1 : T0 + 1);   // per-wave transpose rows
+    static constexpr int SCR = SROWS * SCR_LD;             // floats per wave
+    static constexpr int COMB_F4 = (NG - 1) * TH * NW * 64; // group-combine dump (aliases exchange)
+    static constexpr int MAIN_F4 = EX_F4 > COMB_F4 ? EX_F4 : COMB_F4;
+    static constexpr int LDS_BYTES = 16 * MAIN_F4 + 4 * WAVES * SCR;
+    static_assert(TH == 2 || TH == 4, "TH");
+};
+
+// slab position -> natural parameter (or -1) for the cooperative kernel's accumulator order
+// [wave w][k][lane][r], k over RGW0 tiles (kt0, w), RGW1 tiles (at, w), RGW2 tile (w, 0),
+// B1 tile w, B2 tile w, B3 (wave 0 only).
+__device__ __forceinline__ int imap_coop_at(const Net &n, int T0, int TH, int j) {
+    const int NW = T0 + TH + 4;
+    const int w = j / (NW * 256), rem = j % (NW * 256);
+    const int k = rem >> 8, lane = (rem >> 2) & 63, r = rem & 3, c = lane & 15, g = lane >> 4;
+    int i, a, b;
+    if (k < T0) { i = 0; a = 16 * k + 4 * g + r; b = 16 * w + c; }
+    else if (k < T0 + TH) { i = 1; a = 16 * (k - T0) + 4 * g + r; b = 16 * w + c; }
+    else if (k == T0 + TH) { i = 2; a = 16 * w + 4 * g + r; b = c; }
+    else {
+        const int bi = k - (T0 + TH + 1);                 // 0: B1, 1: B2, 2: B3
+        if (c != 0 || (bi == 2 && w != 0)) return -1;
+        const int nb = bi == 2 ? 4 * g + r : 16 * w + 4 * g + r;
+        return nb < n.L[bi + 1] ? n.boff[bi] + nb : -1;
+    }
+    return (a < n.L[i] && b < n.L[i + 1]) ? n.woff[i] + a * n.L[i + 1] + b : -1;
+}
+
+__global__ void build_imap_coop_kernel(Net n, int T0, int TH, int *imap, int len) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < len) imap[j] = imap_coop_at(n, T0, TH, j);
+}
+
+template <int T0, int TH, int ACT, int MODE>
+__global__ void __launch_bounds__(512)
+fvp_coop_kernel(IterArgs A, Net net) {
+    using Q = CoopCfg<T0, TH>;
+    using C = FastCfg<T0, TH, TH, 1>;                      // pack offsets (same fragment packs)
+    constexpr bool FV = MODE == 0;
+    constexpr int T1 = TH, T2 = TH;
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    f4 *L4 = reinterpret_cast<f4 *>(lds);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int c = lane & 15, g = lane >> 4, grp = wave / Q::GW, w = wave % Q::GW;
+    float *scr = lds + 4 * Q::MAIN_F4 + wave * Q::SCR;
+    const int ntiles = A.ntiles, n = A.n;
+    const f4 *obs4 = reinterpret_cast<const f4 *>(A.obs4);
+    const f4 *TP = reinterpret_cast<const f4 *>(A.tpack);
+    const f4 *VP = reinterpret_cast<const f4 *>(A.vpack);
+    if (*A.skip) return;                                   // grid-uniform
+
+    // this wave's weight fragments (theta and direction packs), straight to registers
+    f4 fa0[T0], vfa0[T0], fa1[T1], vfa1[T1], fb1[T2];
+#pragma unroll
+    for (int kt = 0; kt < T0; ++kt) {
+        fa0[kt] = TP[C::FA0 / 4 + (w * T0 + kt) * 64 + lane];
+        vfa0[kt] = FV ? VP[C::VFA0 / 4 + (w * T0 + kt) * 64 + lane] : f4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int kt = 0; kt < T1; ++kt) {
+        fa1[kt] = TP[C::FA1 / 4 + (w * T1 + kt) * 64 + lane];
+        vfa1[kt] = FV ? VP[C::VFA1 / 4 + (w * T1 + kt) * 64 + lane] : f4{0.f, 0.f, 0.f, 0.f};
+        fb1[kt] = TP[C::FB1 / 4 + (w * T2 + kt) * 64 + lane];
+    }
+    const f4 fa2 = TP[C::FA2 / 4 + w * 64 + lane];
+    const f4 vfa2 = FV ? VP[C::VFA2 / 4 + w * 64 + lane] : f4{0.f, 0.f, 0.f, 0.f};
+    const f4 fb2 = TP[C::FB2 / 4 + w * 64 + lane];
+    const f4 b0w = TP[C::BI0 / 4 + w * 4 + g], b1w = TP[C::BI1 / 4 + w * 4 + g], b2 = TP[C::BI2 / 4 + g];
+    const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
+    const f4 vb0w = FV ? VP[C::VB0 / 4 + w * 4 + g] : zero4, vb1w = FV ? VP[C::VB1 / 4 + w * 4 + g] : zero4;
+    const f4 vb2 = FV ? VP[C::VB2 / 4 + g] : zero4, iv = TP[C::IV / 4 + g];
+
+    const int a1 = ACT >= 0 ? (ACT & 3) : net.act[1];
+    const int a2 = ACT >= 0 ? ((ACT >> 2) & 3) : net.act[2];
+    const int a3 = ACT >= 0 ? ((ACT >> 4) & 3) : net.act[3];
+    const bool y3_needed = act_needs_y(a3);
+
+    f4 accW0[T0], accW1[T1], accW2 = zero4, sB1 = zero4, sB2 = zero4, sB3 = zero4;
+#pragma unroll
+    for (int k = 0; k < T0; ++k) accW0[k] = zero4;
+#pragma unroll
+    for (int k = 0; k < T1; ++k) accW1[k] = zero4;
+
+    // every wave of the block runs the same number of tile steps (barriers inside)
+    const int gstride = gridDim.x * Q::NG;
+    const int nsteps = (ntiles + gstride - 1) / gstride;
+    for (int step = 0; step < nsteps; ++step) {
+        const int tile = step * gstride + blockIdx.x * Q::NG + grp;
+        const int tc = min(tile, ntiles - 1);
+        const bool live = tile < ntiles && tc * 16 + c < n;
+        const int par = step & 1;
+        f4 *xb = L4 + Q::XB + ((par * Q::NG + grp) * TH) * 128;     // [row tile][2][64]
+        f4 *pb = L4 + Q::PB + ((par * Q::NG + grp) * TH) * 128;
+        f4 *gb = L4 + Q::GB + ((par * Q::NG + grp) * TH) * 64;
+        f4 x0[T0];
+#pragma unroll
+        for (int kt = 0; kt < T0; ++kt) x0[kt] = obs4[(long)(tc * 16 + c) * (4 * T0) + kt * 4 + g];
+
+        // ---- layer 0, row tile w ----
+        f4 a = b0w, ra = vb0w;
+#pragma unroll
+        for (int kt = 0; kt < T0; ++kt)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                a = MFMA(fa0[kt][s], x0[kt][s], a);
+                if constexpr (FV) ra = MFMA(vfa0[kt][s], x0[kt][s], ra);
+            }
+        f4 r1w;
+        const f4 y1w = act_fwd(a1, a, ra, r1w);
+        xb[w * 128 + lane] = y1w;
+        if constexpr (FV) xb[w * 128 + 64 + lane] = r1w;
+        __syncthreads();
+        f4 y1[T1], r1[T1];
+#pragma unroll
+        for (int kt = 0; kt < T1; ++kt) {
+            y1[kt] = xb[kt * 128 + lane];
+            r1[kt] = FV ? xb[kt * 128 + 64 + lane] : zero4;
+        }
+
+        // ---- layer 1, row tile w ----
+        a = b1w;
+        ra = vb1w;
+        f4 rb = zero4;
+#pragma unroll
+        for (int kt = 0; kt < T1; ++kt)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                a = MFMA(fa1[kt][s], y1[kt][s], a);
+                if constexpr (FV) {
+                    ra = MFMA(fa1[kt][s], r1[kt][s], ra);
+                    rb = MFMA(vfa1[kt][s], y1[kt][s], rb);
+                }
+            }
+        f4 r2w;
+        const f4 y2w = act_fwd(a2, a, ra + rb, r2w);
+
+        // ---- layer 2: this wave's share (input row tile w), summed over the group in LDS ----
+        f4 a3p = zero4, r3p = zero4, r3q = zero4;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            if (y3_needed) a3p = MFMA(fa2[s], y2w[s], a3p);
+            if constexpr (FV) {
+                r3p = MFMA(fa2[s], r2w[s], r3p);
+                r3q = MFMA(vfa2[s], y2w[s], r3q);
+            }
+        }
+        pb[w * 128 + lane] = a3p;
+        pb[w * 128 + 64 + lane] = r3p + r3q;
+        __syncthreads();
+        f4 x3 = b2, rx3 = vb2;
+#pragma unroll
+        for (int kt = 0; kt < TH; ++kt) {                  // fixed order
+            x3 += pb[kt * 128 + lane];
+            rx3 += pb[kt * 128 + 64 + lane];
+        }
+        f4 r3, g3;
+        const f4 y3 = act_fwd(a3, x3, rx3, r3);
+        if constexpr (FV) {
+            g3 = act_bwd(a3, y3, r3 * iv);
+        } else {
+            const f4 dm = reinterpret_cast<const f4 *>(A.pg_d4)[(long)(tc * 16 + c) * 4 + g];
+            const float adv = A.pg_adv[tc * 16 + c];
+            g3 = act_bwd(a3, y3, (adv * dm) * reinterpret_cast<const f4 *>(A.pg_iv4)[g]);
+        }
+        g3 = live ? g3 : zero4;
+        if (w == 0) sB3 += g3;
+
+        // ---- RGW2 tile (w, 0) += Y2_w . G3^T ----
+        scr_put(scr, 0, y2w, c, g);
+        scr_put(scr, 16, g3, c, g);
+        {
+            const f4 ya = scr_get(scr, 0, c, g), gg = scr_get(scr, 16, c, g);
+#pragma unroll
+            for (int s = 0; s < 4; ++s) accW2 = MFMA(ya[s], gg[s], accW2);
+        }
+        // ---- G2 row tile w = act2'(W2 G3) ----
+        f4 t = zero4;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) t = MFMA(fb2[s], g3[s], t);
+        const f4 g2w = act_bwd(a2, y2w, t);
+        sB2 += g2w;
+        gb[w * 64 + lane] = g2w;
+        __syncthreads();
+        f4 g2[T2];
+#pragma unroll
+        for (int kt = 0; kt < T2; ++kt) g2[kt] = gb[kt * 64 + lane];
+        // ---- G1 row tile w = act1'(W1 G2) ----
+        t = zero4;
+#pragma unroll
+        for (int kt = 0; kt < T2; ++kt)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) t = MFMA(fb1[kt][s], g2[kt][s], t);
+        const f4 g1w = act_bwd(a1, y1w, t);
+        sB1 += g1w;
+        // ---- RGW1 tiles (at, w) += Y1_at . G2_w^T ----
+#pragma unroll
+        for (int at = 0; at < T1; ++at) scr_put(scr, 16 * at, y1[at], c, g);
+        scr_put(scr, 16 * T1, g2w, c, g);
+        {
+            const f4 gg = scr_get(scr, 16 * T1, c, g);
+#pragma unroll
+            for (int at = 0; at < T1; ++at) {
+                const f4 ya = scr_get(scr, 16 * at, c, g);
+#pragma unroll
+                for (int s = 0; s < 4; ++s) accW1[at] = MFMA(ya[s], gg[s], accW1[at]);
+            }
+        }
+        // ---- RGW0 tiles (kt0, w) += X0_kt0 . G1_w^T ----
+#pragma unroll
+        for (int kt = 0; kt < T0; ++kt) scr_put(scr, 16 * kt, x0[kt], c, g);
+        scr_put(scr, 16 * T0, g1w, c, g);
+        {
+            const f4 gg = scr_get(scr, 16 * T0, c, g);
+#pragma unroll
+            for (int kt = 0; kt < T0; ++kt) {
+                const f4 ya = scr_get(scr, 16 * kt, c, g);
+#pragma unroll
+                for (int s = 0; s < 4; ++s) accW0[kt] = MFMA(ya[s], gg[s], accW0[kt]);
+            }
+        }
+    }
+
+    // ---- epilogue: bias sums over the sample columns, NG-way group combine, block partial ----
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        sB1[r] = rowsum16(sB1[r]);
+        sB2[r] = rowsum16(sB2[r]);
+        sB3[r] = rowsum16(sB3[r]);
+    }
+    f4 acc[Q::NW];
+    {
+        int k = 0;
+#pragma unroll
+        for (int i = 0; i < T0; ++i) acc[k++] = accW0[i];
+#pragma unroll
+        for (int i = 0; i < T1; ++i) acc[k++] = accW1[i];
+        acc[k++] = accW2;
+        acc[k++] = sB1;
+        acc[k++] = sB2;
+        acc[k++] = sB3;
+    }
+    __syncthreads();                                       // exchange buffers are free now
+    if (grp > 0) {
+#pragma unroll
+        for (int k = 0; k < Q::NW; ++k) L4[(((grp - 1) * TH + w) * Q::NW + k) * 64 + lane] = acc[k];
+    }
+    __syncthreads();
+    if (grp == 0) {
+#pragma unroll
+        for (int q = 1; q < Q::NG; ++q)
+#pragma unroll
+            for (int k = 0; k < Q::NW; ++k) acc[k] += L4[(((q - 1) * TH + w) * Q::NW + k) * 64 + lane];
+        if (A.acc_out) {
+            double *dst = A.acc_out + (long)(blockIdx.x % A.R_out) * A.P;
+#pragma unroll
+            for (int k = 0; k < Q::NW; ++k)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int m = imap_coop_at(net, T0, TH, (w * Q::NW + k) * 256 + lane * 4 + r);
+                    if (m >= 0) unsafeAtomicAdd(dst + m, (double)acc[k][r]);
+                }
+        } else {
+            f4 *slab4 = reinterpret_cast<f4 *>(A.slabs + (long)blockIdx.x * Q::SLAB);
+#pragma unroll
+            for (int k = 0; k < Q::NW; ++k) slab4[(w * Q::NW + k) * 64 + lane] = acc[k];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Generic FVP kernel: any depth, any widths (one thread per sample, fp32).
 // Per-sample activations live in a block-private global scratch laid out
 // [row][256] so that every access is coalesced across the block.
@@ -1225,7 +1514,8 @@ template <int E>
 __global__ void __launch_bounds__(1024)
 cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restrict__ p_in,
                  const double *__restrict__ r_in, double *p_out, double *r_out, double *x, int P, int nw, Ctl *ctl,
-                 const CgSt *st_in, CgSt *st_out, double *hist) {
+                 const CgSt *st_in, CgSt *st_out, double *hist,
+                 const int *__restrict__ vmap, float *__restrict__ vpack, int vlen) {
     __shared__ double sh[16];
     const int done = ctl->done;
     const double n = ctl->n_total, lam = ctl->damping, th = ctl->resth;
@@ -1265,14 +1555,21 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
     const double nr = block_sum(rr, sh);
     const double xn = block_sum(xx, sh);
     const double beta = nr / sin.rdotr;
+    extern __shared__ double sp[];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const int q = threadIdx.x + e * 1024;
         if (q < P) {
+            const double pn = rv[e] + beta * pv[e];
             x[q] = xv[e];
             r_out[q] = rv[e];
-            p_out[q] = rv[e] + beta * pv[e];
+            p_out[q] = pn;
+            if (vlen) sp[q] = pn;
         }
+    }
+    if (vlen) {                                        // fp32 fragment pack of p' for the next FVP
+        __syncthreads();
+        write_vpack(sp, vmap, vpack, vlen);
     }
     if (threadIdx.x == 0) {
         const int it = sin.iter + 1;
@@ -1343,6 +1640,31 @@ static const FastEntry kFast[] = {
     FAST_SHAPE(2, 1, 1, 1), FAST_SHAPE(2, 2, 2, 1), FAST_SHAPE(2, 4, 4, 1),
 };
 
+// cooperative kernels (T1 == T2 == TH, T3 == 1)
+template <int T0, int TH, int ACT, int MODE>
+static void coop_launch(dim3 g, int lds, hipStream_t st, const IterArgs &a, const Net &net) {
+    hipLaunchKernelGGL((fvp_coop_kernel<T0, TH, ACT, MODE>), g, dim3(CoopCfg<T0, TH>::THREADS), lds, st, a, net);
+}
+template <int T0, int TH, int ACT>
+static hipError_t coop_attr(int lds) {
+    hipError_t e = hipFuncSetAttribute((const void *)fvp_coop_kernel<T0, TH, ACT, 0>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute((const void *)fvp_coop_kernel<T0, TH, ACT, 1>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+}
+struct CoopEntry {
+    int T0, TH, act;
+    fast_launch_fn launch, launch_pg;
+    hipError_t (*attr)(int);
+    int lds, slab, ng;
+};
+#define COOP_ENTRY(t0, th, act)                                                                                   \
+    {t0, th, act, coop_launch<t0, th, act, 0>, coop_launch<t0, th, act, 1>, coop_attr<t0, th, act>,               \
+     CoopCfg<t0, th>::LDS_BYTES, CoopCfg<t0, th>::SLAB, CoopCfg<t0, th>::NG}
+#define COOP_SHAPE(t0, th) COOP_ENTRY(t0, th, ACT_TTL), COOP_ENTRY(t0, th, -1)
+static const CoopEntry kCoop[] = {COOP_SHAPE(1, 2), COOP_SHAPE(1, 4), COOP_SHAPE(2, 2), COOP_SHAPE(2, 4)};
+
 struct trpo_dev {
     int device;
     hipStream_t stream;
@@ -1350,6 +1672,10 @@ struct trpo_dev {
     int P, nw;
     // fast path
     const FastEntry *fast;
+    const CoopEntry *coop_e;    // cooperative kernel for wide hidden layers (else NULL)
+    int coop;
+    fast_launch_fn k_fvp, k_pg; // the tile kernel serving this shape, FVP and policy-gradient modes
+    int k_lds, k_tiles;         // its dynamic LDS bytes and tiles per block per step
     Pack pack;
     float *tpack, *vpack;
     int *tmap, *vmap;
@@ -1538,12 +1864,37 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
         const int len = pk.tlen > pk.vlen ? pk.tlen : pk.vlen;
         hipLaunchKernelGGL(build_maps_kernel, dim3(cdiv(len, 256)), dim3(256), 0, d->stream, n, pk, d->tmap, d->vmap);
         if (d->fast->attr(d->fast->lds) != hipSuccess) FAIL("hipFuncSetAttribute(LDS=%d) failed", d->fast->lds);
+        d->k_fvp = d->fast->launch;
+        d->k_pg = d->fast->launch_pg;
+        d->k_lds = d->fast->lds;
+        d->k_tiles = d->fast->waves;
         d->slab = d->fast->slab;
-        DMALLOC(d->imap, sizeof(int) * d->slab);
-        hipLaunchKernelGGL(build_imap_kernel, dim3(cdiv(d->slab, 256)), dim3(256), 0, d->stream, n, pk, d->imap,
-                           d->slab);
-        snprintf(d->name, sizeof d->name, "mfma-mlp3 %dx%dx%dx%d%s", T[0], T[1], T[2], T[3],
-                 d->fast->act >= 0 ? " ttl" : "");
+        // wide hidden layers: the cooperative kernel (TRPO_COOP=0 keeps the one-wave-per-tile kernel)
+        d->coop_e = NULL;
+        d->coop = 0;
+        const char *ec = getenv("TRPO_COOP");
+        if (!(ec && atoi(ec) == 0) && T[1] == T[2] && (T[1] == 2 || T[1] == 4) && T[3] == 1)
+            for (const CoopEntry &e : kCoop)
+                if (e.T0 == T[0] && e.TH == T[1] && e.act == d->fast->act) d->coop_e = &e;
+        if (d->coop_e) {
+            if (d->coop_e->attr(d->coop_e->lds) != hipSuccess)
+                FAIL("hipFuncSetAttribute(LDS=%d) failed", d->coop_e->lds);
+            d->coop = 1;
+            d->k_fvp = d->coop_e->launch;
+            d->k_pg = d->coop_e->launch_pg;
+            d->k_lds = d->coop_e->lds;
+            d->k_tiles = d->coop_e->ng;
+            d->slab = d->coop_e->slab;
+            DMALLOC(d->imap, sizeof(int) * d->slab);
+            hipLaunchKernelGGL(build_imap_coop_kernel, dim3(cdiv(d->slab, 256)), dim3(256), 0, d->stream, n, T[0],
+                               T[1], d->imap, d->slab);
+        } else {
+            DMALLOC(d->imap, sizeof(int) * d->slab);
+            hipLaunchKernelGGL(build_imap_kernel, dim3(cdiv(d->slab, 256)), dim3(256), 0, d->stream, n, pk, d->imap,
+                               d->slab);
+        }
+        snprintf(d->name, sizeof d->name, "mfma-mlp3 %dx%dx%dx%d%s%s", T[0], T[1], T[2], T[3],
+                 d->fast->act >= 0 ? " ttl" : "", d->coop ? " coop" : "");
     } else {
         DMALLOC(d->th32, sizeof(float) * d->P);
         DMALLOC(d->v32, sizeof(float) * d->P);
@@ -1642,7 +1993,7 @@ static void choose_reduction(trpo_dev *d) {
     // (G x P values per FVP); otherwise block slabs + a reduce kernel
     // decided from P only, so every rank of a sharded run picks the same collective pattern
     const char *e = getenv("TRPO_ATOMIC");
-    const bool ok = d->fast && d->fast->emax <= 4 && d->P <= 2048;
+    const bool ok = d->fast && !d->coop && d->fast->emax <= 4 && d->P <= 2048;
     d->atomic = ok && 256L * d->P <= 400000;
     if (e) d->atomic = ok && atoi(e) != 0;
 }
@@ -1656,7 +2007,7 @@ static int choose_grid(trpo_dev *d) {
     const char *e = getenv("TRPO_FVP_BLOCKS");
     if (d->fast) {
         const int ntiles = cdiv((long)d->n, 16);
-        int g = cdiv(ntiles, d->fast->waves);
+        int g = cdiv(ntiles, d->k_tiles);
         if (g > cus) g = cus;
         if (e && atoi(e) > 0) g = atoi(e);
         return g < 1 ? 1 : g;
@@ -1809,7 +2160,7 @@ static int enqueue_fvp_core(trpo_dev *d, const double *src, const int *skip) {
     if (d->fast) {
         // src has already been packed into d->vpack (by the caller or the CG kernels)
         IterArgs a = plain_args(d, skip);
-        d->fast->launch(dim3(d->grid), d->fast->lds, d->stream, a, n);
+        d->k_fvp(dim3(d->grid), d->k_lds, d->stream, a, n);
         HCHK(hipGetLastError());
     } else {
         hipLaunchKernelGGL(to_f32_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, d->v32, src, d->P);
@@ -1846,7 +2197,7 @@ extern "C" int trpo_dev_fvp_kernel(trpo_dev *d) {
     HCHK(hipSetDevice(d->device));
     if (d->fast) {
         IterArgs a = plain_args(d, &d->ctl->zero);
-        d->fast->launch(dim3(d->grid), d->fast->lds, d->stream, a, d->net);
+        d->k_fvp(dim3(d->grid), d->k_lds, d->stream, a, d->net);
     } else {
         hipLaunchKernelGGL(fvp_generic_kernel, dim3(d->grid), dim3(GEN_T), 0, d->stream, d->obs32, (int)d->n,
                            d->th32, d->v32, d->iv32, d->scratch, d->srows, d->slabs, d->net, &d->ctl->zero);
@@ -1888,7 +2239,7 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
     CG_DISPATCH(E, cg_init_kernel, dim3(1), dim3(1024), shm, d->stream, b, x, d->rbuf[0], d->pbuf[0], d->P, d->ctl,
                 d->st, d->hist, (int)maxiter, resth, d->vmap, d->vpack, vlen, d->atomic ? acc_slot(d, 0) : nullptr,
                 d->atomic ? RP : 0);
-    if (d->fast) {
+    if (d->fast && !d->coop) {
         for (long j = 0; j < M; ++j) {
             IterArgs a = plain_args(d, done);
             if (d->atomic) {
@@ -1913,7 +2264,7 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
                 a.hist = d->hist;
                 a.vmap = d->vmap;
             }
-            d->fast->launch(dim3(d->grid), d->fast->lds, d->stream, a, d->net);
+            d->k_fvp(dim3(d->grid), d->k_lds, d->stream, a, d->net);
             int rc;
             if (d->atomic) {
                 rc = allreduce(d, acc_slot(d, j), (size_t)RP);
@@ -1928,17 +2279,19 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
             const int in = (int)((M - 1) & 1), out = (int)(M & 1);
             CG_DISPATCH(E, cg_update_kernel, dim3(1), dim3(1024), 0, d->stream,
                         d->atomic ? acc_slot(d, M - 1) : d->zacc, d->atomic ? d->R : 1, d->pbuf[in], d->rbuf[in],
-                        d->pbuf[out], d->rbuf[out], x, d->P, d->nw, d->ctl, d->st + in, d->st + out, d->hist);
+                        d->pbuf[out], d->rbuf[out], x, d->P, d->nw, d->ctl, d->st + in, d->st + out, d->hist,
+                        (const int *)nullptr, (float *)nullptr, 0);
         }
     } else {
-        // generic kernel (or an empty local shard): FVP, reduce, [all-reduce], CG step per iteration
+        // generic or cooperative kernel: FVP, reduce, [all-reduce], CG step per iteration
         for (long j = 0; j < M; ++j) {
             const int cur = (int)(j & 1), nxt = (int)((j + 1) & 1);
             int rc = enqueue_fvp_core(d, d->pbuf[cur], done);
             if (rc) return rc;
-            CG_DISPATCH(E, cg_update_kernel, dim3(1), dim3(1024), 0, d->stream, d->zacc, 1, d->pbuf[cur],
-                        d->rbuf[cur], d->pbuf[nxt], d->rbuf[nxt], x, d->P, d->nw, d->ctl, d->st + cur, d->st + nxt,
-                        d->hist);
+            // cooperative kernel: the update also packs p' for the next FVP (fp32 fragment order)
+            CG_DISPATCH(E, cg_update_kernel, dim3(1), dim3(1024), d->coop ? shm : 0, d->stream, d->zacc, 1,
+                        d->pbuf[cur], d->rbuf[cur], d->pbuf[nxt], d->rbuf[nxt], x, d->P, d->nw, d->ctl, d->st + cur,
+                        d->st + nxt, d->hist, d->vmap, d->vpack, d->coop ? vlen : 0);
         }
     }
     HCHK(hipGetLastError());
@@ -2055,8 +2408,8 @@ extern "C" int trpo_dev_read_stamps(unsigned long long *out, int n) {
 extern "C" int trpo_dev_geometry(const trpo_dev *d, int *blocks, int *threads, int *lds_bytes) {
     if (!d) return -1;
     if (blocks) *blocks = d->grid;
-    if (threads) *threads = d->fast ? 64 * d->fast->waves : GEN_T;
-    if (lds_bytes) *lds_bytes = d->fast ? d->fast->lds : 0;
+    if (threads) *threads = d->fast ? 512 : GEN_T;
+    if (lds_bytes) *lds_bytes = d->fast ? d->k_lds : 0;
     return 0;
 }
 
@@ -2129,7 +2482,7 @@ int trpo_dev_pg_sums_fast(trpo_dev *d, const double *roll64, const double **zacc
     a.pg_d4 = reinterpret_cast<const float4 *>(d->pg_d);
     a.pg_adv = d->pg_adv;
     a.pg_iv4 = reinterpret_cast<const float4 *>(d->pg_iv);
-    d->fast->launch_pg(dim3(d->grid), d->fast->lds, d->stream, a, d->net);
+    d->k_pg(dim3(d->grid), d->k_lds, d->stream, a, d->net);
     HCHK(hipGetLastError());
     hipLaunchKernelGGL(reduce_slabs_kernel, dim3(cdiv(d->slab, 64)), dim3(1024), 0, d->stream, d->slabs, d->grid,
                        d->slab, d->imap, d->zacc, &d->ctl->zero);
