@@ -199,6 +199,28 @@ def bench_update(device, n=N_TOTAL, reps=20):
     return out
 
 
+def bench_baseline(device, num_ep=20, ep_len=150, reps=50):
+    """One value-baseline objective + gradient evaluation (src/TRPO_Baseline.c evaluate(), the
+    L-BFGS callback) on the reference's own batch shape (20 episodes x 150 steps, [16,16,16,1]),
+    device-resident data; the clean-room CPU port timed beside it (1 core)."""
+    import oracle
+    L = [16, 16, 16, 1]
+    x, obs, tgt = synth.make_baseline_problem(L, num_ep, ep_len)
+    with trpo_amd.Baseline(L, "lttl", device=device) as b:
+        b.set_data(obs, tgt, num_ep, ep_len)
+        b.evaluate(x)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            f, g = b.evaluate(x)
+        dev = (time.perf_counter() - t0) / reps
+    t0 = time.perf_counter()
+    fo, go, _ = oracle.baseline_evaluate(L, "lttl", x, obs, tgt, num_ep, ep_len)
+    cpu = time.perf_counter() - t0
+    return {"evaluate_us": 1e6 * dev, "cpu_port_evaluate_us_1core": 1e6 * cpu, "samples": num_ep * ep_len,
+            "grad_relL2_vs_cpu": float(np.linalg.norm(g - go) / np.linalg.norm(go)),
+            "what": "host-visible wall per L-BFGS callback incl. x upload and g/f download"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -283,6 +305,7 @@ def main():
                                         "kernel_tflops": flops_per_sample(L2) * N_TOTAL / (k3 * 1e-3) / 1e12}
         c3.close()
         extra["C5_update_armDOF_0_N50000"] = bench_update(device)
+        extra["C5_baseline_evaluate_N3000"] = bench_baseline(device)
         result["extra"] = extra
 
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:

@@ -14,6 +14,9 @@
  *   CG_FPGA        <- src/include/TRPO.h:101    (accelerator twin, same signature)
  *   TRPO_Update    <- src/include/TRPO.h:104    (impl. src/TRPO_Update.c:10-1011: policy
  *                     gradient, CG step, FVP(x) step size, backtracking line search)
+ *   TRPOBaselineParam <- src/include/TRPO.h:50-77 (field-for-field identical layout)
+ *   evaluate       <- src/TRPO_Baseline.c:29    (the value-baseline objective + gradient that
+ *                     liblbfgs calls back, lbfgs_evaluate_t of src/include/lbfgs.h:378)
  *
  * Same prototypes, same by-value TRPOparam, same ownership (caller owns Input/b
  * and Result, fp64, length NumParamsCalc()), same return convention (elapsed
@@ -60,7 +63,33 @@ double CG(TRPOparam param, double *Result, double *b, size_t MaxIter, double Res
 double FVP_FPGA(TRPOparam param, double *Result, double *Input);
 double CG_FPGA(TRPOparam param, double *Result, double *b, size_t MaxIter, double ResidualTh, size_t NumThreads);
 double TRPO_Update(TRPOparam param, double *Result, size_t NumThreads);
+
+typedef struct {
+    size_t NumLayers;
+    size_t ObservSpaceDim;   /* the baseline's input is [Obs, step / EpLen]: LayerSizeBase[0] = this + 1 */
+    size_t NumEpBatch;
+    size_t EpLen;
+    size_t NumSamples;       /* NumEpBatch * EpLen */
+    size_t NumParams;        /* weights + biases (no LogStd) */
+    int PaddedParams;        /* NumParams rounded up to 16 (the L-BFGS vector length) */
+    char *AcFunc;
+    size_t *LayerSizeBase;
+    double **WBase;          /* written from x on every call, like the reference */
+    double **BBase;
+    double **LayerBase;      /* reference scratch; untouched */
+    double **GWBase;
+    double **GBBase;
+    double **GLayerBase;
+    double *Observ;          /* [NumSamples][ObservSpaceDim] */
+    double *Target;          /* [NumSamples] */
+    double *Predict;         /* [NumSamples], written on every call */
+} TRPOBaselineParam;
 #endif
+
+/* liblbfgs callback (double precision lbfgsfloatval_t): instance = TRPOBaselineParam*.
+ * Objective 0.01 * mean((Predict - Target)^2) + 0.001 * |x[0:NumParams]|^2 and its gradient
+ * (zero beyond NumParams).  Returns -1 for an unsupported activation like the reference. */
+double evaluate(void *instance, const double *x, double *g, const int n, const double step);
 
 /* ------------------------------------------------------------------------- */
 /* Part 2: in-memory context API                                             */
@@ -148,6 +177,17 @@ int trpo_ctx_set_rollout(trpo_ctx *ctx, const double *mean, const double *action
 double trpo_ctx_update(trpo_ctx *ctx, size_t cg_max_iter, double cg_residual_th, double max_kl,
                        int max_backtracks, double accept_ratio, double *theta_out, double *b_out,
                        double *x_out, trpo_update_info *info, int verbose);
+
+/* Value-baseline context: data uploaded once per fit, then one device evaluation per L-BFGS
+ * callback.  layer_size[0] = observation dim + 1 (the time feature). */
+typedef struct trpo_baseline trpo_baseline;
+trpo_baseline *trpo_baseline_create(size_t num_layers, const size_t *layer_size, const char *acfunc, int device);
+void trpo_baseline_destroy(trpo_baseline *b);
+/* observ [num_ep * ep_len][layer_size[0] - 1], target [num_ep * ep_len] */
+int trpo_baseline_set_data(trpo_baseline *b, const double *observ, const double *target, size_t num_ep,
+                           size_t ep_len);
+/* objective at x (n >= NumParams entries, L-BFGS padding allowed); g (n) and predict (may be NULL) */
+double trpo_baseline_evaluate(trpo_baseline *b, const double *x, double *g, int n, double *predict);
 
 /* Introspection: which kernel family serves this context ("mfma-mlp3 T0xT1xT2xT3"
  * or "generic"), and the FVP launch geometry. */

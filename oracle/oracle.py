@@ -54,6 +54,9 @@ def lib():
         L.oracle_update.argtypes = [C.c_size_t, _sp, C.c_char_p, _dp, _dp, _dp, _dp, _dp, _dp, C.c_size_t,
                                     C.c_double, C.c_size_t, C.c_double, C.c_double, C.c_int, C.c_double,
                                     _dp, _dp, _dp, _dp, _dp, C.POINTER(C.c_int), C.c_int]
+        L.oracle_baseline_evaluate.restype = C.c_double
+        L.oracle_baseline_evaluate.argtypes = [C.c_size_t, _sp, C.c_char_p, _dp, C.c_int, _dp, _dp, C.c_size_t,
+                                               C.c_size_t, _dp, _dp]
         L.oracle_load_rollout.restype = C.c_int
         L.oracle_load_rollout.argtypes = [C.c_char_p, C.c_size_t, _sp, C.c_size_t, _dp, _dp, _dp, _dp, _dp]
         _lib = L
@@ -170,3 +173,13 @@ def load_rollout(path, layers, n):
     if lib().oracle_load_rollout(path.encode(), len(layers), _ls(layers), n, obs, std, mean, action, adv):
         raise IOError(path)
     return obs, std, mean, action, adv
+
+
+def baseline_evaluate(layers, acfunc, x, observ, target, num_ep, ep_len):
+    """src/TRPO_Baseline.c:29-240.  x: PaddedParams (or NumParams) values.  Returns (f, g, predict)."""
+    x = _f64(x)
+    g = np.zeros(x.size)
+    pred = np.zeros(num_ep * ep_len)
+    f = lib().oracle_baseline_evaluate(len(layers), _ls(layers), acfunc.encode(), x, x.size, _f64(observ),
+                                       _f64(target), num_ep, ep_len, g, pred)
+    return f, g, pred

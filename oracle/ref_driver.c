@@ -11,6 +11,9 @@
  *   ref_driver cg   MODEL DATA N LAYERS ACFUNC DAMPING BIN  MAXITER RESTH OUT [THREADS]
  *   ref_driver time MODEL DATA N LAYERS ACFUNC DAMPING BIN  MAXITER RESTH [THREADS]
  *   ref_driver update MODEL DATA N LAYERS ACFUNC DAMPING OUT [THREADS]
+ *   ref_driver baseline LAYERS ACFUNC NUMEP EPLEN OBSFILE TARGETFILE XFILE OUT
+ *       (the reference's evaluate(), src/TRPO_Baseline.c:29; OUT = g [PaddedParams] then
+ *        Predict [N]; the objective is printed as "f %.17g")
  *
  * LAYERS is a comma list (e.g. 15,16,16,3); ACFUNC a string (e.g. lttl).
  * Vectors are text, one %.17g value per line.  The reference's own stdout
@@ -22,6 +25,10 @@
 #include <sys/time.h>
 
 #include "TRPO.h"
+#include "lbfgs.h"
+
+lbfgsfloatval_t evaluate(void *param_in, const lbfgsfloatval_t *x, lbfgsfloatval_t *g, const int n,
+                         const lbfgsfloatval_t step);   /* defined in src/TRPO_Baseline.c, no header prototype */
 
 static size_t parse_layers(const char *s, size_t *ls) {
     size_t n = 0;
@@ -60,7 +67,62 @@ static double wall(void) {
     return tv.tv_sec + 1e-6 * tv.tv_usec;
 }
 
+static int run_baseline(int argc, char **argv) {
+    if (argc < 10) return 2;
+    size_t ls[16];
+    const size_t nl = parse_layers(argv[2], ls);
+    char acf[17] = {0};
+    strncpy(acf, argv[3], 16);
+    const size_t nep = (size_t)strtoull(argv[4], NULL, 10), eplen = (size_t)strtoull(argv[5], NULL, 10);
+    const size_t N = nep * eplen, O = ls[0] - 1;
+    const size_t np = NumParamsCalc(ls, nl) - 1;
+    const int padded = (int)((np + 15) / 16 * 16);
+    double *obs = calloc(N * O, sizeof(double)), *tgt = calloc(N, sizeof(double));
+    double *pred = calloc(N, sizeof(double)), *x = calloc(padded, sizeof(double)), *g = calloc(padded, sizeof(double));
+    if (read_vec(argv[6], obs, N * O) || read_vec(argv[7], tgt, N) || read_vec(argv[8], x, np)) return 1;
+    double *W[16], *B[16], *Lay[16], *GW[16], *GB[16], *GL[16];
+    for (size_t i = 0; i + 1 < nl; ++i) {
+        W[i] = calloc(ls[i] * ls[i + 1], sizeof(double));
+        B[i] = calloc(ls[i + 1], sizeof(double));
+        GW[i] = calloc(ls[i] * ls[i + 1], sizeof(double));
+        GB[i] = calloc(ls[i + 1], sizeof(double));
+    }
+    for (size_t i = 0; i < nl; ++i) {
+        Lay[i] = calloc(ls[i], sizeof(double));
+        GL[i] = calloc(ls[i], sizeof(double));
+    }
+    TRPOBaselineParam bp;             /* filled like src/TRPO_MuJoCo.c:256-277 */
+    memset(&bp, 0, sizeof bp);
+    bp.NumLayers = nl;
+    bp.ObservSpaceDim = O;
+    bp.NumEpBatch = nep;
+    bp.EpLen = eplen;
+    bp.NumSamples = N;
+    bp.NumParams = np;
+    bp.PaddedParams = padded;
+    bp.AcFunc = acf;
+    bp.LayerSizeBase = ls;
+    bp.WBase = W;
+    bp.BBase = B;
+    bp.LayerBase = Lay;
+    bp.GWBase = GW;
+    bp.GBBase = GB;
+    bp.GLayerBase = GL;
+    bp.Observ = obs;
+    bp.Target = tgt;
+    bp.Predict = pred;
+    double f = evaluate(&bp, x, g, padded, 1.0);
+    printf("f %.17g\n", f);
+    FILE *out = fopen(argv[9], "w");
+    if (!out) return 1;
+    for (int i = 0; i < padded; ++i) fprintf(out, "%.17g\n", g[i]);
+    for (size_t i = 0; i < N; ++i) fprintf(out, "%.17g\n", pred[i]);
+    fclose(out);
+    return 0;
+}
+
 int main(int argc, char **argv) {
+    if (argc > 1 && !strcmp(argv[1], "baseline")) return run_baseline(argc, argv);
     if (argc < 9) {
         fprintf(stderr, "usage: see header of ref_driver.c\n");
         return 2;

@@ -30,6 +30,7 @@
  *                  FVP(x), shs, lagrange   src/TRPO_Update.c:633-866
  *                  line search             src/TRPO_Update.c:868-1007
  *                  (theta starts as the CG step x: :850-852 quirk kept)
+ *   - value-baseline objective evaluate()  src/TRPO_Baseline.c:29-240
  */
 #include <math.h>
 #include <stdint.h>
@@ -571,4 +572,71 @@ int oracle_load_rollout(const char *path, size_t nl, const size_t *ls, size_t n,
 bad:
     fclose(f);
     return -1;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Value-baseline objective (src/TRPO_Baseline.c:29-240)                     */
+/* ------------------------------------------------------------------------- */
+/* x: NumParams (+ padding) parameters of the baseline MLP ls[0] = O + 1 (time feature), ...,
+ * ls[nl-1] = 1.  observ [num_ep * ep_len][O], target [N].  g[n], predict[N] outputs.
+ * Returns the objective 0.01 mean (pred - target)^2 + 0.001 |x|^2, or -1. */
+double oracle_baseline_evaluate(size_t nl, const size_t *ls, const char *ac, const double *x, int n,
+                                const double *observ, const double *target, size_t num_ep, size_t ep_len,
+                                double *g, double *predict) {
+    if (nl < 2 || nl > OR_MAX_LAYERS || ls[nl - 1] != 1) return -1;
+    for (size_t i = 1; i < nl; ++i)
+        if (ac[i] != 'l' && ac[i] != 't') return -1;
+    const size_t O = ls[0] - 1, N = num_ep * ep_len;
+    const size_t np = oracle_num_params(ls, nl) - 1;
+    const double *W[OR_MAX_LAYERS], *B[OR_MAX_LAYERS];
+    size_t Pfull;
+    or_layers(nl, ls, x, W, B, &Pfull);
+    size_t maxw = 0;
+    for (size_t i = 0; i < nl; ++i) maxw = ls[i] > maxw ? ls[i] : maxw;
+    double *buf = (double *)calloc(2 * nl * maxw, sizeof(double));
+    double *y[OR_MAX_LAYERS], *gl[OR_MAX_LAYERS];
+    for (size_t i = 0; i < nl; ++i) {
+        y[i] = buf + (2 * i) * maxw;
+        gl[i] = buf + (2 * i + 1) * maxw;
+    }
+    for (int i = 0; i < n; ++i) g[i] = 0;
+    for (size_t ep = 0; ep < num_ep; ++ep) {
+        for (size_t st = 0; st < ep_len; ++st) {
+            const size_t pos = ep * ep_len + st;
+            for (size_t i = 0; i < O; ++i) y[0][i] = observ[pos * O + i];
+            y[0][O] = (double)st / (double)ep_len;                        /* :96-100 */
+            for (size_t i = 0; i + 1 < nl; ++i) {                           /* :104-131 */
+                for (size_t j = 0; j < ls[i + 1]; ++j) {
+                    double v = B[i][j];
+                    for (size_t k = 0; k < ls[i]; ++k) v += y[i][k] * W[i][k * ls[i + 1] + j];
+                    if (ac[i + 1] == 't') v = tanh(v);
+                    y[i + 1][j] = v;
+                }
+            }
+            predict[pos] = y[nl - 1][0];                                    /* :135 */
+            gl[nl - 1][0] = 0.02 * (predict[pos] - target[pos]);            /* :140 */
+            size_t off = np;
+            for (size_t i = nl - 1; i > 0; --i) {                           /* :143-205 */
+                for (size_t j = 0; j < ls[i]; ++j)
+                    if (ac[i] == 't') gl[i][j] = gl[i][j] * (1 - y[i][j] * y[i][j]);
+                off -= ls[i - 1] * ls[i] + ls[i];
+                for (size_t j = 0; j < ls[i - 1]; ++j)
+                    for (size_t k = 0; k < ls[i]; ++k) g[off + j * ls[i] + k] += gl[i][k] * y[i - 1][j];
+                for (size_t k = 0; k < ls[i]; ++k) g[off + ls[i - 1] * ls[i] + k] += gl[i][k];
+                for (size_t j = 0; j < ls[i - 1]; ++j) {
+                    double t = 0;
+                    for (size_t k = 0; k < ls[i]; ++k) t += gl[i][k] * W[i - 1][j * ls[i] + k];
+                    gl[i - 1][j] = t;
+                }
+            }
+        }
+    }
+    for (size_t q = 0; q < np; ++q) g[q] = g[q] / (double)N + 0.002 * x[q];   /* :210-224 */
+    double mse = 0;
+    for (size_t i = 0; i < N; ++i) mse += 0.01 * (predict[i] - target[i]) * (predict[i] - target[i]);
+    mse = mse / (double)N;
+    double l2 = 0;
+    for (size_t q = 0; q < np; ++q) l2 += x[q] * x[q];
+    free(buf);
+    return mse + 0.001 * l2;
 }

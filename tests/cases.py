@@ -92,6 +92,11 @@ def update_inputs(c):
                 adv=adv, damping=c["damping"])
 
 
+def baseline_inputs(c):
+    """(x, observ, target) of a baseline case; the expected file holds g [padded] then predict [N]."""
+    return synth.make_baseline_problem(c["layers"], c["num_ep"], c["ep_len"], scale=c["scale"], pad_value=c["pad"])
+
+
 def expected(c):
     return np.loadtxt(os.path.join(GOLDEN, c["expected"]))
 

@@ -72,6 +72,13 @@ CASES = [
     # every backtrack rejected: the reference returns the CG step x itself (:850-852)
     dict(name="syn_update_reject_n5000", kind="update", src="synth", layers=ARM, acfunc="lttl", n=5000,
          logstd=[0.0, 0.0, 0.0], std=[1.0, 1.0, 1.0], adv="neg_abs"),
+    # --- value-baseline objective evaluate() (src/TRPO_Baseline.c:29-240) ---
+    dict(name="syn_baseline_n3000", kind="baseline", layers=[16, 16, 16, 1], acfunc="lttl", num_ep=20, ep_len=150,
+         scale=1.0, pad=0.0),
+    dict(name="syn_baseline_n777", kind="baseline", layers=[16, 16, 16, 1], acfunc="lttl", num_ep=7, ep_len=111,
+         scale=1.7, pad=0.25),
+    dict(name="syn_baseline_lin_n1000", kind="baseline", layers=[16, 32, 16, 1], acfunc="lltl", num_ep=10,
+         ep_len=100, scale=0.8, pad=0.0),
 ]
 
 
@@ -130,9 +137,31 @@ def run_update_case(case, tmp):
     return rec
 
 
+def run_baseline_case(case, tmp):
+    x, obs, target = synth.make_baseline_problem(case["layers"], case["num_ep"], case["ep_len"],
+                                                 scale=case["scale"], pad_value=case["pad"])
+    files = {}
+    for key, arr in (("obs", obs.ravel()), ("tgt", target), ("x", x)):
+        files[key] = os.path.join(tmp, case["name"] + "." + key)
+        synth.write_vector_file(files[key], arr)
+    out = os.path.join(HERE, case["name"] + ".txt")
+    cmd = [DRIVER, "baseline", ",".join(str(v) for v in case["layers"]), case["acfunc"], str(case["num_ep"]),
+           str(case["ep_len"]), files["obs"], files["tgt"], files["x"], out]
+    res = subprocess.run(cmd, capture_output=True, text=True, check=True)
+    rec = dict(case)
+    rec["f"] = float(re.search(r"f (\S+)", res.stdout).group(1))
+    rec["padded"] = int(x.size)
+    rec["n"] = case["num_ep"] * case["ep_len"]
+    rec["expected"] = os.path.basename(out)
+    print("%-24s f=%.15g" % (case["name"], rec["f"]), flush=True)
+    return rec
+
+
 def run_case(case, tmp):
     if case["kind"] == "update":
         return run_update_case(case, tmp)
+    if case["kind"] == "baseline":
+        return run_baseline_case(case, tmp)
     model, data, layers, acfunc, vin = build_inputs(case, tmp)
     vpath = os.path.join(tmp, case["name"] + ".in")
     synth.write_vector_file(vpath, vin)

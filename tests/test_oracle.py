@@ -13,6 +13,7 @@ FVPCG = [c for c in cases.manifest() if c["kind"] in ("fvp", "cg")]
 FAST = [c["name"] for c in FVPCG if c["n"] <= 5000]
 SLOW = [c["name"] for c in FVPCG if c["n"] > 5000]
 UPDATE = [c["name"] for c in cases.manifest() if c["kind"] == "update"]
+BASELINE = [c["name"] for c in cases.manifest() if c["kind"] == "baseline"]
 
 
 def _run(c, threads=1):
@@ -108,3 +109,15 @@ def test_oracle_policy_gradient_is_the_fixture_cg_rhs():
     b, _ = oracle.policy_grad(x["layers"], x["acfunc"], x["theta"], x["obs"], x["mean"], x["action"], x["adv"])
     b_fix = np.loadtxt(cases.GOLDEN + "/ArmTestCG.txt")[:, 0]
     assert cases.rel_l2(b, b_fix) < 1e-6
+
+
+@pytest.mark.parametrize("name", BASELINE)
+def test_oracle_baseline_evaluate_matches_reference(name):
+    """evaluate() restated (src/TRPO_Baseline.c:29-240) vs the reference's own evaluate."""
+    c = cases.case(name)
+    x, obs, tgt = cases.baseline_inputs(c)
+    f, g, pred = oracle.baseline_evaluate(c["layers"], c["acfunc"], x, obs, tgt, c["num_ep"], c["ep_len"])
+    exp = cases.expected(c)
+    assert abs(f - c["f"]) <= 1e-14 * abs(c["f"])
+    np.testing.assert_array_equal(g, exp[:c["padded"]])
+    np.testing.assert_array_equal(pred, exp[c["padded"]:])

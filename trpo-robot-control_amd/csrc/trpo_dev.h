@@ -54,6 +54,13 @@ int trpo_dev_surrogate(trpo_dev *d, const double *fullstep, int k0, int nk, doub
 int trpo_dev_update_solve(trpo_dev *d, size_t maxiter, double resth, double *b, double *x, double *z,
                           double *adv_sum);
 
+/* Value-baseline objective (src/TRPO_Baseline.c), its own small device object. */
+typedef struct trpo_bdev trpo_bdev;
+trpo_bdev *trpo_bdev_create(int device, size_t nl, const size_t *ls, const char *ac, char *err, size_t errlen);
+void trpo_bdev_destroy(trpo_bdev *b);
+int trpo_bdev_set_data(trpo_bdev *b, const double *obs, const double *target, size_t n);
+int trpo_bdev_eval(trpo_bdev *b, const double *theta, double *gsum, double *pred);
+
 const char *trpo_dev_kernel_name(const trpo_dev *d);
 int trpo_dev_geometry(const trpo_dev *d, int *blocks, int *threads, int *lds_bytes);
 size_t trpo_dev_num_params(const trpo_dev *d);

@@ -685,3 +685,160 @@ double TRPO_Update(TRPOparam param, double *Result, size_t NumThreads) {
     pthread_mutex_unlock(&g_lock);
     return t;
 }
+
+/* ------------------------------------------------------------------------- */
+/* value-baseline objective for L-BFGS (src/TRPO_Baseline.c:29-240)          */
+/* ------------------------------------------------------------------------- */
+struct trpo_baseline {
+    trpo_bdev *dev;
+    size_t nl, ls[MAX_LAYERS];
+    char ac[MAX_LAYERS + 1];
+    size_t np;                 /* weights + biases */
+    size_t n;
+    double *gsum;              /* np + 2 */
+    double *obs_h, *tgt_h;     /* last uploaded data (drop-in change detection) */
+    size_t cap;
+};
+
+trpo_baseline *trpo_baseline_create(size_t num_layers, const size_t *layer_size, const char *acfunc, int device) {
+    if (check_shape(num_layers, layer_size, acfunc)) return NULL;
+    for (size_t i = 1; i < num_layers; ++i)
+        if (acfunc[i] != 'l' && acfunc[i] != 't') {   /* evaluate() knows only these (:120-128) */
+            set_err("Activation Function for Layer [%zu] is %c. Unsupported.", i, acfunc[i]);
+            return NULL;
+        }
+    if (layer_size[num_layers - 1] != 1) {
+        set_err("the baseline predicts one value (LayerSizeBase[last] = 1)");
+        return NULL;
+    }
+    trpo_baseline *b = (trpo_baseline *)calloc(1, sizeof(trpo_baseline));
+    if (!b) return NULL;
+    b->nl = num_layers;
+    memcpy(b->ls, layer_size, num_layers * sizeof(size_t));
+    memcpy(b->ac, acfunc, num_layers);
+    b->np = NumParamsCalc(b->ls, b->nl) - 1;
+    b->gsum = (double *)calloc(b->np + 2, sizeof(double));
+    char err[256] = {0};
+    b->dev = trpo_bdev_create(device, num_layers, layer_size, acfunc, err, sizeof err);
+    if (!b->dev || !b->gsum) {
+        set_err("%s", err[0] ? err : "baseline allocation failed");
+        trpo_baseline_destroy(b);
+        return NULL;
+    }
+    return b;
+}
+
+void trpo_baseline_destroy(trpo_baseline *b) {
+    if (!b) return;
+    trpo_bdev_destroy(b->dev);
+    free(b->gsum);
+    free(b->obs_h);
+    free(b->tgt_h);
+    free(b);
+}
+
+int trpo_baseline_set_data(trpo_baseline *b, const double *observ, const double *target, size_t num_ep,
+                           size_t ep_len) {
+    if (!b || !observ || !target || !num_ep || !ep_len) return TRPO_E_INVALID;
+    const size_t n = num_ep * ep_len, O = b->ls[0] - 1, L0 = b->ls[0];
+    double *x = (double *)malloc(sizeof(double) * n * L0);
+    if (!x) return TRPO_E_NOMEM;
+    for (size_t s = 0; s < n; ++s) {          /* input = [Obs, currentStep / EpLen] (:96-100) */
+        memcpy(x + s * L0, observ + s * O, O * sizeof(double));
+        x[s * L0 + O] = (double)(s % ep_len) / (double)ep_len;
+    }
+    int rc = trpo_bdev_set_data(b->dev, x, target, n);
+    free(x);
+    if (rc) {
+        set_err("baseline data upload failed (code %d)", rc);
+        return rc < 0 ? rc : TRPO_E_DEVICE;
+    }
+    b->n = n;
+    return 0;
+}
+
+double trpo_baseline_evaluate(trpo_baseline *b, const double *x, double *g, int n, double *predict) {
+    if (!b || !x || !g || n < (int)b->np || !b->n) return TRPO_E_INVALID;
+    int rc = trpo_bdev_eval(b->dev, x, b->gsum, predict);
+    if (rc) {
+        set_err("baseline evaluation failed on the device (code %d)", rc);
+        return rc < 0 ? rc : TRPO_E_DEVICE;
+    }
+    /* gradient (:210-224): sum / N + 0.002 * parameter; zero on the L-BFGS padding */
+    const double N = (double)b->n;
+    for (size_t q = 0; q < b->np; ++q) g[q] = b->gsum[q] / N + 0.002 * x[q];
+    for (int q = (int)b->np; q < n; ++q) g[q] = 0;
+    /* objective (:227-240): 0.01 * mean squared error + 0.001 * |x|^2 over the real parameters */
+    const double mse = 0.01 * b->gsum[b->np] / N;
+    double l2 = 0;
+    for (size_t q = 0; q < b->np; ++q) l2 += x[q] * x[q];
+    return mse + 0.001 * l2;
+}
+
+/* The drop-in for src/TRPO_Baseline.c:29 (liblbfgs callback).  One cached device context per
+ * network shape; the sample data is re-uploaded only when its contents change (compared with
+ * the last upload), so the ~25 callbacks of one lbfgs() fit upload once. */
+static trpo_baseline *g_base;
+
+double evaluate(void *instance, const double *x, double *g, const int n, const double step) {
+    (void)step;
+    TRPOBaselineParam *p = (TRPOBaselineParam *)instance;
+    if (!p || !x || !g || !p->LayerSizeBase || !p->AcFunc || !p->Observ || !p->Target) return -1;
+    if (p->NumLayers < 2 || p->LayerSizeBase[0] != p->ObservSpaceDim + 1 ||
+        p->NumSamples != p->NumEpBatch * p->EpLen) {
+        fprintf(stderr, "[ERROR] inconsistent TRPOBaselineParam (LayerSizeBase[0] = ObservSpaceDim + 1, "
+                        "NumSamples = NumEpBatch * EpLen)\n");
+        return -1;
+    }
+    for (size_t i = 1; i < p->NumLayers; ++i)
+        if (p->AcFunc[i] != 'l' && p->AcFunc[i] != 't') {
+            printf("[ERROR] Activation Function for Layer [%zu] is %c. Unsupported.\n", i, p->AcFunc[i]);
+            return -1;
+        }
+    pthread_mutex_lock(&g_lock);
+    double f = -1;
+    trpo_baseline *b = g_base;
+    if (b && (b->nl != p->NumLayers || memcmp(b->ls, p->LayerSizeBase, p->NumLayers * sizeof(size_t)) ||
+              memcmp(b->ac, p->AcFunc, p->NumLayers))) {
+        trpo_baseline_destroy(b);
+        b = g_base = NULL;
+    }
+    if (!b) b = g_base = trpo_baseline_create(p->NumLayers, p->LayerSizeBase, p->AcFunc, -1);
+    if (b) {
+        const size_t N = p->NumSamples, O = p->ObservSpaceDim;
+        int rc = 0;
+        const int same = b->n == N && b->cap >= N && b->obs_h && !memcmp(b->obs_h, p->Observ, N * O * sizeof(double)) &&
+                         !memcmp(b->tgt_h, p->Target, N * sizeof(double));
+        if (!same) {
+            rc = trpo_baseline_set_data(b, p->Observ, p->Target, p->NumEpBatch, p->EpLen);
+            if (!rc && N > b->cap) {
+                free(b->obs_h);
+                free(b->tgt_h);
+                b->obs_h = (double *)malloc(sizeof(double) * N * O + 1);
+                b->tgt_h = (double *)malloc(sizeof(double) * N + 1);
+                b->cap = (b->obs_h && b->tgt_h) ? N : 0;
+            }
+            if (!rc && b->cap >= N) {
+                memcpy(b->obs_h, p->Observ, N * O * sizeof(double));
+                memcpy(b->tgt_h, p->Target, N * sizeof(double));
+            }
+        }
+        if (!rc) f = trpo_baseline_evaluate(b, x, g, n, p->Predict);
+        /* the reference leaves W/B = x in the param's arrays (:64-81) */
+        if (f >= 0 && p->WBase && p->BBase) {
+            size_t pos = 0;
+            for (size_t i = 0; i + 1 < p->NumLayers; ++i) {
+                const size_t cur = p->LayerSizeBase[i], nxt = p->LayerSizeBase[i + 1];
+                if (p->WBase[i]) memcpy(p->WBase[i], x + pos, cur * nxt * sizeof(double));
+                pos += cur * nxt;
+                if (p->BBase[i]) memcpy(p->BBase[i], x + pos, nxt * sizeof(double));
+                pos += nxt;
+            }
+        }
+        if (f < 0) fprintf(stderr, "[ERROR] %s\n", g_err);
+    } else {
+        fprintf(stderr, "[ERROR] %s\n", g_err);
+    }
+    pthread_mutex_unlock(&g_lock);
+    return f;
+}

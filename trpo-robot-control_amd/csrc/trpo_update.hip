@@ -627,3 +627,200 @@ extern "C" int trpo_dev_surrogate(trpo_dev *d, const double *fullstep, int k0, i
     HCHK(hipStreamSynchronize(v.stream));
     return 0;
 }
+
+// ===========================================================================
+// Value-baseline objective for L-BFGS (reference src/TRPO_Baseline.c:29-240):
+// per sample forward of the baseline MLP on [Obs, step / EpLen], output seed
+// 0.02 (Predict - Target), backprop, gradient sums; fp64 like the policy-gradient
+// generic kernel (N is small, ~3000, and L-BFGS wants consistent f and g).
+// ===========================================================================
+__global__ void __launch_bounds__(UT)
+baseline_kernel(Net net, const double *__restrict__ th, const double *__restrict__ obs,
+                const double *__restrict__ target, int n, double *ws, int rows, int use_lds,
+                double *__restrict__ slabs, double *__restrict__ pred) {
+    extern __shared__ double lds64[];
+    const int tid = threadIdx.x;
+    double *Y = use_lds ? lds64 : ws + (long)blockIdx.x * rows * RS;
+    int roff[MAXL + 1];
+    row_offsets(net, roff);
+    const int tot = roff[net.nl], P = net.P, last = net.nl - 1;
+    const int G0 = tot, GL = 2 * tot;          // gradient rows mirror Y's; then (y - t)^2 and a zero row
+    int goff[MAXL];
+    for (int i = 0; i + 1 < net.nl; ++i) goff[i] = G0 + roff[i + 1];
+    double *slab = slabs + (long)blockIdx.x * (P + 1);
+    const ThetaPlain T{th};
+    for (int q = tid; q <= P; q += UT) slab[q] = 0.0;
+    const int npass = (n + UT - 1) / UT;
+    for (int pass = blockIdx.x; pass < npass; pass += gridDim.x) {
+        const int s = pass * UT + tid;
+        const bool live = s < n;
+        forward64(net, T, obs, s, live, Y, roff, tid);
+        const double y = Y[roff[last] * RS + tid];
+        const double d = live ? y - target[s] : 0.0;
+        if (live) pred[s] = y;                                         // :135
+        Y[(G0 + roff[last]) * RS + tid] = 0.02 * d;                    // :140
+        Y[GL * RS + tid] = d * d;
+        Y[(GL + 1) * RS + tid] = 0.0;
+        for (int i = last; i >= 1; --i) {                              // :143-188
+            const int cur = net.L[i], a = net.act[i];
+            for (int j = 0; j < cur; ++j) {
+                const int e = (roff[i] + j) * RS + tid;
+                Y[G0 * RS + e] = act_d64(a, Y[e], Y[G0 * RS + e]);
+            }
+            if (i >= 2) {
+                const int prev = net.L[i - 1], wo = net.woff[i - 1];
+                for (int j = 0; j < prev; ++j) {
+                    double t = 0.0;
+#pragma unroll 4
+                    for (int k = 0; k < cur; ++k) t += Y[(G0 + roff[i] + k) * RS + tid] * th[wo + j * cur + k];
+                    Y[(G0 + roff[i - 1] + j) * RS + tid] = t;
+                }
+            }
+        }
+        __syncthreads();
+        contract_pass(net, Y, roff, goff, GL, slab, tid);
+        __syncthreads();
+    }
+}
+
+struct trpo_bdev {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    Net net;
+    double *theta = nullptr, *obs = nullptr, *target = nullptr, *pred = nullptr;
+    size_t n = 0, cap = 0;
+    double *ws = nullptr;
+    size_t ws_cap = 0;
+    double *slabs = nullptr;
+    size_t slab_cap = 0;
+    double *sum = nullptr;
+    int G = 1, rows = 0, use_lds = 0, lds = 0;
+};
+
+static int act_code64(char a) {
+    switch (a) {
+    case 'l': return ACT_L;
+    case 't': return ACT_T;
+    case 'o': return ACT_O;
+    case 's': return ACT_S;
+    default: return -1;
+    }
+}
+
+extern "C" void trpo_bdev_destroy(trpo_bdev *b) {
+    if (!b) return;
+    if (b->stream) hipStreamSynchronize(b->stream);
+    void *ptrs[] = {b->theta, b->obs, b->target, b->pred, b->ws, b->slabs, b->sum};
+    for (void *p : ptrs)
+        if (p) hipFree(p);
+    if (b->stream) hipStreamDestroy(b->stream);
+    delete b;
+}
+
+extern "C" trpo_bdev *trpo_bdev_create(int device, size_t nl, const size_t *ls, const char *ac, char *err,
+                                       size_t errlen) {
+    if (nl < 2 || nl > MAXL || !ls || !ac) {
+        if (err) snprintf(err, errlen, "invalid baseline network (NumLayers=%zu)", nl);
+        return nullptr;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        if (err) snprintf(err, errlen, "no HIP device available");
+        return nullptr;
+    }
+    if (device < 0) {
+        const char *e = getenv("TRPO_DEVICE");
+        device = e ? atoi(e) : 0;
+    }
+    trpo_bdev *b = new trpo_bdev();
+    b->device = device;
+    Net &n = b->net;
+    memset(&n, 0, sizeof n);
+    n.nl = (int)nl;
+    int pos = 0;
+    for (size_t i = 0; i < nl; ++i) {
+        n.L[i] = (int)ls[i];
+        if (i > 0) n.act[i] = act_code64(ac[i]);
+        if (ls[i] == 0 || (i > 0 && n.act[i] < 0)) {
+            if (err) snprintf(err, errlen, "unsupported baseline layer %zu", i);
+            delete b;
+            return nullptr;
+        }
+    }
+    for (size_t i = 0; i + 1 < nl; ++i) {
+        n.woff[i] = pos;
+        pos += n.L[i] * n.L[i + 1];
+        n.boff[i] = pos;
+        pos += n.L[i + 1];
+    }
+    n.A = n.L[nl - 1];
+    n.P = pos + n.A;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc((void **)&b->theta, sizeof(double) * n.P) != hipSuccess ||
+        hipMalloc((void **)&b->sum, sizeof(double) * (n.P + 1)) != hipSuccess) {
+        if (err) snprintf(err, errlen, "baseline device allocation failed");
+        trpo_bdev_destroy(b);
+        return nullptr;
+    }
+    hipMemsetAsync(b->theta, 0, sizeof(double) * n.P, b->stream);
+    b->rows = rows_for(n, false) * 2 + 2;
+    const size_t bytes = sizeof(double) * (size_t)b->rows * RS;
+    b->use_lds = bytes <= (size_t)LDS_CAP;
+    b->lds = b->use_lds ? (int)bytes : 0;
+    if (b->use_lds &&
+        hipFuncSetAttribute((const void *)baseline_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_CAP) !=
+            hipSuccess) {
+        if (err) snprintf(err, errlen, "baseline LDS attribute failed");
+        trpo_bdev_destroy(b);
+        return nullptr;
+    }
+    return b;
+}
+
+// obs: [n][L0] including any extra input column(s) the caller appends (the time feature)
+extern "C" int trpo_bdev_set_data(trpo_bdev *b, const double *obs, const double *target, size_t n) {
+    if (!b || (n && (!obs || !target))) return -1;
+    HCHK(hipSetDevice(b->device));
+    const int L0 = b->net.L[0];
+    if (n > b->cap) {
+        if (b->obs) hipFree(b->obs);
+        if (b->target) hipFree(b->target);
+        if (b->pred) hipFree(b->pred);
+        b->obs = b->target = b->pred = nullptr;
+        b->cap = 0;
+        HCHK(hipMalloc((void **)&b->obs, sizeof(double) * n * L0));
+        HCHK(hipMalloc((void **)&b->target, sizeof(double) * n));
+        HCHK(hipMalloc((void **)&b->pred, sizeof(double) * n));
+        b->cap = n;
+    }
+    b->n = n;
+    b->G = n ? (cdiv((long)n, UT) < 1024 ? cdiv((long)n, UT) : 1024) : 1;
+    if (ensure(&b->slabs, &b->slab_cap, (size_t)b->G * (b->net.P + 1), b->stream)) return -2;
+    if (!b->use_lds && ensure(&b->ws, &b->ws_cap, (size_t)b->rows * RS * b->G, b->stream)) return -2;
+    if (n) {
+        HCHK(hipMemcpyAsync(b->obs, obs, sizeof(double) * n * L0, hipMemcpyHostToDevice, b->stream));
+        HCHK(hipMemcpyAsync(b->target, target, sizeof(double) * n, hipMemcpyHostToDevice, b->stream));
+    }
+    HCHK(hipStreamSynchronize(b->stream));
+    return 0;
+}
+
+// theta: natural [W, B per layer] (P - A values); gsum[P + 1]: gradient sums (P - A entries),
+// then sum (y - t)^2 at P - A; pred (n, may be NULL) receives the predictions
+extern "C" int trpo_bdev_eval(trpo_bdev *b, const double *theta, double *gsum, double *pred) {
+    if (!b || !theta || !gsum || !b->n) return -1;
+    HCHK(hipSetDevice(b->device));
+    const Net &net = b->net;
+    const int P = net.P;
+    HCHK(hipMemcpyAsync(b->theta, theta, sizeof(double) * (P - net.A), hipMemcpyHostToDevice, b->stream));
+    hipLaunchKernelGGL(baseline_kernel, dim3(b->G), dim3(UT), b->lds, b->stream, net, (const double *)b->theta,
+                       (const double *)b->obs, (const double *)b->target, (int)b->n, b->ws, b->rows, b->use_lds,
+                       b->slabs, b->pred);
+    hipLaunchKernelGGL(sum_slabs64_kernel, dim3(cdiv(P + 1, 16)), dim3(256), 0, b->stream, b->slabs, b->G, P + 1,
+                       b->sum);
+    HCHK(hipGetLastError());
+    HCHK(hipMemcpyAsync(gsum, b->sum, sizeof(double) * (P + 1), hipMemcpyDeviceToHost, b->stream));
+    if (pred) HCHK(hipMemcpyAsync(pred, b->pred, sizeof(double) * b->n, hipMemcpyDeviceToHost, b->stream));
+    HCHK(hipStreamSynchronize(b->stream));
+    return 0;
+}

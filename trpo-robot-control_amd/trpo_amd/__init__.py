@@ -115,6 +115,16 @@ def lib():
     L.trpo_ctx_update.restype = C.c_double
     L.trpo_ctx_update.argtypes = [C.c_void_p, sz, C.c_double, C.c_double, C.c_int, C.c_double, _dp, _dp, _dp,
                                   P(UpdateInfo), C.c_int]
+    L.evaluate.restype = C.c_double
+    L.evaluate.argtypes = [C.c_void_p, _dp, _dp, C.c_int, C.c_double]
+    L.trpo_baseline_create.restype = C.c_void_p
+    L.trpo_baseline_create.argtypes = [sz, P(sz), C.c_char_p, C.c_int]
+    L.trpo_baseline_destroy.restype = None
+    L.trpo_baseline_destroy.argtypes = [C.c_void_p]
+    L.trpo_baseline_set_data.restype = C.c_int
+    L.trpo_baseline_set_data.argtypes = [C.c_void_p, _dp, _dp, sz, sz]
+    L.trpo_baseline_evaluate.restype = C.c_double
+    L.trpo_baseline_evaluate.argtypes = [C.c_void_p, _dp, _dp, C.c_int, C.c_void_p]
     L.trpo_last_error.restype = C.c_char_p
     L.trpo_last_error.argtypes = []
     L.trpo_cache_clear.restype = None
@@ -124,6 +134,95 @@ def lib():
 
 
 MAX_BACKTRACKS = 32
+
+
+class TRPOBaselineParam(C.Structure):
+    """src/include/TRPO.h:50-77 (field-for-field)."""
+    _fields_ = [("NumLayers", C.c_size_t), ("ObservSpaceDim", C.c_size_t), ("NumEpBatch", C.c_size_t),
+                ("EpLen", C.c_size_t), ("NumSamples", C.c_size_t), ("NumParams", C.c_size_t),
+                ("PaddedParams", C.c_int), ("AcFunc", C.c_char_p), ("LayerSizeBase", C.POINTER(C.c_size_t)),
+                ("WBase", C.POINTER(C.POINTER(C.c_double))), ("BBase", C.POINTER(C.POINTER(C.c_double))),
+                ("LayerBase", C.POINTER(C.POINTER(C.c_double))), ("GWBase", C.POINTER(C.POINTER(C.c_double))),
+                ("GBBase", C.POINTER(C.POINTER(C.c_double))), ("GLayerBase", C.POINTER(C.POINTER(C.c_double))),
+                ("Observ", C.POINTER(C.c_double)), ("Target", C.POINTER(C.c_double)),
+                ("Predict", C.POINTER(C.c_double))]
+
+
+def make_baseline_param(layers_base, acfunc: str, observ, target, num_ep: int, ep_len: int):
+    """A TRPOBaselineParam as src/TRPO_MuJoCo.c:256-277 fills it (W/B arrays allocated, scratch NULL).
+    The numpy arrays are kept alive on the returned object (._keep); .predict is the Predict array."""
+    p = TRPOBaselineParam()
+    observ = np.ascontiguousarray(observ, np.float64)
+    target = np.ascontiguousarray(target, np.float64)
+    n = num_ep * ep_len
+    predict = np.zeros(n)
+    npar = NumParamsCalc(list(layers_base)) - layers_base[-1]
+    W = [np.zeros(layers_base[i] * layers_base[i + 1]) for i in range(len(layers_base) - 1)]
+    B = [np.zeros(layers_base[i + 1]) for i in range(len(layers_base) - 1)]
+    dpp = C.POINTER(C.c_double)
+    warr = (dpp * len(W))(*[w.ctypes.data_as(dpp) for w in W])
+    barr = (dpp * len(B))(*[b.ctypes.data_as(dpp) for b in B])
+    ls = _sizes(layers_base)
+    p.NumLayers, p.ObservSpaceDim, p.NumEpBatch, p.EpLen = len(layers_base), layers_base[0] - 1, num_ep, ep_len
+    p.NumSamples, p.NumParams, p.PaddedParams = n, npar, (npar + 15) // 16 * 16
+    p.AcFunc = acfunc.encode()
+    p.LayerSizeBase = C.cast(ls, C.POINTER(C.c_size_t))
+    p.WBase, p.BBase = C.cast(warr, C.POINTER(dpp)), C.cast(barr, C.POINTER(dpp))
+    p.Observ, p.Target, p.Predict = observ.ctypes.data_as(dpp), target.ctypes.data_as(dpp), predict.ctypes.data_as(dpp)
+    p._keep = (observ, target, predict, W, B, warr, barr, ls, p.AcFunc)
+    p.predict, p.W, p.B = predict, W, B
+    return p
+
+
+def evaluate(param: TRPOBaselineParam, x, g) -> float:
+    """src/TRPO_Baseline.c:29: the liblbfgs callback (g is written in place)."""
+    return float(lib().evaluate(C.byref(param), np.ascontiguousarray(x, np.float64), g, len(g), 1.0))
+
+
+class Baseline:
+    """Device-resident value-baseline objective for L-BFGS (include/trpo_mi355x.h)."""
+
+    def __init__(self, layers_base, acfunc: str, device: int = -1):
+        self.layers = [int(v) for v in layers_base]
+        self.np = NumParamsCalc(self.layers) - self.layers[-1]
+        self._h = lib().trpo_baseline_create(len(self.layers), _sizes(self.layers), acfunc.encode(), device)
+        if not self._h:
+            raise TRPOError("trpo_baseline_create failed: " + last_error())
+        self.n = 0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().trpo_baseline_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def set_data(self, observ, target, num_ep: int, ep_len: int):
+        rc = lib().trpo_baseline_set_data(self._h, np.ascontiguousarray(observ, np.float64),
+                                          np.ascontiguousarray(target, np.float64), num_ep, ep_len)
+        if rc < 0:
+            raise TRPOError("set_data failed: " + last_error())
+        self.n = num_ep * ep_len
+
+    def evaluate(self, x, want_predict=False):
+        """Returns (f, g) or (f, g, predict)."""
+        x = np.ascontiguousarray(x, np.float64)
+        g = np.zeros(x.size)
+        pred = np.zeros(self.n) if want_predict else None
+        f = lib().trpo_baseline_evaluate(self._h, x, g, x.size, pred.ctypes.data if want_predict else None)
+        if f < 0:
+            raise TRPOError("evaluate failed: " + last_error())
+        return (f, g, pred) if want_predict else (f, g)
 
 
 class UpdateInfo(C.Structure):

@@ -24,7 +24,7 @@ _M1 = np.uint64(0xBF58476D1CE4E5B9)
 _M2 = np.uint64(0x94D049BB133111EB)
 
 # stream ids keep the different inputs independent
-STREAM_OBS, STREAM_W, STREAM_V, STREAM_B, STREAM_ACT, STREAM_ADV = 1, 2, 3, 4, 5, 6
+STREAM_OBS, STREAM_W, STREAM_V, STREAM_B, STREAM_ACT, STREAM_ADV, STREAM_RET = 1, 2, 3, 4, 5, 6, 7
 
 
 def _splitmix(seed: int, stream: int, count: int, offset: int = 0) -> np.ndarray:
@@ -126,6 +126,21 @@ def make_rollout(layers, acfunc: str, theta: np.ndarray, obs: np.ndarray, std, s
     action = mean + np.asarray(std, dtype=np.float64) * normal(seed, STREAM_ACT, n * A).reshape(n, A)
     adv = normal(seed, STREAM_ADV, n)
     return mean, action, adv
+
+
+def make_baseline_problem(layers_base, num_ep: int, ep_len: int, seed: int = SEED, scale: float = 1.0,
+                          pad_value: float = 0.0):
+    """Value-baseline fit inputs (src/TRPO_Baseline.c): x [PaddedParams] (the baseline MLP's
+    weights and biases, zero-/pad_value-padded to a multiple of 16), observations
+    [num_ep * ep_len][layers_base[0] - 1] and regression targets (returns ~ N(0, 2^2))."""
+    npar = num_params(layers_base) - layers_base[-1]
+    padded = (npar + 15) // 16 * 16
+    x = np.full(padded, pad_value)
+    x[:npar] = scale * make_theta(layers_base, seed)[:npar]
+    n = num_ep * ep_len
+    obs = make_obs(n, layers_base[0] - 1, seed)
+    target = normal(seed, STREAM_RET, n, sigma=2.0)
+    return x, obs, target
 
 
 def write_model_file(path: str, theta: np.ndarray) -> None:
