@@ -35,6 +35,7 @@ from trpo_amd import synth  # noqa: E402
 
 ARM = [15, 16, 16, 3]
 N_TOTAL = 50_000
+PEAK_FP64_TFLOPS = 78.6       # MI355X dense fp64 matrix (AMD spec sheet; the guide lists fp32/bf16 only)
 CG_ITERS = 10
 DAMPING = 0.1
 PEAK_FP32_TFLOPS = 157.3     # MI355X dense FP32 (vector = matrix), MI355X_MICROARCH.md
@@ -93,11 +94,12 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def make_ctx(L, n_total, dist, device):
+def make_ctx(L, n_total, dist, device, precision=None):
     theta = synth.make_theta(L)
     obs_all = synth.make_obs(n_total, L[0])
     lo, hi = shard(n_total, dist.rank, dist.world)
-    ctx = trpo_amd.Context(L, "lttl", theta, obs_all[lo:hi], np.ones(L[-1]), DAMPING, device=device)
+    ctx = trpo_amd.Context(L, "lttl", theta, obs_all[lo:hi], np.ones(L[-1]), DAMPING, device=device,
+                           precision=precision)
     if dist.world > 1:
         uid = dist.bcast_bytes(trpo_amd.unique_id() if dist.rank == 0 else None)
         ctx.attach_comm(dist.rank, dist.world, uid)
@@ -179,7 +181,7 @@ def bench_update(device, n=N_TOTAL, reps=20):
     wall = (time.perf_counter() - t0) / reps
     ctx.close()
     out = {"update_ms": 1e3 * wall, "accepted": r["accepted"], "cg_iters": int(r["cg_iters"]),
-           "samples": n, "what": "policy gradient + CG(10, 1e-10) + FVP(x) + line search, fp64 PG/line search"}
+           "samples": n, "what": "policy gradient (fp32 tile kernel, fp64 sums) + CG(10, 1e-10) + FVP(x) + fp64 line search"}
     if os.path.exists(oracle.REF_DRIVER_FAST):
         with tempfile.TemporaryDirectory() as tmp:
             mf, df, of = (os.path.join(tmp, f) for f in ("m.txt", "d.txt", "o.txt"))
@@ -304,6 +306,16 @@ def main():
                                         "kernel_ms": k3,
                                         "kernel_tflops": flops_per_sample(L2) * N_TOTAL / (k3 * 1e-3) / 1e12}
         c3.close()
+        # fp64 precision mode (the reference's arithmetic, fp64 MFMA): same CG(10) workloads
+        for key, L in (("C1_cg10_armDOF_0_N50000_fp64", [15, 16, 16, 3]), ("C3_cg10_2x64_N50000_fp64", L2)):
+            cf, _, _ = make_ctx(L, N_TOTAL, dist, device, precision="fp64")
+            tf = time_steps(cf, dist, 20, 3, synth.make_b(synth.num_params(L)))
+            kf = cf.time_ms(0, reps)
+            extra[key] = {"cg_wall_ms": 1e3 * tf / 20, "fvp_samples_per_s": CG_ITERS * N_TOTAL / (tf / 20),
+                          "kernel": cf.kernel_name, "kernel_ms": kf,
+                          "kernel_tflops": flops_per_sample(L) * N_TOTAL / (kf * 1e-3) / 1e12,
+                          "peak_fp64_mfma_tflops": PEAK_FP64_TFLOPS}
+            cf.close()
         extra["C5_update_armDOF_0_N50000"] = bench_update(device)
         extra["C5_baseline_evaluate_N3000"] = bench_baseline(device)
         result["extra"] = extra

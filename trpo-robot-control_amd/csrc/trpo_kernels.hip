@@ -253,24 +253,26 @@ __device__ __forceinline__ bool act_needs_y(int a) { return a == ACT_T || a == A
 //             FB_i[it][kt][lane][s] = W_i[16it+c][16kt+4g+s]   (i = 1, 2)
 //             BI_i[j] = b_i[j];  IV[j] = 1/sigma_j^2 (filled separately)
 // v pack:     VFA_i like FA_i, VB_i like BI_i
-__device__ int map_frag(const Net &n, int i, int local, int nkt, bool fwd) {
+// p64: fp64 packs (v_mfma_f64_16x16x4_f64 keeps row g + 4s where the f32 MFMA keeps 4g + s)
+__device__ int map_frag(const Net &n, int i, int local, int nkt, bool fwd, bool p64 = false) {
     const int idx4 = local >> 2, s = local & 3, lane = idx4 & 63, tk = idx4 >> 6;
     const int kt = tk % nkt, ot = tk / nkt, g = lane >> 4, c = lane & 15;
+    const int ks = p64 ? g + 4 * s : 4 * g + s;
     int in, out;
-    if (fwd) { in = 16 * kt + 4 * g + s; out = 16 * ot + c; }
-    else     { in = 16 * ot + c;         out = 16 * kt + 4 * g + s; }
+    if (fwd) { in = 16 * kt + ks; out = 16 * ot + c; }
+    else     { in = 16 * ot + c;  out = 16 * kt + ks; }
     if (in >= n.L[i] || out >= n.L[i + 1]) return -1;
     return n.woff[i] + in * n.L[i + 1] + out;
 }
 
 // v-pack slot -> natural parameter (or -1).  Pure integer math on the shape, so the fused
 // kernel evaluates it in registers instead of loading a map (T compile-time there).
-__device__ __forceinline__ int vmap_at(const Net &n, const int (&T)[4], int e) {
+__device__ __forceinline__ int vmap_at(const Net &n, const int (&T)[4], int e, bool p64 = false) {
     const int vfa1 = 256 * T[0] * T[1], vfa2 = vfa1 + 256 * T[1] * T[2], vb0 = vfa2 + 256 * T[2] * T[3];
     const int vb1 = vb0 + 16 * T[1], vb2 = vb1 + 16 * T[2], end = vb2 + 16 * T[3];
-    if (e < vfa1) return map_frag(n, 0, e, T[0], true);
-    if (e < vfa2) return map_frag(n, 1, e - vfa1, T[1], true);
-    if (e < vb0) return map_frag(n, 2, e - vfa2, T[2], true);
+    if (e < vfa1) return map_frag(n, 0, e, T[0], true, p64);
+    if (e < vfa2) return map_frag(n, 1, e - vfa1, T[1], true, p64);
+    if (e < vb0) return map_frag(n, 2, e - vfa2, T[2], true, p64);
     if (e < vb1) return e - vb0 < n.L[1] ? n.boff[0] + (e - vb0) : -1;
     if (e < vb2) return e - vb1 < n.L[2] ? n.boff[1] + (e - vb1) : -1;
     if (e < end) return e - vb2 < n.L[3] ? n.boff[2] + (e - vb2) : -1;
@@ -303,15 +305,15 @@ __device__ __forceinline__ int imap_at(const Net &n, const int (&T)[4], int j) {
     return -1;
 }
 
-__global__ void build_maps_kernel(Net n, Pack pk, int *tmap, int *vmap) {
+__global__ void build_maps_kernel(Net n, Pack pk, int *tmap, int *vmap, int p64) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e < pk.tlen) {
         int m = -1;
         for (int i = 0; i < 3; ++i) {
             if (e >= pk.fa[i] && e < pk.fa[i] + 256 * pk.T[i] * pk.T[i + 1])
-                m = map_frag(n, i, e - pk.fa[i], pk.T[i], true);
+                m = map_frag(n, i, e - pk.fa[i], pk.T[i], true, p64 != 0);
             if (i > 0 && e >= pk.fb[i] && e < pk.fb[i] + 256 * pk.T[i] * pk.T[i + 1])
-                m = map_frag(n, i, e - pk.fb[i], pk.T[i + 1], false);
+                m = map_frag(n, i, e - pk.fb[i], pk.T[i + 1], false, p64 != 0);
             if (e >= pk.bi[i] && e < pk.bi[i] + 16 * pk.T[i + 1]) {
                 const int j = e - pk.bi[i];
                 m = j < n.L[i + 1] ? n.boff[i] + j : -1;
@@ -319,14 +321,17 @@ __global__ void build_maps_kernel(Net n, Pack pk, int *tmap, int *vmap) {
         }
         tmap[e] = m;
     }
-    if (e < pk.vlen) vmap[e] = vmap_at(n, pk.T, e);
+    if (e < pk.vlen) vmap[e] = vmap_at(n, pk.T, e, p64 != 0);
 }
 
-__global__ void gather_pack_kernel(float *dst, const double *src, const int *map, int len) {
+// packs are fp32 or (f64 != 0) fp64
+__global__ void gather_pack_kernel(void *dst, const double *src, const int *map, int len, int f64) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e < len) {
         const int m = map[e];
-        dst[e] = m >= 0 ? (float)src[m] : 0.0f;
+        const double v = m >= 0 ? src[m] : 0.0;
+        if (f64) reinterpret_cast<double *>(dst)[e] = v;
+        else reinterpret_cast<float *>(dst)[e] = (float)v;
     }
 }
 
@@ -342,17 +347,25 @@ __global__ void iota_kernel(int *v, int len, int valid) {
     if (j < len) v[j] = j < valid ? j : -1;
 }
 
-__global__ void set_invvar_kernel(float *iv, const double *stdv, int A, int len) {
+__global__ void set_invvar_kernel(void *iv, const double *stdv, int A, int len, int f64) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j < len) iv[j] = j < A ? (float)(1.0 / stdv[j] / stdv[j]) : 0.0f;
+    if (j < len) {
+        const double v = j < A ? 1.0 / stdv[j] / stdv[j] : 0.0;
+        if (f64) reinterpret_cast<double *>(iv)[j] = v;
+        else reinterpret_cast<float *>(iv)[j] = (float)v;
+    }
 }
 
-// observations fp64 [n][L0] -> fp32 [npad][16*T0], zero padded
-__global__ void obs_pad_kernel(float *dst, const double *src, int n, int npad, int L0, int ld) {
+// observations fp64 [n][L0] -> [npad][16*T0], zero padded; fp32, or fp64 with the features of
+// each 16-block in the fp64 MFMA row order (slot 4g + r holds feature g + 4r)
+__global__ void obs_pad_kernel(void *dst, const double *src, int n, int npad, int L0, int ld, int f64) {
     const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= (long)npad * ld) return;
     const int s = (int)(e / ld), k = (int)(e % ld);
-    dst[e] = (s < n && k < L0) ? (float)src[(long)s * L0 + k] : 0.0f;
+    const int q = k & 15, kf = f64 ? (k - q) + (q >> 2) + 4 * (q & 3) : k;
+    const double v = (s < n && kf < L0) ? src[(long)s * L0 + kf] : 0.0;
+    if (f64) reinterpret_cast<double *>(dst)[e] = v;
+    else reinterpret_cast<float *>(dst)[e] = (float)v;
 }
 
 __global__ void to_f32_kernel(float *dst, const double *src, int len) {
@@ -1033,103 +1046,188 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
 }
 
 // ---------------------------------------------------------------------------
-// Cooperative tile kernel for wide hidden layers (T1 == T2 == TH in {2, 4}, T3 == 1, e.g. the
-// 2x64-tanh policy): the TH waves of a GROUP process one 16-sample tile together, wave w owning
-// hidden row tile w of layers 1 and 2.  Per tile a wave issues 1/TH of the MFMAs, holds only its
-// own weight fragments (in registers) and its own slice of the gradient accumulators, and the
-// block's 8 waves are NG = 8 / TH groups -- so the end-of-block combine is NG-way instead of
-// 8-way and the per-tile latency is ~1/TH of the one-wave-per-tile kernel.  Exchanges through
-// LDS (double-buffered by tile parity): y1/Ry1 after layer 0, the layer-2 partial products over
-// the row tiles, and G2.  MODE 0: FVP; MODE 1: policy gradient (as fvp_mlp3_kernel).
+// Cooperative tile kernel, fp32 or fp64 (T).  The TH waves of a GROUP process one 16-sample
+// tile together, wave w owning hidden row tile w of layers 1 and 2 (T1 == T2 == TH, T3 == 1).
+// Per tile a wave issues 1/TH of the MFMAs, holds only its own weight fragments (registers) and
+// its own slice of the gradient accumulators; the NG = WAVES / TH groups of a block are combined
+// once at the end.  Exchanges through LDS (double-buffered by tile parity, none when TH == 1):
+// y1/Ry1 after layer 0, the layer-2 partial products over the row tiles, and G2.
+// fp32 serves the wide policies (2x64: TH = 4); fp64 (v_mfma_f64_16x16x4_f64, every shape) is the
+// reference-exact precision mode.  MODE 0: FVP; MODE 1: policy gradient (as fvp_mlp3_kernel).
+// The f64 MFMA's result layout differs from f32's: lane (c, g) register r holds row g + 4r
+// (f32: 4g + r), so the fp64 packs use that neuron <-> (g, s) permutation (PT<T>::neu).
 // ---------------------------------------------------------------------------
-template <int T0, int TH>
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+template <typename T> struct PT;
+template <> struct PT<float> {
+    typedef f4 V;
+    static __device__ __forceinline__ V mfma(float a, float b, V c) {
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+    }
+    static __host__ __device__ __forceinline__ int neu(int g, int r) { return 4 * g + r; }
+    static __device__ __forceinline__ float rsum16(float v) { return rowsum16(v); }
+    static __device__ __forceinline__ float th(float x) { return tanh_fast(x); }
+    static __device__ __forceinline__ float sg(float x) { return sigmoid_fast(x); }
+};
+template <> struct PT<double> {
+    typedef d4 V;
+    static __device__ __forceinline__ V mfma(double a, double b, V c) {
+        return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+    }
+    static __host__ __device__ __forceinline__ int neu(int g, int r) { return g + 4 * r; }
+    static __device__ __forceinline__ double rsum16(double v) { return rowsum16_f64(v); }
+    static __device__ __forceinline__ double th(double x) { return tanh(x); }
+    static __device__ __forceinline__ double sg(double x) { return 1.0 / (1.0 + exp(-x)); }
+};
+
+template <typename T, typename V>
+__device__ __forceinline__ V actv_fwd(int a, V x, V rx, V &ry) {
+    V y;
+    if (a == ACT_T) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            y[r] = PT<T>::th(x[r]);
+            ry[r] = rx[r] * ((T)1 - y[r] * y[r]);
+        }
+    } else if (a == ACT_S) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            y[r] = PT<T>::sg(x[r]);
+            ry[r] = rx[r] * y[r] * ((T)1 - y[r]);
+        }
+    } else if (a == ACT_O) {
+        y = (T)0.1 * x;
+        ry = (T)0.1 * rx;
+    } else {
+        y = x;
+        ry = rx;
+    }
+    return y;
+}
+template <typename T, typename V>
+__device__ __forceinline__ V actv_bwd(int a, V y, V g) {
+    if (a == ACT_T) return g * ((T)1 - y * y);
+    if (a == ACT_S) return g * y * ((T)1 - y);
+    if (a == ACT_O) return (T)0.1 * g;
+    return g;
+}
+template <typename T>
+__device__ __forceinline__ void scr_put_t(T *scr, int row0, typename PT<T>::V t, int c, int g) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) scr[(row0 + PT<T>::neu(g, r)) * SCR_LD + c] = t[r];
+}
+template <typename T>
+__device__ __forceinline__ typename PT<T>::V scr_get_t(const T *scr, int row0, int c, int g) {
+    return *reinterpret_cast<const typename PT<T>::V *>(scr + (row0 + c) * SCR_LD + 4 * g);
+}
+// a D-layout vector of natural-order values (biases, 1/sigma^2): lane group g, register r -> neu(g, r)
+template <typename T>
+__device__ __forceinline__ typename PT<T>::V dvec(const T *base, int g) {
+    typename PT<T>::V v;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = base[PT<T>::neu(g, r)];
+    return v;
+}
+
+template <typename T, int T0, int TH>
 struct CoopCfg {
-    static constexpr int WAVES = 8, GW = TH, NG = WAVES / GW, THREADS = 64 * WAVES;
-    static constexpr int NW = T0 + TH + 4;                 // accumulator f4 per lane per wave
-    static constexpr int SLAB = TH * NW * 256;             // floats per block partial
-    // LDS, f4 units: exchange buffers [parity][group][row tile][...][lane]
-    static constexpr int XB = 0, XB_N = 2 * NG * TH * 2 * 64;
-    static constexpr int PB = XB + XB_N, PB_N = 2 * NG * TH * 2 * 64;
-    static constexpr int GB = PB + PB_N, GB_N = 2 * NG * TH * 64;
-    static constexpr int EX_F4 = GB + GB_N;
+    static constexpr bool F64 = sizeof(T) == 8;
+    static constexpr int WAVES = (F64 && TH > 1) ? 4 : 8;   // fp64 exchanges are twice the bytes
+    static constexpr int GW = TH, NG = WAVES / GW, THREADS = 64 * WAVES;
+    static constexpr int NW = T0 + TH + 4;                 // accumulator vectors per lane per wave
+    static constexpr int SLAB = TH * NW * 256;             // T per block partial
+    // LDS in V (4 x T) units: exchange buffers [parity][group][row tile][...][lane]
+    static constexpr int XB = 0, XB_N = GW > 1 ? 2 * NG * TH * 2 * 64 : 0;
+    static constexpr int PB = XB + XB_N, PB_N = GW > 1 ? 2 * NG * TH * 2 * 64 : 0;
+    static constexpr int GB = PB + PB_N, GB_N = GW > 1 ? 2 * NG * TH * 64 : 0;
+    static constexpr int EX_V = GB + GB_N;
     static constexpr int SROWS = 16 * (TH + 1 > T0 + 1 ? TH + 1 : T0 + 1);   // per-wave transpose rows
-    static constexpr int SCR = SROWS * SCR_LD;             // floats per wave
-    static constexpr int COMB_F4 = (NG - 1) * TH * NW * 64; // group-combine dump (aliases exchange)
-    static constexpr int MAIN_F4 = EX_F4 > COMB_F4 ? EX_F4 : COMB_F4;
-    static constexpr int LDS_BYTES = 16 * MAIN_F4 + 4 * WAVES * SCR;
-    static_assert(TH == 2 || TH == 4, "TH");
+    static constexpr int SCR = SROWS * SCR_LD;             // T per wave
+    static constexpr int COMB_V = (NG - 1) * TH * NW * 64; // group-combine dump (aliases exchange)
+    static constexpr int MAIN_V = EX_V > COMB_V ? EX_V : COMB_V;
+    static constexpr int LDS_BYTES = 4 * (int)sizeof(T) * MAIN_V + (int)sizeof(T) * WAVES * SCR;
+    static_assert(TH == 1 || TH == 2 || TH == 4, "TH");
+    static_assert(LDS_BYTES <= 160 * 1024, "LDS");
 };
 
 // slab position -> natural parameter (or -1) for the cooperative kernel's accumulator order
 // [wave w][k][lane][r], k over RGW0 tiles (kt0, w), RGW1 tiles (at, w), RGW2 tile (w, 0),
-// B1 tile w, B2 tile w, B3 (wave 0 only).
-__device__ __forceinline__ int imap_coop_at(const Net &n, int T0, int TH, int j) {
+// B1 tile w, B2 tile w, B3 (wave 0 only); p64: the fp64 row permutation.
+__device__ __forceinline__ int imap_coop_at(const Net &n, int T0, int TH, int j, bool p64) {
     const int NW = T0 + TH + 4;
     const int w = j / (NW * 256), rem = j % (NW * 256);
     const int k = rem >> 8, lane = (rem >> 2) & 63, r = rem & 3, c = lane & 15, g = lane >> 4;
+    const int nr = p64 ? g + 4 * r : 4 * g + r;
     int i, a, b;
-    if (k < T0) { i = 0; a = 16 * k + 4 * g + r; b = 16 * w + c; }
-    else if (k < T0 + TH) { i = 1; a = 16 * (k - T0) + 4 * g + r; b = 16 * w + c; }
-    else if (k == T0 + TH) { i = 2; a = 16 * w + 4 * g + r; b = c; }
+    if (k < T0) { i = 0; a = 16 * k + nr; b = 16 * w + c; }
+    else if (k < T0 + TH) { i = 1; a = 16 * (k - T0) + nr; b = 16 * w + c; }
+    else if (k == T0 + TH) { i = 2; a = 16 * w + nr; b = c; }
     else {
         const int bi = k - (T0 + TH + 1);                 // 0: B1, 1: B2, 2: B3
         if (c != 0 || (bi == 2 && w != 0)) return -1;
-        const int nb = bi == 2 ? 4 * g + r : 16 * w + 4 * g + r;
+        const int nb = bi == 2 ? nr : 16 * w + nr;
         return nb < n.L[bi + 1] ? n.boff[bi] + nb : -1;
     }
     return (a < n.L[i] && b < n.L[i + 1]) ? n.woff[i] + a * n.L[i + 1] + b : -1;
 }
 
-__global__ void build_imap_coop_kernel(Net n, int T0, int TH, int *imap, int len) {
+__global__ void build_imap_coop_kernel(Net n, int T0, int TH, int p64, int *imap, int len) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j < len) imap[j] = imap_coop_at(n, T0, TH, j);
+    if (j < len) imap[j] = imap_coop_at(n, T0, TH, j, p64 != 0);
 }
 
-template <int T0, int TH, int ACT, int MODE>
-__global__ void __launch_bounds__(512)
+template <typename T, int T0, int TH, int ACT, int MODE>
+__global__ void __launch_bounds__((CoopCfg<T, T0, TH>::THREADS))
 fvp_coop_kernel(IterArgs A, Net net) {
-    using Q = CoopCfg<T0, TH>;
+    using Q = CoopCfg<T, T0, TH>;
     using C = FastCfg<T0, TH, TH, 1>;                      // pack offsets (same fragment packs)
+    using V = typename PT<T>::V;
     constexpr bool FV = MODE == 0;
     constexpr int T1 = TH, T2 = TH;
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    f4 *L4 = reinterpret_cast<f4 *>(lds);
+    T *ldsT = reinterpret_cast<T *>(lds);
+    V *LV = reinterpret_cast<V *>(lds);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int c = lane & 15, g = lane >> 4, grp = wave / Q::GW, w = wave % Q::GW;
-    float *scr = lds + 4 * Q::MAIN_F4 + wave * Q::SCR;
+    T *scr = ldsT + 4 * Q::MAIN_V + wave * Q::SCR;
     const int ntiles = A.ntiles, n = A.n;
-    const f4 *obs4 = reinterpret_cast<const f4 *>(A.obs4);
-    const f4 *TP = reinterpret_cast<const f4 *>(A.tpack);
-    const f4 *VP = reinterpret_cast<const f4 *>(A.vpack);
+    const V *obs4 = reinterpret_cast<const V *>(A.obs4);
+    const V *TP = reinterpret_cast<const V *>(A.tpack);
+    const V *VP = reinterpret_cast<const V *>(A.vpack);
+    const T *TPs = reinterpret_cast<const T *>(A.tpack);
+    const T *VPs = reinterpret_cast<const T *>(A.vpack);
     if (*A.skip) return;                                   // grid-uniform
 
+    const V zero4 = {0, 0, 0, 0};
     // this wave's weight fragments (theta and direction packs), straight to registers
-    f4 fa0[T0], vfa0[T0], fa1[T1], vfa1[T1], fb1[T2];
+    V fa0[T0], vfa0[T0], fa1[T1], vfa1[T1], fb1[T2];
 #pragma unroll
     for (int kt = 0; kt < T0; ++kt) {
         fa0[kt] = TP[C::FA0 / 4 + (w * T0 + kt) * 64 + lane];
-        vfa0[kt] = FV ? VP[C::VFA0 / 4 + (w * T0 + kt) * 64 + lane] : f4{0.f, 0.f, 0.f, 0.f};
+        vfa0[kt] = FV ? VP[C::VFA0 / 4 + (w * T0 + kt) * 64 + lane] : zero4;
     }
 #pragma unroll
     for (int kt = 0; kt < T1; ++kt) {
         fa1[kt] = TP[C::FA1 / 4 + (w * T1 + kt) * 64 + lane];
-        vfa1[kt] = FV ? VP[C::VFA1 / 4 + (w * T1 + kt) * 64 + lane] : f4{0.f, 0.f, 0.f, 0.f};
+        vfa1[kt] = FV ? VP[C::VFA1 / 4 + (w * T1 + kt) * 64 + lane] : zero4;
         fb1[kt] = TP[C::FB1 / 4 + (w * T2 + kt) * 64 + lane];
     }
-    const f4 fa2 = TP[C::FA2 / 4 + w * 64 + lane];
-    const f4 vfa2 = FV ? VP[C::VFA2 / 4 + w * 64 + lane] : f4{0.f, 0.f, 0.f, 0.f};
-    const f4 fb2 = TP[C::FB2 / 4 + w * 64 + lane];
-    const f4 b0w = TP[C::BI0 / 4 + w * 4 + g], b1w = TP[C::BI1 / 4 + w * 4 + g], b2 = TP[C::BI2 / 4 + g];
-    const f4 zero4 = {0.f, 0.f, 0.f, 0.f};
-    const f4 vb0w = FV ? VP[C::VB0 / 4 + w * 4 + g] : zero4, vb1w = FV ? VP[C::VB1 / 4 + w * 4 + g] : zero4;
-    const f4 vb2 = FV ? VP[C::VB2 / 4 + g] : zero4, iv = TP[C::IV / 4 + g];
+    const V fa2 = TP[C::FA2 / 4 + w * 64 + lane];
+    const V vfa2 = FV ? VP[C::VFA2 / 4 + w * 64 + lane] : zero4;
+    const V fb2 = TP[C::FB2 / 4 + w * 64 + lane];
+    const V b0w = dvec<T>(TPs + C::BI0 + 16 * w, g), b1w = dvec<T>(TPs + C::BI1 + 16 * w, g);
+    const V b2 = dvec<T>(TPs + C::BI2, g), iv = dvec<T>(TPs + C::IV, g);
+    const V vb0w = FV ? dvec<T>(VPs + C::VB0 + 16 * w, g) : zero4;
+    const V vb1w = FV ? dvec<T>(VPs + C::VB1 + 16 * w, g) : zero4;
+    const V vb2 = FV ? dvec<T>(VPs + C::VB2, g) : zero4;
 
     const int a1 = ACT >= 0 ? (ACT & 3) : net.act[1];
     const int a2 = ACT >= 0 ? ((ACT >> 2) & 3) : net.act[2];
     const int a3 = ACT >= 0 ? ((ACT >> 4) & 3) : net.act[3];
     const bool y3_needed = act_needs_y(a3);
 
-    f4 accW0[T0], accW1[T1], accW2 = zero4, sB1 = zero4, sB2 = zero4, sB3 = zero4;
+    V accW0[T0], accW1[T1], accW2 = zero4, sB1 = zero4, sB2 = zero4, sB3 = zero4;
 #pragma unroll
     for (int k = 0; k < T0; ++k) accW0[k] = zero4;
 #pragma unroll
@@ -1143,133 +1241,147 @@ fvp_coop_kernel(IterArgs A, Net net) {
         const int tc = min(tile, ntiles - 1);
         const bool live = tile < ntiles && tc * 16 + c < n;
         const int par = step & 1;
-        f4 *xb = L4 + Q::XB + ((par * Q::NG + grp) * TH) * 128;     // [row tile][2][64]
-        f4 *pb = L4 + Q::PB + ((par * Q::NG + grp) * TH) * 128;
-        f4 *gb = L4 + Q::GB + ((par * Q::NG + grp) * TH) * 64;
-        f4 x0[T0];
+        V *xb = LV + Q::XB + ((par * Q::NG + grp) * TH) * 128;     // [row tile][2][64]
+        V *pb = LV + Q::PB + ((par * Q::NG + grp) * TH) * 128;
+        V *gb = LV + Q::GB + ((par * Q::NG + grp) * TH) * 64;
+        V x0[T0];
 #pragma unroll
         for (int kt = 0; kt < T0; ++kt) x0[kt] = obs4[(long)(tc * 16 + c) * (4 * T0) + kt * 4 + g];
 
         // ---- layer 0, row tile w ----
-        f4 a = b0w, ra = vb0w;
+        V a = b0w, ra = vb0w;
 #pragma unroll
         for (int kt = 0; kt < T0; ++kt)
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
-                a = MFMA(fa0[kt][s], x0[kt][s], a);
-                if constexpr (FV) ra = MFMA(vfa0[kt][s], x0[kt][s], ra);
+                a = PT<T>::mfma(fa0[kt][s], x0[kt][s], a);
+                if constexpr (FV) ra = PT<T>::mfma(vfa0[kt][s], x0[kt][s], ra);
             }
-        f4 r1w;
-        const f4 y1w = act_fwd(a1, a, ra, r1w);
-        xb[w * 128 + lane] = y1w;
-        if constexpr (FV) xb[w * 128 + 64 + lane] = r1w;
-        __syncthreads();
-        f4 y1[T1], r1[T1];
+        V r1w;
+        const V y1w = actv_fwd<T>(a1, a, ra, r1w);
+        V y1[T1], r1[T1];
+        if constexpr (Q::GW > 1) {
+            xb[w * 128 + lane] = y1w;
+            if constexpr (FV) xb[w * 128 + 64 + lane] = r1w;
+            __syncthreads();
 #pragma unroll
-        for (int kt = 0; kt < T1; ++kt) {
-            y1[kt] = xb[kt * 128 + lane];
-            r1[kt] = FV ? xb[kt * 128 + 64 + lane] : zero4;
+            for (int kt = 0; kt < T1; ++kt) {
+                y1[kt] = xb[kt * 128 + lane];
+                r1[kt] = FV ? xb[kt * 128 + 64 + lane] : zero4;
+            }
+        } else {
+            y1[0] = y1w;
+            r1[0] = r1w;
         }
 
         // ---- layer 1, row tile w ----
         a = b1w;
         ra = vb1w;
-        f4 rb = zero4;
+        V rb = zero4;
 #pragma unroll
         for (int kt = 0; kt < T1; ++kt)
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
-                a = MFMA(fa1[kt][s], y1[kt][s], a);
+                a = PT<T>::mfma(fa1[kt][s], y1[kt][s], a);
                 if constexpr (FV) {
-                    ra = MFMA(fa1[kt][s], r1[kt][s], ra);
-                    rb = MFMA(vfa1[kt][s], y1[kt][s], rb);
+                    ra = PT<T>::mfma(fa1[kt][s], r1[kt][s], ra);
+                    rb = PT<T>::mfma(vfa1[kt][s], y1[kt][s], rb);
                 }
             }
-        f4 r2w;
-        const f4 y2w = act_fwd(a2, a, ra + rb, r2w);
+        V r2w;
+        const V y2w = actv_fwd<T>(a2, a, ra + rb, r2w);
 
-        // ---- layer 2: this wave's share (input row tile w), summed over the group in LDS ----
-        f4 a3p = zero4, r3p = zero4, r3q = zero4;
+        // ---- layer 2: this wave's share (input row tile w), summed over the group ----
+        V a3p = zero4, r3p = zero4, r3q = zero4;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-            if (y3_needed) a3p = MFMA(fa2[s], y2w[s], a3p);
+            if (y3_needed) a3p = PT<T>::mfma(fa2[s], y2w[s], a3p);
             if constexpr (FV) {
-                r3p = MFMA(fa2[s], r2w[s], r3p);
-                r3q = MFMA(vfa2[s], y2w[s], r3q);
+                r3p = PT<T>::mfma(fa2[s], r2w[s], r3p);
+                r3q = PT<T>::mfma(vfa2[s], y2w[s], r3q);
             }
         }
-        pb[w * 128 + lane] = a3p;
-        pb[w * 128 + 64 + lane] = r3p + r3q;
-        __syncthreads();
-        f4 x3 = b2, rx3 = vb2;
+        V x3 = b2, rx3 = vb2;
+        if constexpr (Q::GW > 1) {
+            pb[w * 128 + lane] = a3p;
+            pb[w * 128 + 64 + lane] = r3p + r3q;
+            __syncthreads();
 #pragma unroll
-        for (int kt = 0; kt < TH; ++kt) {                  // fixed order
-            x3 += pb[kt * 128 + lane];
-            rx3 += pb[kt * 128 + 64 + lane];
-        }
-        f4 r3, g3;
-        const f4 y3 = act_fwd(a3, x3, rx3, r3);
-        if constexpr (FV) {
-            g3 = act_bwd(a3, y3, r3 * iv);
+            for (int kt = 0; kt < TH; ++kt) {              // fixed order
+                x3 += pb[kt * 128 + lane];
+                rx3 += pb[kt * 128 + 64 + lane];
+            }
         } else {
-            const f4 dm = reinterpret_cast<const f4 *>(A.pg_d4)[(long)(tc * 16 + c) * 4 + g];
-            const float adv = A.pg_adv[tc * 16 + c];
-            g3 = act_bwd(a3, y3, (adv * dm) * reinterpret_cast<const f4 *>(A.pg_iv4)[g]);
+            x3 += a3p;
+            rx3 += r3p + r3q;
+        }
+        V r3, g3;
+        const V y3 = actv_fwd<T>(a3, x3, rx3, r3);
+        if constexpr (FV) {
+            g3 = actv_bwd<T>(a3, y3, r3 * iv);
+        } else {
+            const V dm = dvec<T>(reinterpret_cast<const T *>(A.pg_d4) + (long)(tc * 16 + c) * 16, g);
+            const T adv = reinterpret_cast<const T *>(A.pg_adv)[tc * 16 + c];
+            g3 = actv_bwd<T>(a3, y3, (adv * dm) * dvec<T>(reinterpret_cast<const T *>(A.pg_iv4), g));
         }
         g3 = live ? g3 : zero4;
         if (w == 0) sB3 += g3;
 
         // ---- RGW2 tile (w, 0) += Y2_w . G3^T ----
-        scr_put(scr, 0, y2w, c, g);
-        scr_put(scr, 16, g3, c, g);
+        scr_put_t<T>(scr, 0, y2w, c, g);
+        scr_put_t<T>(scr, 16, g3, c, g);
         {
-            const f4 ya = scr_get(scr, 0, c, g), gg = scr_get(scr, 16, c, g);
+            const V ya = scr_get_t<T>(scr, 0, c, g), gg = scr_get_t<T>(scr, 16, c, g);
 #pragma unroll
-            for (int s = 0; s < 4; ++s) accW2 = MFMA(ya[s], gg[s], accW2);
+            for (int s = 0; s < 4; ++s) accW2 = PT<T>::mfma(ya[s], gg[s], accW2);
         }
         // ---- G2 row tile w = act2'(W2 G3) ----
-        f4 t = zero4;
+        V t = zero4;
 #pragma unroll
-        for (int s = 0; s < 4; ++s) t = MFMA(fb2[s], g3[s], t);
-        const f4 g2w = act_bwd(a2, y2w, t);
+        for (int s = 0; s < 4; ++s) t = PT<T>::mfma(fb2[s], g3[s], t);
+        const V g2w = actv_bwd<T>(a2, y2w, t);
         sB2 += g2w;
-        gb[w * 64 + lane] = g2w;
-        __syncthreads();
-        f4 g2[T2];
+        V g2[T2];
+        if constexpr (Q::GW > 1) {
+            gb[w * 64 + lane] = g2w;
+            __syncthreads();
 #pragma unroll
-        for (int kt = 0; kt < T2; ++kt) g2[kt] = gb[kt * 64 + lane];
+            for (int kt = 0; kt < T2; ++kt) g2[kt] = gb[kt * 64 + lane];
+        } else {
+            g2[0] = g2w;
+        }
         // ---- G1 row tile w = act1'(W1 G2) ----
         t = zero4;
 #pragma unroll
         for (int kt = 0; kt < T2; ++kt)
 #pragma unroll
-            for (int s = 0; s < 4; ++s) t = MFMA(fb1[kt][s], g2[kt][s], t);
-        const f4 g1w = act_bwd(a1, y1w, t);
+            for (int s = 0; s < 4; ++s) t = PT<T>::mfma(fb1[kt][s], g2[kt][s], t);
+        const V g1w = actv_bwd<T>(a1, y1w, t);
         sB1 += g1w;
         // ---- RGW1 tiles (at, w) += Y1_at . G2_w^T ----
 #pragma unroll
-        for (int at = 0; at < T1; ++at) scr_put(scr, 16 * at, y1[at], c, g);
-        scr_put(scr, 16 * T1, g2w, c, g);
+        for (int at = 0; at < T1; ++at) scr_put_t<T>(scr, 16 * at, y1[at], c, g);
+        scr_put_t<T>(scr, 16 * T1, g2w, c, g);
         {
-            const f4 gg = scr_get(scr, 16 * T1, c, g);
+            const V gg = scr_get_t<T>(scr, 16 * T1, c, g);
 #pragma unroll
             for (int at = 0; at < T1; ++at) {
-                const f4 ya = scr_get(scr, 16 * at, c, g);
+                const V ya = scr_get_t<T>(scr, 16 * at, c, g);
 #pragma unroll
-                for (int s = 0; s < 4; ++s) accW1[at] = MFMA(ya[s], gg[s], accW1[at]);
+                for (int s = 0; s < 4; ++s) accW1[at] = PT<T>::mfma(ya[s], gg[s], accW1[at]);
             }
         }
         // ---- RGW0 tiles (kt0, w) += X0_kt0 . G1_w^T ----
 #pragma unroll
-        for (int kt = 0; kt < T0; ++kt) scr_put(scr, 16 * kt, x0[kt], c, g);
-        scr_put(scr, 16 * T0, g1w, c, g);
+        for (int kt = 0; kt < T0; ++kt) scr_put_t<T>(scr, 16 * kt, x0[kt], c, g);
+        scr_put_t<T>(scr, 16 * T0, g1w, c, g);
         {
-            const f4 gg = scr_get(scr, 16 * T0, c, g);
+            const V gg = scr_get_t<T>(scr, 16 * T0, c, g);
 #pragma unroll
             for (int kt = 0; kt < T0; ++kt) {
-                const f4 ya = scr_get(scr, 16 * kt, c, g);
+                const V ya = scr_get_t<T>(scr, 16 * kt, c, g);
 #pragma unroll
-                for (int s = 0; s < 4; ++s) accW0[kt] = MFMA(ya[s], gg[s], accW0[kt]);
+                for (int s = 0; s < 4; ++s) accW0[kt] = PT<T>::mfma(ya[s], gg[s], accW0[kt]);
             }
         }
     }
@@ -1277,11 +1389,11 @@ fvp_coop_kernel(IterArgs A, Net net) {
     // ---- epilogue: bias sums over the sample columns, NG-way group combine, block partial ----
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        sB1[r] = rowsum16(sB1[r]);
-        sB2[r] = rowsum16(sB2[r]);
-        sB3[r] = rowsum16(sB3[r]);
+        sB1[r] = PT<T>::rsum16(sB1[r]);
+        sB2[r] = PT<T>::rsum16(sB2[r]);
+        sB3[r] = PT<T>::rsum16(sB3[r]);
     }
-    f4 acc[Q::NW];
+    V acc[Q::NW];
     {
         int k = 0;
 #pragma unroll
@@ -1293,28 +1405,30 @@ fvp_coop_kernel(IterArgs A, Net net) {
         acc[k++] = sB2;
         acc[k++] = sB3;
     }
-    __syncthreads();                                       // exchange buffers are free now
-    if (grp > 0) {
+    if constexpr (Q::NG > 1) {
+        __syncthreads();                                   // exchange buffers are free now
+        if (grp > 0) {
 #pragma unroll
-        for (int k = 0; k < Q::NW; ++k) L4[(((grp - 1) * TH + w) * Q::NW + k) * 64 + lane] = acc[k];
+            for (int k = 0; k < Q::NW; ++k) LV[(((grp - 1) * TH + w) * Q::NW + k) * 64 + lane] = acc[k];
+        }
+        __syncthreads();
     }
-    __syncthreads();
     if (grp == 0) {
 #pragma unroll
         for (int q = 1; q < Q::NG; ++q)
 #pragma unroll
-            for (int k = 0; k < Q::NW; ++k) acc[k] += L4[(((q - 1) * TH + w) * Q::NW + k) * 64 + lane];
+            for (int k = 0; k < Q::NW; ++k) acc[k] += LV[(((q - 1) * TH + w) * Q::NW + k) * 64 + lane];
         if (A.acc_out) {
             double *dst = A.acc_out + (long)(blockIdx.x % A.R_out) * A.P;
 #pragma unroll
             for (int k = 0; k < Q::NW; ++k)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int m = imap_coop_at(net, T0, TH, (w * Q::NW + k) * 256 + lane * 4 + r);
+                    const int m = imap_coop_at(net, T0, TH, (w * Q::NW + k) * 256 + lane * 4 + r, Q::F64);
                     if (m >= 0) unsafeAtomicAdd(dst + m, (double)acc[k][r]);
                 }
         } else {
-            f4 *slab4 = reinterpret_cast<f4 *>(A.slabs + (long)blockIdx.x * Q::SLAB);
+            V *slab4 = reinterpret_cast<V *>(reinterpret_cast<T *>(A.slabs) + (long)blockIdx.x * Q::SLAB);
 #pragma unroll
             for (int k = 0; k < Q::NW; ++k) slab4[(w * Q::NW + k) * 64 + lane] = acc[k];
         }
@@ -1412,8 +1526,9 @@ fvp_generic_kernel(const float *__restrict__ obs, int n, const float *__restrict
 // ---------------------------------------------------------------------------
 // zacc[imap[j]] = sum over blocks of slabs[b][j], fp64, fixed order; j runs over the slab
 // layout (contiguous, coalesced).  block = 64 slab positions x 16 block groups.
+template <typename ST>
 __global__ void __launch_bounds__(1024)
-reduce_slabs_kernel(const float *__restrict__ slabs, int G, int slab, const int *__restrict__ imap,
+reduce_slabs_kernel(const ST *__restrict__ slabs, int G, int slab, const int *__restrict__ imap,
                     double *__restrict__ zacc, const int *__restrict__ skip) {
     __shared__ double part[16][64];
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
@@ -1423,11 +1538,11 @@ reduce_slabs_kernel(const float *__restrict__ slabs, int G, int slab, const int 
     double s = 0.0;
     if (j < slab) {
         for (int b0 = 0; b0 < G; b0 += 256) {      // 16 independent loads in flight per chunk
-            float v[16];
+            ST v[16];
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
                 const int b = b0 + ty + 16 * k;
-                v[k] = b < G ? slabs[(long)b * slab + j] : 0.0f;
+                v[k] = b < G ? slabs[(long)b * slab + j] : (ST)0;
             }
 #pragma unroll
             for (int k = 0; k < 16; ++k) s += (double)v[k];
@@ -1457,10 +1572,12 @@ __global__ void fvp_epilogue_kernel(const double *__restrict__ zacc, const doubl
 // ---------------------------------------------------------------------------
 
 // p -> fragment-order fp32 pack for the next FVP (fast path only; vlen == 0 otherwise)
-__device__ void write_vpack(const double *sp, const int *__restrict__ vmap, float *__restrict__ vpack, int vlen) {
+__device__ void write_vpack(const double *sp, const int *__restrict__ vmap, void *vpack, int vlen, int f64) {
     for (int e = threadIdx.x; e < vlen; e += blockDim.x) {
         const int m = vmap[e];
-        vpack[e] = m >= 0 ? (float)sp[m] : 0.0f;
+        const double v = m >= 0 ? sp[m] : 0.0;
+        if (f64) reinterpret_cast<double *>(vpack)[e] = v;
+        else reinterpret_cast<float *>(vpack)[e] = (float)v;
     }
 }
 
@@ -1468,8 +1585,8 @@ __device__ void write_vpack(const double *sp, const int *__restrict__ vmap, floa
 template <int E>
 __global__ void __launch_bounds__(1024)
 cg_init_kernel(const double *__restrict__ b, double *x, double *r, double *p, int P, Ctl *ctl, CgSt *st,
-               double *hist, int maxiter, double resth, const int *__restrict__ vmap, float *__restrict__ vpack,
-               int vlen, double *acc_zero, int zero_len) {
+               double *hist, int maxiter, double resth, const int *__restrict__ vmap, void *vpack,
+               int vlen, int f64, double *acc_zero, int zero_len) {
     __shared__ double sh[16];
     extern __shared__ double sp[];
     double bv[E];
@@ -1504,7 +1621,7 @@ cg_init_kernel(const double *__restrict__ b, double *x, double *r, double *p, in
         hist[1] = 0.0;
         ctl->done = (rr < resth || maxiter == 0) ? 1 : 0;
     }
-    write_vpack(sp, vmap, vpack, vlen);    // block_sum's barriers ordered the sp writes
+    write_vpack(sp, vmap, vpack, vlen, f64);    // block_sum's barriers ordered the sp writes
 }
 
 // One CG step after z = F p is available as R_in fp64 partial-sum replicas (src/TRPO_CG.c:65-103):
@@ -1515,7 +1632,7 @@ __global__ void __launch_bounds__(1024)
 cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restrict__ p_in,
                  const double *__restrict__ r_in, double *p_out, double *r_out, double *x, int P, int nw, Ctl *ctl,
                  const CgSt *st_in, CgSt *st_out, double *hist,
-                 const int *__restrict__ vmap, float *__restrict__ vpack, int vlen) {
+                 const int *__restrict__ vmap, void *vpack, int vlen, int f64) {
     __shared__ double sh[16];
     const int done = ctl->done;
     const double n = ctl->n_total, lam = ctl->damping, th = ctl->resth;
@@ -1569,7 +1686,7 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
     }
     if (vlen) {                                        // fp32 fragment pack of p' for the next FVP
         __syncthreads();
-        write_vpack(sp, vmap, vpack, vlen);
+        write_vpack(sp, vmap, vpack, vlen, f64);
     }
     if (threadIdx.x == 0) {
         const int it = sin.iter + 1;
@@ -1640,30 +1757,35 @@ static const FastEntry kFast[] = {
     FAST_SHAPE(2, 1, 1, 1), FAST_SHAPE(2, 2, 2, 1), FAST_SHAPE(2, 4, 4, 1),
 };
 
-// cooperative kernels (T1 == T2 == TH, T3 == 1)
-template <int T0, int TH, int ACT, int MODE>
+// cooperative kernels (T1 == T2 == TH, T3 == 1); element type T: fp32 or the fp64 precision mode
+template <typename T, int T0, int TH, int ACT, int MODE>
 static void coop_launch(dim3 g, int lds, hipStream_t st, const IterArgs &a, const Net &net) {
-    hipLaunchKernelGGL((fvp_coop_kernel<T0, TH, ACT, MODE>), g, dim3(CoopCfg<T0, TH>::THREADS), lds, st, a, net);
+    hipLaunchKernelGGL((fvp_coop_kernel<T, T0, TH, ACT, MODE>), g, dim3(CoopCfg<T, T0, TH>::THREADS), lds, st, a,
+                       net);
 }
-template <int T0, int TH, int ACT>
+template <typename T, int T0, int TH, int ACT>
 static hipError_t coop_attr(int lds) {
-    hipError_t e = hipFuncSetAttribute((const void *)fvp_coop_kernel<T0, TH, ACT, 0>,
+    hipError_t e = hipFuncSetAttribute((const void *)fvp_coop_kernel<T, T0, TH, ACT, 0>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
-    return hipFuncSetAttribute((const void *)fvp_coop_kernel<T0, TH, ACT, 1>,
+    return hipFuncSetAttribute((const void *)fvp_coop_kernel<T, T0, TH, ACT, 1>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 }
 struct CoopEntry {
-    int T0, TH, act;
+    int f64, T0, TH, act;
     fast_launch_fn launch, launch_pg;
     hipError_t (*attr)(int);
-    int lds, slab, ng;
+    int lds, slab, ng, threads;
 };
-#define COOP_ENTRY(t0, th, act)                                                                                   \
-    {t0, th, act, coop_launch<t0, th, act, 0>, coop_launch<t0, th, act, 1>, coop_attr<t0, th, act>,               \
-     CoopCfg<t0, th>::LDS_BYTES, CoopCfg<t0, th>::SLAB, CoopCfg<t0, th>::NG}
-#define COOP_SHAPE(t0, th) COOP_ENTRY(t0, th, ACT_TTL), COOP_ENTRY(t0, th, -1)
-static const CoopEntry kCoop[] = {COOP_SHAPE(1, 2), COOP_SHAPE(1, 4), COOP_SHAPE(2, 2), COOP_SHAPE(2, 4)};
+#define COOP_ENTRY(T, t0, th, act)                                                                                \
+    {sizeof(T) == 8, t0, th, act, coop_launch<T, t0, th, act, 0>, coop_launch<T, t0, th, act, 1>,                \
+     coop_attr<T, t0, th, act>, CoopCfg<T, t0, th>::LDS_BYTES, CoopCfg<T, t0, th>::SLAB, CoopCfg<T, t0, th>::NG,  \
+     CoopCfg<T, t0, th>::THREADS}
+#define COOP_SHAPE(T, t0, th) COOP_ENTRY(T, t0, th, ACT_TTL), COOP_ENTRY(T, t0, th, -1)
+static const CoopEntry kCoop[] = {
+    COOP_SHAPE(float, 1, 2),  COOP_SHAPE(float, 1, 4),  COOP_SHAPE(float, 2, 2),  COOP_SHAPE(float, 2, 4),
+    COOP_SHAPE(double, 1, 1), COOP_SHAPE(double, 1, 2), COOP_SHAPE(double, 1, 4), COOP_SHAPE(double, 2, 1),
+    COOP_SHAPE(double, 2, 2), COOP_SHAPE(double, 2, 4)};
 
 struct trpo_dev {
     int device;
@@ -1677,11 +1799,13 @@ struct trpo_dev {
     fast_launch_fn k_fvp, k_pg; // the tile kernel serving this shape, FVP and policy-gradient modes
     int k_lds, k_tiles;         // its dynamic LDS bytes and tiles per block per step
     Pack pack;
-    float *tpack, *vpack;
+    int f64;                    // fp64 precision mode: fp64 packs/observations/slabs, fp64 MFMA kernel
+    size_t esz;                 // pack / observation / slab element bytes (4 or 8)
+    void *tpack, *vpack;
     int *tmap, *vmap;
     int *imap;                  // slab position -> natural parameter (reduce kernel)
     int slab;                   // floats per block partial
-    f4 *obs4;
+    void *obs4;
     // generic path
     float *th32, *v32, *iv32, *obs32, *scratch;
     int srows;
@@ -1689,7 +1813,7 @@ struct trpo_dev {
     // common
     double *theta64;            // natural theta (device, fp64)
     double *obs64;              // local observations [n][L0], fp64 (TRPO_Update path)
-    float *pg_d, *pg_adv, *pg_iv;   // policy-gradient mode inputs (fp32, padded like obs4)
+    void *pg_d, *pg_adv, *pg_iv;    // policy-gradient mode inputs (element esz, padded like obs4)
     size_t pg_cap;
     void *upd;                  // TRPO_Update path state (trpo_update.hip)
     double *std64;
@@ -1699,7 +1823,7 @@ struct trpo_dev {
     CgSt *st;                   // 2 ping-ponged CG scalar states
     double *accbuf;             // atomic mode: 3 x R fp64 replicas of the P-vector
     int atomic, R;
-    float *slabs;
+    void *slabs;
     int slab_blocks;            // capacity
     int grid;                   // FVP blocks for the current n
     Ctl *ctl;
@@ -1807,6 +1931,16 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
     }
     const char *force = getenv("TRPO_FORCE_GENERIC");
     if (force && atoi(force)) d->fast = NULL;
+    {
+        // precision mode: "fp64" runs the FVP in fp64 (v_mfma_f64_16x16x4_f64) -- the reference's
+        // own precision -- through the cooperative kernel, which covers every tile-kernel shape
+        const char *ep = getenv("TRPO_PRECISION");
+        d->f64 = ep && (strcmp(ep, "fp64") == 0 || strcmp(ep, "64") == 0 || strcmp(ep, "double") == 0);
+        if (ep && !d->f64 && strcmp(ep, "fp32") != 0 && strcmp(ep, "32") != 0 && strcmp(ep, "float") != 0)
+            FAIL("TRPO_PRECISION=%s: expected fp32 or fp64", ep);
+        if (d->f64 && !d->fast) FAIL("TRPO_PRECISION=fp64 needs a 3-layer network with widths <= 64");
+        d->esz = d->f64 ? sizeof(double) : sizeof(float);
+    }
 
     if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) FAIL("stream create failed");
     if (hipEventCreate(&d->ev0) != hipSuccess || hipEventCreate(&d->ev1) != hipSuccess) FAIL("event create");
@@ -1857,12 +1991,13 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
         pk.vb[2] = pk.vb[1] + 16 * T[2];
         pk.vlen = pk.vb[2] + 16 * T[3];
         if (pk.tlen != d->fast->tlen || pk.vlen != d->fast->vlen) FAIL("internal: pack layout mismatch");
-        DMALLOC(d->tpack, sizeof(float) * pk.tlen);
-        DMALLOC(d->vpack, sizeof(float) * pk.vlen);
+        DMALLOC(d->tpack, d->esz * pk.tlen);
+        DMALLOC(d->vpack, d->esz * pk.vlen);
         DMALLOC(d->tmap, sizeof(int) * pk.tlen);
         DMALLOC(d->vmap, sizeof(int) * pk.vlen);
         const int len = pk.tlen > pk.vlen ? pk.tlen : pk.vlen;
-        hipLaunchKernelGGL(build_maps_kernel, dim3(cdiv(len, 256)), dim3(256), 0, d->stream, n, pk, d->tmap, d->vmap);
+        hipLaunchKernelGGL(build_maps_kernel, dim3(cdiv(len, 256)), dim3(256), 0, d->stream, n, pk, d->tmap, d->vmap,
+                           d->f64);
         if (d->fast->attr(d->fast->lds) != hipSuccess) FAIL("hipFuncSetAttribute(LDS=%d) failed", d->fast->lds);
         d->k_fvp = d->fast->launch;
         d->k_pg = d->fast->launch_pg;
@@ -1873,9 +2008,10 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
         d->coop_e = NULL;
         d->coop = 0;
         const char *ec = getenv("TRPO_COOP");
-        if (!(ec && atoi(ec) == 0) && T[1] == T[2] && (T[1] == 2 || T[1] == 4) && T[3] == 1)
+        if ((d->f64 || !(ec && atoi(ec) == 0)) && T[1] == T[2] && T[3] == 1)
             for (const CoopEntry &e : kCoop)
-                if (e.T0 == T[0] && e.TH == T[1] && e.act == d->fast->act) d->coop_e = &e;
+                if (e.f64 == d->f64 && e.T0 == T[0] && e.TH == T[1] && e.act == d->fast->act) d->coop_e = &e;
+        if (d->f64 && !d->coop_e) FAIL("internal: no fp64 kernel for tile shape %dx%dx%dx%d", T[0], T[1], T[2], T[3]);
         if (d->coop_e) {
             if (d->coop_e->attr(d->coop_e->lds) != hipSuccess)
                 FAIL("hipFuncSetAttribute(LDS=%d) failed", d->coop_e->lds);
@@ -1887,14 +2023,14 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
             d->slab = d->coop_e->slab;
             DMALLOC(d->imap, sizeof(int) * d->slab);
             hipLaunchKernelGGL(build_imap_coop_kernel, dim3(cdiv(d->slab, 256)), dim3(256), 0, d->stream, n, T[0],
-                               T[1], d->imap, d->slab);
+                               T[1], d->f64, d->imap, d->slab);
         } else {
             DMALLOC(d->imap, sizeof(int) * d->slab);
             hipLaunchKernelGGL(build_imap_kernel, dim3(cdiv(d->slab, 256)), dim3(256), 0, d->stream, n, pk, d->imap,
                                d->slab);
         }
-        snprintf(d->name, sizeof d->name, "mfma-mlp3 %dx%dx%dx%d%s%s", T[0], T[1], T[2], T[3],
-                 d->fast->act >= 0 ? " ttl" : "", d->coop ? " coop" : "");
+        snprintf(d->name, sizeof d->name, "mfma-mlp3 %dx%dx%dx%d%s%s%s", T[0], T[1], T[2], T[3],
+                 d->fast->act >= 0 ? " ttl" : "", d->coop ? " coop" : "", d->f64 ? " fp64" : "");
     } else {
         DMALLOC(d->th32, sizeof(float) * d->P);
         DMALLOC(d->v32, sizeof(float) * d->P);
@@ -1906,6 +2042,7 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
         DMALLOC(d->imap, sizeof(int) * d->slab);
         hipLaunchKernelGGL(iota_kernel, dim3(cdiv(d->slab, 256)), dim3(256), 0, d->stream, d->imap, d->slab, d->nw);
         snprintf(d->name, sizeof d->name, "generic");
+        d->esz = sizeof(float);
     }
     if (hipStreamSynchronize(d->stream) != hipSuccess) FAIL("initialisation kernels failed");
     d->damping = 0.1;
@@ -1960,7 +2097,7 @@ extern "C" int trpo_dev_set_theta(trpo_dev *d, const double *theta) {
     HCHK(hipMemcpyAsync(d->theta64, theta, sizeof(double) * d->P, hipMemcpyHostToDevice, d->stream));
     if (d->fast) {
         hipLaunchKernelGGL(gather_pack_kernel, dim3(cdiv(d->pack.iv, 256)), dim3(256), 0, d->stream, d->tpack,
-                           d->theta64, d->tmap, d->pack.iv);
+                           d->theta64, d->tmap, d->pack.iv, d->f64);
     } else {
         hipLaunchKernelGGL(to_f32_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, d->th32, d->theta64, d->P);
     }
@@ -1978,10 +2115,10 @@ extern "C" int trpo_dev_set_std(trpo_dev *d, const double *stdv) {
     if (d->fast) {
         const int len = 16 * d->pack.T[3];
         hipLaunchKernelGGL(set_invvar_kernel, dim3(1), dim3(cdiv(len, 64) * 64), 0, d->stream,
-                           d->tpack + d->pack.iv, d->std64, d->net.A, len);
+                           (void *)((char *)d->tpack + d->esz * d->pack.iv), d->std64, d->net.A, len, d->f64);
     } else {
-        hipLaunchKernelGGL(set_invvar_kernel, dim3(cdiv(d->net.A, 256)), dim3(256), 0, d->stream, d->iv32, d->std64,
-                           d->net.A, d->net.A);
+        hipLaunchKernelGGL(set_invvar_kernel, dim3(cdiv(d->net.A, 256)), dim3(256), 0, d->stream, (void *)d->iv32,
+                           d->std64, d->net.A, d->net.A, 0);
     }
     HCHK(hipGetLastError());
     HCHK(hipStreamSynchronize(d->stream));
@@ -1993,7 +2130,7 @@ static void choose_reduction(trpo_dev *d) {
     // (G x P values per FVP); otherwise block slabs + a reduce kernel
     // decided from P only, so every rank of a sharded run picks the same collective pattern
     const char *e = getenv("TRPO_ATOMIC");
-    const bool ok = d->fast && !d->coop && d->fast->emax <= 4 && d->P <= 2048;
+    const bool ok = d->fast && !d->coop && !d->f64 && d->fast->emax <= 4 && d->P <= 2048;
     d->atomic = ok && 256L * d->P <= 400000;
     if (e) d->atomic = ok && atoi(e) != 0;
 }
@@ -2037,12 +2174,12 @@ extern "C" int trpo_dev_set_obs(trpo_dev *d, const double *obs, size_t n) {
         const int ld = 16 * d->pack.T[0];
         if (npad > d->npad_cap) {
             if (d->obs4) hipFree(d->obs4);
-            HCHK(hipMalloc((void **)&d->obs4, sizeof(float) * npad * ld));
+            HCHK(hipMalloc((void **)&d->obs4, d->esz * npad * ld));
             d->npad_cap = npad;
         }
         if (n)
             hipLaunchKernelGGL(obs_pad_kernel, dim3(cdiv((long)npad * ld, 256)), dim3(256), 0, d->stream,
-                               (float *)d->obs4, tmp, (int)n, (int)npad, L0, ld);
+                               d->obs4, tmp, (int)n, (int)npad, L0, ld, d->f64);
     } else {
         if ((size_t)n * L0 > d->npad_cap) {
             if (d->obs32) hipFree(d->obs32);
@@ -2059,8 +2196,8 @@ extern "C" int trpo_dev_set_obs(trpo_dev *d, const double *obs, size_t n) {
     }
     if (d->grid > d->slab_blocks) {
         if (d->slabs) hipFree(d->slabs);
-        HCHK(hipMalloc((void **)&d->slabs, sizeof(float) * (size_t)d->slab * d->grid));
-        HCHK(hipMemsetAsync(d->slabs, 0, sizeof(float) * (size_t)d->slab * d->grid, d->stream));
+        HCHK(hipMalloc((void **)&d->slabs, d->esz * (size_t)d->slab * d->grid));
+        HCHK(hipMemsetAsync(d->slabs, 0, d->esz * (size_t)d->slab * d->grid, d->stream));
         d->slab_blocks = d->grid;
     }
     HCHK(hipGetLastError());
@@ -2144,14 +2281,24 @@ static IterArgs plain_args(trpo_dev *d, const int *skip) {
     a.ntiles = cdiv((long)d->n, 16);
     a.P = d->P;
     a.nw = d->nw;
-    a.tpack = d->tpack;
-    a.vpack = d->vpack;
-    a.slabs = d->slabs;
+    a.tpack = (const float *)d->tpack;      // fp64 mode: the kernel reinterprets (element type T)
+    a.vpack = (const float *)d->vpack;
+    a.slabs = (float *)d->slabs;
     a.imap = d->imap;
     a.skip = skip;
     a.R_out = 1;
     a.R_in = 1;
     return a;
+}
+
+// block partials (fp32, or fp64 in the fp64 mode) -> d->zacc, fixed order
+static void launch_reduce(trpo_dev *d, const int *skip) {
+    if (d->f64)
+        hipLaunchKernelGGL(reduce_slabs_kernel<double>, dim3(cdiv(d->slab, 64)), dim3(1024), 0, d->stream,
+                           (const double *)d->slabs, d->grid, d->slab, d->imap, d->zacc, skip);
+    else
+        hipLaunchKernelGGL(reduce_slabs_kernel<float>, dim3(cdiv(d->slab, 64)), dim3(1024), 0, d->stream,
+                           (const float *)d->slabs, d->grid, d->slab, d->imap, d->zacc, skip);
 }
 
 // enqueue: partial sums of F*src into d->zacc (global over ranks)
@@ -2165,11 +2312,10 @@ static int enqueue_fvp_core(trpo_dev *d, const double *src, const int *skip) {
     } else {
         hipLaunchKernelGGL(to_f32_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, d->v32, src, d->P);
         hipLaunchKernelGGL(fvp_generic_kernel, dim3(d->grid), dim3(GEN_T), 0, d->stream, d->obs32, (int)d->n,
-                           d->th32, d->v32, d->iv32, d->scratch, d->srows, d->slabs, n, skip);
+                           d->th32, d->v32, d->iv32, d->scratch, d->srows, (float *)d->slabs, n, skip);
         HCHK(hipGetLastError());
     }
-    hipLaunchKernelGGL(reduce_slabs_kernel, dim3(cdiv(d->slab, 64)), dim3(1024), 0, d->stream, d->slabs, d->grid,
-                       d->slab, d->imap, d->zacc, skip);
+    launch_reduce(d, skip);
     HCHK(hipGetLastError());
     if (d->comm) {
         if (ncclAllReduce(d->zacc, d->zacc, d->nw, ncclFloat64, ncclSum, d->comm, d->stream) != ncclSuccess) return -4;
@@ -2183,7 +2329,7 @@ extern "C" int trpo_dev_fvp(trpo_dev *d) {
     HCHK(hipSetDevice(d->device));
     if (d->fast)
         hipLaunchKernelGGL(gather_pack_kernel, dim3(cdiv(d->pack.vlen, 256)), dim3(256), 0, d->stream, d->vpack,
-                           d->vec[TRPO_VEC_V], d->vmap, d->pack.vlen);
+                           d->vec[TRPO_VEC_V], d->vmap, d->pack.vlen, d->f64);
     int rc = enqueue_fvp_core(d, d->vec[TRPO_VEC_V], &d->ctl->zero);
     if (rc) return rc;
     hipLaunchKernelGGL(fvp_epilogue_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, d->zacc,
@@ -2200,7 +2346,7 @@ extern "C" int trpo_dev_fvp_kernel(trpo_dev *d) {
         d->k_fvp(dim3(d->grid), d->k_lds, d->stream, a, d->net);
     } else {
         hipLaunchKernelGGL(fvp_generic_kernel, dim3(d->grid), dim3(GEN_T), 0, d->stream, d->obs32, (int)d->n,
-                           d->th32, d->v32, d->iv32, d->scratch, d->srows, d->slabs, d->net, &d->ctl->zero);
+                           d->th32, d->v32, d->iv32, d->scratch, d->srows, (float *)d->slabs, d->net, &d->ctl->zero);
     }
     HCHK(hipGetLastError());
     return 0;
@@ -2237,7 +2383,7 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
     const long M = (long)maxiter;
     const int RP = d->R * d->P;
     CG_DISPATCH(E, cg_init_kernel, dim3(1), dim3(1024), shm, d->stream, b, x, d->rbuf[0], d->pbuf[0], d->P, d->ctl,
-                d->st, d->hist, (int)maxiter, resth, d->vmap, d->vpack, vlen, d->atomic ? acc_slot(d, 0) : nullptr,
+                d->st, d->hist, (int)maxiter, resth, d->vmap, d->vpack, vlen, d->f64, d->atomic ? acc_slot(d, 0) : nullptr,
                 d->atomic ? RP : 0);
     if (d->fast && !d->coop) {
         for (long j = 0; j < M; ++j) {
@@ -2269,8 +2415,7 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
             if (d->atomic) {
                 rc = allreduce(d, acc_slot(d, j), (size_t)RP);
             } else {
-                hipLaunchKernelGGL(reduce_slabs_kernel, dim3(cdiv(d->slab, 64)), dim3(1024), 0, d->stream, d->slabs,
-                                   d->grid, d->slab, d->imap, d->zacc, done);
+                launch_reduce(d, done);
                 rc = allreduce(d, d->zacc, d->nw);
             }
             if (rc) return rc;
@@ -2280,7 +2425,7 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
             CG_DISPATCH(E, cg_update_kernel, dim3(1), dim3(1024), 0, d->stream,
                         d->atomic ? acc_slot(d, M - 1) : d->zacc, d->atomic ? d->R : 1, d->pbuf[in], d->rbuf[in],
                         d->pbuf[out], d->rbuf[out], x, d->P, d->nw, d->ctl, d->st + in, d->st + out, d->hist,
-                        (const int *)nullptr, (float *)nullptr, 0);
+                        (const int *)nullptr, (void *)nullptr, 0, 0);
         }
     } else {
         // generic or cooperative kernel: FVP, reduce, [all-reduce], CG step per iteration
@@ -2291,7 +2436,7 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
             // cooperative kernel: the update also packs p' for the next FVP (fp32 fragment order)
             CG_DISPATCH(E, cg_update_kernel, dim3(1), dim3(1024), d->coop ? shm : 0, d->stream, d->zacc, 1,
                         d->pbuf[cur], d->rbuf[cur], d->pbuf[nxt], d->rbuf[nxt], x, d->P, d->nw, d->ctl, d->st + cur,
-                        d->st + nxt, d->hist, d->vmap, d->vpack, d->coop ? vlen : 0);
+                        d->st + nxt, d->hist, d->vmap, d->vpack, d->coop ? vlen : 0, d->f64);
         }
     }
     HCHK(hipGetLastError());
@@ -2408,7 +2553,7 @@ extern "C" int trpo_dev_read_stamps(unsigned long long *out, int n) {
 extern "C" int trpo_dev_geometry(const trpo_dev *d, int *blocks, int *threads, int *lds_bytes) {
     if (!d) return -1;
     if (blocks) *blocks = d->grid;
-    if (threads) *threads = d->fast ? 512 : GEN_T;
+    if (threads) *threads = d->coop ? d->coop_e->threads : d->fast ? 64 * d->fast->waves : GEN_T;
     if (lds_bytes) *lds_bytes = d->fast ? d->k_lds : 0;
     return 0;
 }
@@ -2441,21 +2586,23 @@ extern "C" double trpo_dev_n_total(const trpo_dev *d) { return d ? d->n_total : 
 // policy gradient through the MFMA tile kernel (MODE 1) -- TRPO_Update path
 // ---------------------------------------------------------------------------
 // (Action - Mean) rows [npad][ld] in fp32 (difference taken in fp64) and Adv [npad]
+template <typename T>
 __global__ void pg_prep_kernel(const double *__restrict__ roll, int n, int npad, int A, int ld,
-                               float *__restrict__ dm, float *__restrict__ adv) {
+                               T *__restrict__ dm, T *__restrict__ adv) {
     const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= (long)npad * ld) return;
     const int s = (int)(e / ld), j = (int)(e % ld), W = 2 * A + 1;
-    dm[e] = (s < n && j < A) ? (float)(roll[(long)s * W + A + j] - roll[(long)s * W + j]) : 0.0f;
-    if (j == 0) adv[s] = s < n ? (float)roll[(long)s * W + 2 * A] : 0.0f;
+    dm[e] = (s < n && j < A) ? (T)(roll[(long)s * W + A + j] - roll[(long)s * W + j]) : (T)0;
+    if (j == 0) adv[s] = s < n ? (T)roll[(long)s * W + 2 * A] : (T)0;
 }
 
 // 1 / sigma^2 with sigma = exp(LogStd) of the current parameters
-__global__ void pg_iv_kernel(const double *__restrict__ theta, int P, int A, int len, float *__restrict__ iv) {
+template <typename T>
+__global__ void pg_iv_kernel(const double *__restrict__ theta, int P, int A, int len, T *__restrict__ iv) {
     const int j = threadIdx.x;
     if (j < len) {
         const double es = j < A ? exp(theta[P - A + j]) : 1.0;
-        iv[j] = j < A ? (float)(1.0 / (es * es)) : 0.0f;
+        iv[j] = j < A ? (T)(1.0 / (es * es)) : (T)0;
     }
 }
 
@@ -2469,23 +2616,29 @@ int trpo_dev_pg_sums_fast(trpo_dev *d, const double *roll64, const double **zacc
         if (d->pg_adv) hipFree(d->pg_adv);
         d->pg_d = d->pg_adv = NULL;
         d->pg_cap = 0;
-        HCHK(hipMalloc((void **)&d->pg_d, sizeof(float) * npad * ld));
-        HCHK(hipMalloc((void **)&d->pg_adv, sizeof(float) * npad));
+        HCHK(hipMalloc((void **)&d->pg_d, d->esz * npad * ld));
+        HCHK(hipMalloc((void **)&d->pg_adv, d->esz * npad));
         d->pg_cap = npad;
     }
-    if (!d->pg_iv) HCHK(hipMalloc((void **)&d->pg_iv, sizeof(float) * ld));
-    hipLaunchKernelGGL(pg_prep_kernel, dim3(cdiv((long)npad * ld, 256)), dim3(256), 0, d->stream, roll64,
-                       (int)d->n, (int)npad, d->net.A, ld, d->pg_d, d->pg_adv);
-    hipLaunchKernelGGL(pg_iv_kernel, dim3(1), dim3(cdiv(ld, 64) * 64), 0, d->stream, d->theta64, d->P, d->net.A, ld,
-                       d->pg_iv);
+    if (!d->pg_iv) HCHK(hipMalloc((void **)&d->pg_iv, d->esz * ld));
+    if (d->f64) {
+        hipLaunchKernelGGL(pg_prep_kernel<double>, dim3(cdiv((long)npad * ld, 256)), dim3(256), 0, d->stream, roll64,
+                           (int)d->n, (int)npad, d->net.A, ld, (double *)d->pg_d, (double *)d->pg_adv);
+        hipLaunchKernelGGL(pg_iv_kernel<double>, dim3(1), dim3(cdiv(ld, 64) * 64), 0, d->stream, d->theta64, d->P,
+                           d->net.A, ld, (double *)d->pg_iv);
+    } else {
+        hipLaunchKernelGGL(pg_prep_kernel<float>, dim3(cdiv((long)npad * ld, 256)), dim3(256), 0, d->stream, roll64,
+                           (int)d->n, (int)npad, d->net.A, ld, (float *)d->pg_d, (float *)d->pg_adv);
+        hipLaunchKernelGGL(pg_iv_kernel<float>, dim3(1), dim3(cdiv(ld, 64) * 64), 0, d->stream, d->theta64, d->P,
+                           d->net.A, ld, (float *)d->pg_iv);
+    }
     IterArgs a = plain_args(d, &d->ctl->zero);
     a.pg_d4 = reinterpret_cast<const float4 *>(d->pg_d);
-    a.pg_adv = d->pg_adv;
+    a.pg_adv = (const float *)d->pg_adv;
     a.pg_iv4 = reinterpret_cast<const float4 *>(d->pg_iv);
     d->k_pg(dim3(d->grid), d->k_lds, d->stream, a, d->net);
     HCHK(hipGetLastError());
-    hipLaunchKernelGGL(reduce_slabs_kernel, dim3(cdiv(d->slab, 64)), dim3(1024), 0, d->stream, d->slabs, d->grid,
-                       d->slab, d->imap, d->zacc, &d->ctl->zero);
+    launch_reduce(d, &d->ctl->zero);
     HCHK(hipGetLastError());
     if (allreduce(d, d->zacc, d->nw)) return -4;
     *zacc = d->zacc;

@@ -296,7 +296,10 @@ def CG_FPGA(param: TRPOparam, result: np.ndarray, b: np.ndarray, max_iter: int =
 class Context:
     """Device-resident FVP/CG problem: weights, observations and P-vectors stay in HBM."""
 
-    def __init__(self, layers, acfunc: str, theta, obs, std, cg_damping: float = 0.1, device: int = -1):
+    def __init__(self, layers, acfunc: str, theta, obs, std, cg_damping: float = 0.1, device: int = -1,
+                 precision: str = None):
+        """precision: None (TRPO_PRECISION from the environment, default "fp32") or "fp32" / "fp64".
+        "fp64" runs the FVP in fp64 on the fp64 MFMA -- the reference's own arithmetic."""
         L = lib()
         self.layers = [int(x) for x in layers]
         self.acfunc = acfunc
@@ -308,9 +311,19 @@ class Context:
             raise ValueError("shape mismatch: theta %s obs %s std %s for layers %s"
                              % (theta.shape, obs.shape, std.shape, self.layers))
         self.n = obs.shape[0]
-        self._h = L.trpo_ctx_create(len(self.layers), _sizes(self.layers), acfunc.encode(),
-                                    theta.ctypes.data, obs.ctypes.data, self.n, std.ctypes.data, cg_damping,
-                                    device)
+        saved = os.environ.get("TRPO_PRECISION")
+        if precision is not None:                      # read by the library at context creation
+            os.environ["TRPO_PRECISION"] = precision
+        try:
+            self._h = L.trpo_ctx_create(len(self.layers), _sizes(self.layers), acfunc.encode(),
+                                        theta.ctypes.data, obs.ctypes.data, self.n, std.ctypes.data, cg_damping,
+                                        device)
+        finally:
+            if precision is not None:
+                if saved is None:
+                    os.environ.pop("TRPO_PRECISION", None)
+                else:
+                    os.environ["TRPO_PRECISION"] = saved
         if not self._h:
             raise TRPOError("trpo_ctx_create failed: " + last_error())
 
