@@ -11,7 +11,7 @@ order differs.  Tolerances (stated):
     independent fp64 evaluation lands from the reference: fix_cg_n3150_th0 6.7e-6 (device 6.73e-6),
     [20,32,32,2] 1.0e-7 (device 1.2e-7), [30,64,64,4] 2.0e-8 (device 1.9e-8), others <= 4.1e-9.
     Those two cases carry 3x their measured bound.  Same iteration count, and the residual
-    history to rtol 1e-6 (atol 1e-15 rdotr[0]) down to rdotr = 1e-10 rdotr[0] (the fp64 floor; below it, rounding noise).
+    history to rtol 1e-6 (atol 1e-13 rdotr[0]) down to rdotr = 1e-10 rdotr[0] (the fp64 floor; below it, rounding noise).
   * TRPO_Update: policy gradient <= 1e-12, step / new theta <= 5e-9, line-search ratios rtol 5e-9;
     syn_update_sigma_n5000 2e-7 (explicit-matrix CG lands 5.3e-8 from the reference there)
 """
@@ -31,7 +31,7 @@ CG_TOL_SHAPE = {(20, 32, 32, 2): 4e-7, (30, 64, 64, 4): 6e-8}
 
 def _check_history(rr, ref, iters):
     keep = [i for i in range(iters + 1) if ref[i] >= 1e-10 * ref[0]]     # below: rounding noise
-    np.testing.assert_allclose(np.asarray(rr)[keep], np.asarray(ref)[keep], rtol=1e-6, atol=1e-15 * ref[0])
+    np.testing.assert_allclose(np.asarray(rr)[keep], np.asarray(ref)[keep], rtol=1e-6, atol=1e-13 * ref[0])
     assert len(keep) >= min(iters + 1, 8)
 
 

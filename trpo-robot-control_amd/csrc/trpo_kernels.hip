@@ -1445,7 +1445,7 @@ constexpr int GEN_T = 256;
 __global__ void __launch_bounds__(GEN_T)
 fvp_generic_kernel(const float *__restrict__ obs, int n, const float *__restrict__ th, const float *__restrict__ v,
                    const float *__restrict__ iv, float *__restrict__ scratch, int srows, float *__restrict__ slabs,
-                   Net net, const int *__restrict__ skip) {
+                   int sstride, Net net, const int *__restrict__ skip) {
     if (*skip) return;
     const int tid = threadIdx.x;
     float *Y = scratch + (long)blockIdx.x * 3 * srows * GEN_T;
@@ -1454,7 +1454,7 @@ fvp_generic_kernel(const float *__restrict__ obs, int n, const float *__restrict
     int roff[MAXL + 1];
     roff[0] = 0;
     for (int i = 0; i < net.nl; ++i) roff[i + 1] = roff[i] + net.L[i];
-    float *slab = slabs + (long)blockIdx.x * net.P;
+    float *slab = slabs + (long)blockIdx.x * sstride;
     const int nw = net.P - net.A;
     for (int q = tid; q < nw; q += GEN_T) slab[q] = 0.0f;
 
@@ -1525,36 +1525,44 @@ fvp_generic_kernel(const float *__restrict__ obs, int n, const float *__restrict
 // block = 64 parameters x 16 slab groups
 // ---------------------------------------------------------------------------
 // zacc[imap[j]] = sum over blocks of slabs[b][j], fp64, fixed order; j runs over the slab
-// layout (contiguous, coalesced).  block = 64 slab positions x 16 block groups.
+// layout (contiguous).  A block of 256 threads owns RS_POS consecutive slab positions; each
+// thread loads 16 B (4 fp32 / 2 fp64 positions) from every SG-th block partial (all its loads in
+// flight together), then the SG sub-sums are added in a fixed order through LDS.
+constexpr int RS_POS = 32, RS_THREADS = 256;
 template <typename ST>
-__global__ void __launch_bounds__(1024)
+__global__ void __launch_bounds__(RS_THREADS)
 reduce_slabs_kernel(const ST *__restrict__ slabs, int G, int slab, const int *__restrict__ imap,
                     double *__restrict__ zacc, const int *__restrict__ skip) {
-    __shared__ double part[16][64];
-    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-    const int j = blockIdx.x * 64 + tx;
-    const int m = j < slab ? imap[j] : -1;
+    constexpr int VE = 16 / sizeof(ST), LP = RS_POS / VE, SG = RS_THREADS / LP, NLD = 256 / SG;
+    typedef ST VT __attribute__((ext_vector_type(VE)));
+    __shared__ double part[SG][RS_POS + 1];
+    const int t = threadIdx.x, lp = t % LP, sg = t / LP;
+    const int j0 = blockIdx.x * RS_POS + lp * VE;        // slab % RS_POS == 0 (multiple of 256)
+    const int m = t < RS_POS ? imap[blockIdx.x * RS_POS + t] : -1;
     if (*skip) return;
-    double s = 0.0;
-    if (j < slab) {
-        for (int b0 = 0; b0 < G; b0 += 256) {      // 16 independent loads in flight per chunk
-            ST v[16];
+    double s[VE];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const int b = b0 + ty + 16 * k;
-                v[k] = b < G ? slabs[(long)b * slab + j] : (ST)0;
-            }
+    for (int e = 0; e < VE; ++e) s[e] = 0.0;
+    for (int b0 = sg; b0 < G; b0 += SG * NLD) {
+        VT v[NLD];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) s += (double)v[k];
+        for (int k = 0; k < NLD; ++k) {
+            const int b = b0 + SG * k;
+            v[k] = b < G ? *reinterpret_cast<const VT *>(slabs + (long)b * slab + j0) : (VT)0;
         }
-    }
-    part[ty][tx] = s;
-    __syncthreads();
-    if (ty == 0 && m >= 0) {
-        double t = 0.0;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) t += part[k][tx];
-        zacc[m] = t;
+        for (int k = 0; k < NLD; ++k)
+#pragma unroll
+            for (int e = 0; e < VE; ++e) s[e] += (double)v[k][e];
+    }
+#pragma unroll
+    for (int e = 0; e < VE; ++e) part[sg][lp * VE + e] = s[e];
+    __syncthreads();
+    if (t < RS_POS && m >= 0) {
+        double a = 0.0;
+#pragma unroll 8
+        for (int k = 0; k < SG; ++k) a += part[k][t];
+        zacc[m] = a;
     }
 }
 
@@ -1571,13 +1579,26 @@ __global__ void fvp_epilogue_kernel(const double *__restrict__ zacc, const doubl
 // CG (src/TRPO_CG.c:11-113), one 1024-thread block, all fp64, fixed-order sums
 // ---------------------------------------------------------------------------
 
-// p -> fragment-order fp32 pack for the next FVP (fast path only; vlen == 0 otherwise)
-__device__ void write_vpack(const double *sp, const int *__restrict__ vmap, void *vpack, int vlen, int f64) {
-    for (int e = threadIdx.x; e < vlen; e += blockDim.x) {
-        const int m = vmap[e];
-        const double v = m >= 0 ? sp[m] : 0.0;
-        if (f64) reinterpret_cast<double *>(vpack)[e] = v;
-        else reinterpret_cast<float *>(vpack)[e] = (float)v;
+// p -> fragment-order pack (fp32, or fp64 in the fp64 mode) for the next FVP (fast path only;
+// vlen == 0 otherwise).  The map entries are loaded up front with the kernel's other loads.
+constexpr int VPACK_PER_THREAD = 8;                 // vlen <= 8 * 1024 (checked at context creation)
+__device__ __forceinline__ void load_vmap(const int *__restrict__ vmap, int vlen, int (&vm)[VPACK_PER_THREAD]) {
+#pragma unroll
+    for (int k = 0; k < VPACK_PER_THREAD; ++k) {
+        const int e = threadIdx.x + k * 1024;
+        vm[k] = e < vlen ? vmap[e] : -1;
+    }
+}
+__device__ __forceinline__ void write_vpack(const double *sp, const int (&vm)[VPACK_PER_THREAD], void *vpack, int vlen,
+                                            int f64) {
+#pragma unroll
+    for (int k = 0; k < VPACK_PER_THREAD; ++k) {
+        const int e = threadIdx.x + k * 1024;
+        if (e < vlen) {
+            const double v = vm[k] >= 0 ? sp[vm[k]] : 0.0;
+            if (f64) reinterpret_cast<double *>(vpack)[e] = v;
+            else reinterpret_cast<float *>(vpack)[e] = (float)v;
+        }
     }
 }
 
@@ -1590,11 +1611,13 @@ cg_init_kernel(const double *__restrict__ b, double *x, double *r, double *p, in
     __shared__ double sh[16];
     extern __shared__ double sp[];
     double bv[E];
+    int vm[VPACK_PER_THREAD];
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const int q = threadIdx.x + e * 1024;
         bv[e] = q < P ? b[q] : 0.0;
     }
+    load_vmap(vmap, vlen, vm);
     for (int e = threadIdx.x; e < zero_len; e += 1024) acc_zero[e] = 0.0;
     double s = 0.0;
 #pragma unroll
@@ -1621,7 +1644,7 @@ cg_init_kernel(const double *__restrict__ b, double *x, double *r, double *p, in
         hist[1] = 0.0;
         ctl->done = (rr < resth || maxiter == 0) ? 1 : 0;
     }
-    write_vpack(sp, vmap, vpack, vlen, f64);    // block_sum's barriers ordered the sp writes
+    write_vpack(sp, vm, vpack, vlen, f64);    // block_sum's barriers ordered the sp writes
 }
 
 // One CG step after z = F p is available as R_in fp64 partial-sum replicas (src/TRPO_CG.c:65-103):
@@ -1633,12 +1656,14 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
                  const double *__restrict__ r_in, double *p_out, double *r_out, double *x, int P, int nw, Ctl *ctl,
                  const CgSt *st_in, CgSt *st_out, double *hist,
                  const int *__restrict__ vmap, void *vpack, int vlen, int f64) {
-    __shared__ double sh[16];
+    __shared__ double sh[64 + 128];                  // block_sums_dpp<1> and <2> regions (16 waves)
     const int done = ctl->done;
     const double n = ctl->n_total, lam = ctl->damping, th = ctl->resth;
     const int maxiter = ctl->maxiter;
     const CgSt sin = *st_in;
     double pv[E], zv[E], xv[E], rv[E];
+    int vm[VPACK_PER_THREAD];
+    load_vmap(vmap, vlen, vm);
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const int q = threadIdx.x + e * 1024;
@@ -1660,7 +1685,9 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
         zv[e] = (q < nw ? zv[e] / n : 2.0 * pv[e]) + lam * pv[e];
         pz += pv[e] * zv[e];
     }
-    const double alpha = sin.rdotr / block_sum(pz, sh);
+    double s1[1] = {pz};
+    block_sums_dpp<1>(s1, sh);
+    const double alpha = sin.rdotr / s1[0];
     double rr = 0.0, xx = 0.0;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -1669,8 +1696,9 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
         rr += rv[e] * rv[e];
         xx += xv[e] * xv[e];
     }
-    const double nr = block_sum(rr, sh);
-    const double xn = block_sum(xx, sh);
+    double s2[2] = {rr, xx};
+    block_sums_dpp<2>(s2, sh + 64);
+    const double nr = s2[0], xn = s2[1];
     const double beta = nr / sin.rdotr;
     extern __shared__ double sp[];
 #pragma unroll
@@ -1686,7 +1714,7 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
     }
     if (vlen) {                                        // fp32 fragment pack of p' for the next FVP
         __syncthreads();
-        write_vpack(sp, vmap, vpack, vlen, f64);
+        write_vpack(sp, vm, vpack, vlen, f64);
     }
     if (threadIdx.x == 0) {
         const int it = sin.iter + 1;
@@ -1991,6 +2019,8 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
         pk.vb[2] = pk.vb[1] + 16 * T[2];
         pk.vlen = pk.vb[2] + 16 * T[3];
         if (pk.tlen != d->fast->tlen || pk.vlen != d->fast->vlen) FAIL("internal: pack layout mismatch");
+        if (pk.vlen > VPACK_PER_THREAD * 1024) FAIL("internal: direction pack of %d exceeds the CG kernels' %d",
+                                                    pk.vlen, VPACK_PER_THREAD * 1024);
         DMALLOC(d->tpack, d->esz * pk.tlen);
         DMALLOC(d->vpack, d->esz * pk.vlen);
         DMALLOC(d->tmap, sizeof(int) * pk.tlen);
@@ -2038,7 +2068,7 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
         int rows = 0;
         for (int i = 0; i < n.nl; ++i) rows += n.L[i];
         d->srows = rows;
-        d->slab = d->P;
+        d->slab = cdiv(d->P, RS_POS) * RS_POS;           // row stride of the block partials
         DMALLOC(d->imap, sizeof(int) * d->slab);
         hipLaunchKernelGGL(iota_kernel, dim3(cdiv(d->slab, 256)), dim3(256), 0, d->stream, d->imap, d->slab, d->nw);
         snprintf(d->name, sizeof d->name, "generic");
@@ -2294,10 +2324,10 @@ static IterArgs plain_args(trpo_dev *d, const int *skip) {
 // block partials (fp32, or fp64 in the fp64 mode) -> d->zacc, fixed order
 static void launch_reduce(trpo_dev *d, const int *skip) {
     if (d->f64)
-        hipLaunchKernelGGL(reduce_slabs_kernel<double>, dim3(cdiv(d->slab, 64)), dim3(1024), 0, d->stream,
+        hipLaunchKernelGGL(reduce_slabs_kernel<double>, dim3(d->slab / RS_POS), dim3(RS_THREADS), 0, d->stream,
                            (const double *)d->slabs, d->grid, d->slab, d->imap, d->zacc, skip);
     else
-        hipLaunchKernelGGL(reduce_slabs_kernel<float>, dim3(cdiv(d->slab, 64)), dim3(1024), 0, d->stream,
+        hipLaunchKernelGGL(reduce_slabs_kernel<float>, dim3(d->slab / RS_POS), dim3(RS_THREADS), 0, d->stream,
                            (const float *)d->slabs, d->grid, d->slab, d->imap, d->zacc, skip);
 }
 
@@ -2312,7 +2342,7 @@ static int enqueue_fvp_core(trpo_dev *d, const double *src, const int *skip) {
     } else {
         hipLaunchKernelGGL(to_f32_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, d->v32, src, d->P);
         hipLaunchKernelGGL(fvp_generic_kernel, dim3(d->grid), dim3(GEN_T), 0, d->stream, d->obs32, (int)d->n,
-                           d->th32, d->v32, d->iv32, d->scratch, d->srows, (float *)d->slabs, n, skip);
+                           d->th32, d->v32, d->iv32, d->scratch, d->srows, (float *)d->slabs, d->slab, n, skip);
         HCHK(hipGetLastError());
     }
     launch_reduce(d, skip);
@@ -2346,7 +2376,8 @@ extern "C" int trpo_dev_fvp_kernel(trpo_dev *d) {
         d->k_fvp(dim3(d->grid), d->k_lds, d->stream, a, d->net);
     } else {
         hipLaunchKernelGGL(fvp_generic_kernel, dim3(d->grid), dim3(GEN_T), 0, d->stream, d->obs32, (int)d->n,
-                           d->th32, d->v32, d->iv32, d->scratch, d->srows, (float *)d->slabs, d->net, &d->ctl->zero);
+                           d->th32, d->v32, d->iv32, d->scratch, d->srows, (float *)d->slabs, d->slab, d->net,
+                           &d->ctl->zero);
     }
     HCHK(hipGetLastError());
     return 0;
