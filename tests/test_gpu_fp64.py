@@ -124,3 +124,19 @@ def test_fp64_rejects_shapes_without_tile_kernel():
     th = synth.make_theta(layers)
     with pytest.raises(trpo_amd.TRPOError, match="fp64"):
         trpo_amd.Context(layers, "ltttl", th, synth.make_obs(10, 15), np.ones(3), precision="fp64")
+
+
+@pytest.mark.parametrize("name", ["syn_2x64_cg_n50000", "fix_cg_n3150_th1e-10"])
+def test_fp64_fused_and_unfused_cg_agree(name, monkeypatch):
+    """The cooperative kernel's CG-iteration mode (CG step fused into the FVP prologue, every
+    block redundantly) against the separate cg_update kernel: same iterations, same step."""
+    c = cases.case(name)
+    x = cases.inputs(c)
+    out = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("TRPO_COOP_FUSED", fused)
+        with _ctx(x) as ctx:
+            out[fused] = ctx.cg(x["vin"], c["maxiter"], c["resth"])
+            assert ctx.cg_history()[2] == c["iters"]
+    assert cases.rel_l2(out["1"], out["0"]) <= 1e-9
+    assert cases.rel_l2(out["1"], cases.expected(c)) <= CG_TOL

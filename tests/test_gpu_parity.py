@@ -179,13 +179,16 @@ def test_output_widths_and_activations_against_oracle(layers, acts):
 
 
 @pytest.mark.parametrize("layers", [[15, 32, 32, 3], [20, 32, 32, 2], [30, 64, 64, 4], [15, 64, 64, 3]])
-@pytest.mark.parametrize("coop", ["1", "0"])
-def test_cooperative_kernel_shapes_against_oracle(layers, coop, monkeypatch):
-    """Wide hidden layers run the cooperative tile kernel (TRPO_COOP=0: the one-wave-per-tile
+@pytest.mark.parametrize("mode", ["fused", "unfused", "off"])
+def test_cooperative_kernel_shapes_against_oracle(layers, mode, monkeypatch):
+    """Wide hidden layers run the cooperative tile kernel, by default with the CG step fused into
+    its prologue (TRPO_COOP_FUSED=0: separate cg_update kernel; TRPO_COOP=0: the one-wave-per-tile
     kernel); FVP, CG and the policy gradient against the oracle."""
     import oracle
     from trpo_amd import synth
+    coop = "0" if mode == "off" else "1"
     monkeypatch.setenv("TRPO_COOP", coop)
+    monkeypatch.setenv("TRPO_COOP_FUSED", "0" if mode == "unfused" else "1")
     n = 2345
     th, obs = synth.make_theta(layers), synth.make_obs(n, layers[0])
     std = np.linspace(0.8, 1.1, layers[-1])

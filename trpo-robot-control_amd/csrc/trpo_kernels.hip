@@ -1053,7 +1053,10 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
 // once at the end.  Exchanges through LDS (double-buffered by tile parity, none when TH == 1):
 // y1/Ry1 after layer 0, the layer-2 partial products over the row tiles, and G2.
 // fp32 serves the wide policies (2x64: TH = 4); fp64 (v_mfma_f64_16x16x4_f64, every shape) is the
-// reference-exact precision mode.  MODE 0: FVP; MODE 1: policy gradient (as fvp_mlp3_kernel).
+// reference-exact precision mode.  MODE 0: FVP; MODE 1: policy gradient (as fvp_mlp3_kernel);
+// MODE 2: CG iteration -- the CG step j-1 -> j (src/TRPO_CG.c:65-103) from the reduced F p_{j-1},
+// run redundantly by every block (fixed-order sums: bit-identical in all blocks), p_j staged in
+// LDS and gathered into this wave's direction fragments, then FVP j.
 // The f64 MFMA's result layout differs from f32's: lane (c, g) register r holds row g + 4r
 // (f32: 4g + r), so the fp64 packs use that neuron <-> (g, s) permutation (PT<T>::neu).
 // ---------------------------------------------------------------------------
@@ -1147,6 +1150,9 @@ struct CoopCfg {
     static constexpr int COMB_V = (NG - 1) * TH * NW * 64; // group-combine dump (aliases exchange)
     static constexpr int MAIN_V = EX_V > COMB_V ? EX_V : COMB_V;
     static constexpr int LDS_BYTES = 4 * (int)sizeof(T) * MAIN_V + (int)sizeof(T) * WAVES * SCR;
+    static constexpr int MAIN_BYTES = 4 * (int)sizeof(T) * MAIN_V;   // the fused CG step stages p here
+    // parameter-count bound of the shapes this tiling serves (16 T0 -> 16 TH -> 16 TH -> 16)
+    static constexpr int PMAX = 256 * (T0 * TH + TH * TH + TH) + 16 * (2 * TH + 2);
     static_assert(TH == 1 || TH == 2 || TH == 4, "TH");
     static_assert(LDS_BYTES <= 160 * 1024, "LDS");
 };
@@ -1183,7 +1189,7 @@ fvp_coop_kernel(IterArgs A, Net net) {
     using Q = CoopCfg<T, T0, TH>;
     using C = FastCfg<T0, TH, TH, 1>;                      // pack offsets (same fragment packs)
     using V = typename PT<T>::V;
-    constexpr bool FV = MODE == 0;
+    constexpr bool FV = MODE != 1, UPD = MODE == 2;
     constexpr int T1 = TH, T2 = TH;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     T *ldsT = reinterpret_cast<T *>(lds);
@@ -1200,27 +1206,118 @@ fvp_coop_kernel(IterArgs A, Net net) {
     if (*A.skip) return;                                   // grid-uniform
 
     const V zero4 = {0, 0, 0, 0};
-    // this wave's weight fragments (theta and direction packs), straight to registers
+    // this wave's weight fragments (theta pack), straight to registers
     V fa0[T0], vfa0[T0], fa1[T1], vfa1[T1], fb1[T2];
 #pragma unroll
-    for (int kt = 0; kt < T0; ++kt) {
-        fa0[kt] = TP[C::FA0 / 4 + (w * T0 + kt) * 64 + lane];
-        vfa0[kt] = FV ? VP[C::VFA0 / 4 + (w * T0 + kt) * 64 + lane] : zero4;
-    }
+    for (int kt = 0; kt < T0; ++kt) fa0[kt] = TP[C::FA0 / 4 + (w * T0 + kt) * 64 + lane];
 #pragma unroll
     for (int kt = 0; kt < T1; ++kt) {
         fa1[kt] = TP[C::FA1 / 4 + (w * T1 + kt) * 64 + lane];
-        vfa1[kt] = FV ? VP[C::VFA1 / 4 + (w * T1 + kt) * 64 + lane] : zero4;
         fb1[kt] = TP[C::FB1 / 4 + (w * T2 + kt) * 64 + lane];
     }
     const V fa2 = TP[C::FA2 / 4 + w * 64 + lane];
-    const V vfa2 = FV ? VP[C::VFA2 / 4 + w * 64 + lane] : zero4;
     const V fb2 = TP[C::FB2 / 4 + w * 64 + lane];
     const V b0w = dvec<T>(TPs + C::BI0 + 16 * w, g), b1w = dvec<T>(TPs + C::BI1 + 16 * w, g);
     const V b2 = dvec<T>(TPs + C::BI2, g), iv = dvec<T>(TPs + C::IV, g);
-    const V vb0w = FV ? dvec<T>(VPs + C::VB0 + 16 * w, g) : zero4;
-    const V vb1w = FV ? dvec<T>(VPs + C::VB1 + 16 * w, g) : zero4;
-    const V vb2 = FV ? dvec<T>(VPs + C::VB2, g) : zero4;
+    V vfa2, vb0w, vb1w, vb2;
+    if constexpr (UPD) {
+        // ---- CG step j-1 -> j; z = F p_{j-1} arrives reduced (un-normalised) in acc_in ----
+        constexpr int EP = (Q::PMAX + Q::THREADS - 1) / Q::THREADS;
+        __shared__ double shc[96];                         // block_sums_dpp<1> | <2>, <= 8 waves
+        double *sp = reinterpret_cast<double *>(lds);      // p_j (aliases the tile exchange buffers)
+        const CgSt sin = *A.st_in;
+        const double cn = A.ctl->n_total, clam = A.ctl->damping, cth = A.ctl->resth;
+        const int cmax = A.ctl->maxiter;
+        const bool b0 = blockIdx.x == 0;
+        double pv[EP], rv[EP], zv[EP], xv[EP];
+#pragma unroll
+        for (int e = 0; e < EP; ++e) {                     // every load unconditional (clamped)
+            const int q = tid + e * Q::THREADS, qc = min(q, A.P - 1), qz = min(q, A.nw - 1);
+            const double p0 = A.p_in[qc], r0 = A.r_in[qc], x0 = A.x[b0 ? qc : 0], z0 = A.acc_in[qz];
+            const bool in = q < A.P;
+            pv[e] = in ? p0 : 0.0;
+            rv[e] = in ? r0 : 0.0;
+            xv[e] = (in && b0) ? x0 : 0.0;
+            zv[e] = q < A.nw ? z0 : 0.0;
+        }
+        double s1[1] = {0.0};
+#pragma unroll
+        for (int e = 0; e < EP; ++e) {                     // z = sum/N + lambda p; log-std block 2p + lambda p
+            const int q = tid + e * Q::THREADS;
+            zv[e] = (q < A.nw ? zv[e] / cn : 2.0 * pv[e]) + clam * pv[e];
+            s1[0] += pv[e] * zv[e];
+        }
+        block_sums_dpp<1>(s1, shc);
+        const double alpha = sin.rdotr / s1[0];
+        double s2[2] = {0.0, 0.0};
+#pragma unroll
+        for (int e = 0; e < EP; ++e) {
+            xv[e] += alpha * pv[e];
+            rv[e] -= alpha * zv[e];
+            s2[0] += rv[e] * rv[e];
+            s2[1] += xv[e] * xv[e];
+        }
+        block_sums_dpp<2>(s2, shc + 32);
+        const double nr = s2[0], beta = nr / sin.rdotr;
+#pragma unroll
+        for (int e = 0; e < EP; ++e) {
+            const int q = tid + e * Q::THREADS;
+            if (q < A.P) {
+                const double pn = rv[e] + beta * pv[e];
+                sp[q] = pn;
+                if (b0) {
+                    A.p_out[q] = pn;
+                    A.r_out[q] = rv[e];
+                    A.x[q] = xv[e];
+                }
+            }
+        }
+        const int it = sin.iter + 1;
+        const int done = (nr < cth || it >= cmax) ? 1 : 0;
+        if (b0 && tid == 0) {
+            A.st_out->rdotr = nr;
+            A.st_out->xx = s2[1];
+            A.st_out->iter = it;
+            A.hist[2 * it] = nr;
+            A.hist[2 * it + 1] = sqrt(s2[1]);
+            A.ctl->rdotr = nr;
+            A.ctl->iter = it;
+            A.ctl->done = done;
+        }
+        if (done) return;                                  // block-uniform
+        __syncthreads();
+        // this wave's direction fragments gathered from p_j (pack order -> parameter: vmap_at)
+        constexpr int Tc[4] = {T0, TH, TH, 1};
+        auto vget = [&](int e) -> T {
+            const int m = vmap_at(net, Tc, e, Q::F64);
+            return m >= 0 ? (T)sp[m] : (T)0;
+        };
+#pragma unroll
+        for (int kt = 0; kt < T0; ++kt)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) vfa0[kt][s] = vget(C::VFA0 + ((w * T0 + kt) * 64 + lane) * 4 + s);
+#pragma unroll
+        for (int kt = 0; kt < T1; ++kt)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) vfa1[kt][s] = vget(C::VFA1 + ((w * T1 + kt) * 64 + lane) * 4 + s);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            vfa2[s] = vget(C::VFA2 + (w * 64 + lane) * 4 + s);
+            vb0w[s] = vget(C::VB0 + 16 * w + PT<T>::neu(g, s));
+            vb1w[s] = vget(C::VB1 + 16 * w + PT<T>::neu(g, s));
+            vb2[s] = vget(C::VB2 + PT<T>::neu(g, s));
+        }
+        __syncthreads();                                   // LDS goes back to the tile exchanges
+    } else {
+#pragma unroll
+        for (int kt = 0; kt < T0; ++kt) vfa0[kt] = FV ? VP[C::VFA0 / 4 + (w * T0 + kt) * 64 + lane] : zero4;
+#pragma unroll
+        for (int kt = 0; kt < T1; ++kt) vfa1[kt] = FV ? VP[C::VFA1 / 4 + (w * T1 + kt) * 64 + lane] : zero4;
+        vfa2 = FV ? VP[C::VFA2 / 4 + w * 64 + lane] : zero4;
+        vb0w = FV ? dvec<T>(VPs + C::VB0 + 16 * w, g) : zero4;
+        vb1w = FV ? dvec<T>(VPs + C::VB1 + 16 * w, g) : zero4;
+        vb2 = FV ? dvec<T>(VPs + C::VB2, g) : zero4;
+    }
 
     const int a1 = ACT >= 0 ? (ACT & 3) : net.act[1];
     const int a2 = ACT >= 0 ? ((ACT >> 2) & 3) : net.act[2];
@@ -1796,19 +1893,22 @@ static hipError_t coop_attr(int lds) {
     hipError_t e = hipFuncSetAttribute((const void *)fvp_coop_kernel<T, T0, TH, ACT, 0>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
-    return hipFuncSetAttribute((const void *)fvp_coop_kernel<T, T0, TH, ACT, 1>,
+    e = hipFuncSetAttribute((const void *)fvp_coop_kernel<T, T0, TH, ACT, 1>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+    return hipFuncSetAttribute((const void *)fvp_coop_kernel<T, T0, TH, ACT, 2>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 }
 struct CoopEntry {
     int f64, T0, TH, act;
-    fast_launch_fn launch, launch_pg;
+    fast_launch_fn launch, launch_pg, launch_cg;   // MODE 0 FVP, 1 policy gradient, 2 CG iteration
     hipError_t (*attr)(int);
-    int lds, slab, ng, threads;
+    int lds, slab, ng, threads, main_bytes;
 };
 #define COOP_ENTRY(T, t0, th, act)                                                                                \
     {sizeof(T) == 8, t0, th, act, coop_launch<T, t0, th, act, 0>, coop_launch<T, t0, th, act, 1>,                \
-     coop_attr<T, t0, th, act>, CoopCfg<T, t0, th>::LDS_BYTES, CoopCfg<T, t0, th>::SLAB, CoopCfg<T, t0, th>::NG,  \
-     CoopCfg<T, t0, th>::THREADS}
+     coop_launch<T, t0, th, act, 2>, coop_attr<T, t0, th, act>, CoopCfg<T, t0, th>::LDS_BYTES,                    \
+     CoopCfg<T, t0, th>::SLAB, CoopCfg<T, t0, th>::NG, CoopCfg<T, t0, th>::THREADS, CoopCfg<T, t0, th>::MAIN_BYTES}
 #define COOP_SHAPE(T, t0, th) COOP_ENTRY(T, t0, th, ACT_TTL), COOP_ENTRY(T, t0, th, -1)
 static const CoopEntry kCoop[] = {
     COOP_SHAPE(float, 1, 2),  COOP_SHAPE(float, 1, 4),  COOP_SHAPE(float, 2, 2),  COOP_SHAPE(float, 2, 4),
@@ -1824,6 +1924,7 @@ struct trpo_dev {
     const FastEntry *fast;
     const CoopEntry *coop_e;    // cooperative kernel for wide hidden layers (else NULL)
     int coop;
+    int coop_fused;             // CG step fused into the cooperative FVP kernel (MODE 2)
     fast_launch_fn k_fvp, k_pg; // the tile kernel serving this shape, FVP and policy-gradient modes
     int k_lds, k_tiles;         // its dynamic LDS bytes and tiles per block per step
     Pack pack;
@@ -2051,6 +2152,8 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
             d->k_lds = d->coop_e->lds;
             d->k_tiles = d->coop_e->ng;
             d->slab = d->coop_e->slab;
+            const char *ef = getenv("TRPO_COOP_FUSED");
+            d->coop_fused = !(ef && atoi(ef) == 0) && (size_t)d->coop_e->main_bytes >= sizeof(double) * d->P;
             DMALLOC(d->imap, sizeof(int) * d->slab);
             hipLaunchKernelGGL(build_imap_coop_kernel, dim3(cdiv(d->slab, 256)), dim3(256), 0, d->stream, n, T[0],
                                T[1], d->f64, d->imap, d->slab);
@@ -2455,6 +2558,37 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
             const int in = (int)((M - 1) & 1), out = (int)(M & 1);
             CG_DISPATCH(E, cg_update_kernel, dim3(1), dim3(1024), 0, d->stream,
                         d->atomic ? acc_slot(d, M - 1) : d->zacc, d->atomic ? d->R : 1, d->pbuf[in], d->rbuf[in],
+                        d->pbuf[out], d->rbuf[out], x, d->P, d->nw, d->ctl, d->st + in, d->st + out, d->hist,
+                        (const int *)nullptr, (void *)nullptr, 0, 0);
+        }
+    } else if (d->coop_fused) {
+        // cooperative kernel: K_0 = FVP of p_0 (packed by cg_init); K_j (j >= 1) = CG step j-1 -> j
+        // fused with FVP j (MODE 2); each followed by the slab reduce [+ all-reduce]
+        for (long j = 0; j < M; ++j) {
+            IterArgs a = plain_args(d, done);
+            if (j > 0) {
+                const int in = (int)((j - 1) & 1), out = (int)(j & 1);
+                a.update = 1;
+                a.acc_in = d->zacc;
+                a.R_in = 1;
+                a.p_in = d->pbuf[in];
+                a.r_in = d->rbuf[in];
+                a.p_out = d->pbuf[out];
+                a.r_out = d->rbuf[out];
+                a.x = x;
+                a.st_in = d->st + in;
+                a.st_out = d->st + out;
+                a.ctl = d->ctl;
+                a.hist = d->hist;
+            }
+            (j > 0 ? d->coop_e->launch_cg : d->k_fvp)(dim3(d->grid), d->k_lds, d->stream, a, d->net);
+            launch_reduce(d, done);
+            int rc = allreduce(d, d->zacc, d->nw);
+            if (rc) return rc;
+        }
+        if (M > 0) {
+            const int in = (int)((M - 1) & 1), out = (int)(M & 1);
+            CG_DISPATCH(E, cg_update_kernel, dim3(1), dim3(1024), 0, d->stream, d->zacc, 1, d->pbuf[in], d->rbuf[in],
                         d->pbuf[out], d->rbuf[out], x, d->P, d->nw, d->ctl, d->st + in, d->st + out, d->hist,
                         (const int *)nullptr, (void *)nullptr, 0, 0);
         }
