@@ -71,6 +71,7 @@ struct IterArgs {
     int n, ntiles, P, nw;
     const float *tpack;
     const float *vpack;           // plain FVP: the packed direction
+    const double *v_nat;          // plain FVP: gather the direction from this natural-order vector instead
     float *slabs;                 // slab epilogue (acc_out == nullptr)
     double *acc_out;              // atomic epilogue: R_out fp64 replicas of the P-vector
     int R_out;
@@ -573,6 +574,13 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
         for (int k = 0; k < PER; ++k) {
             const int e = tid + k * C::THREADS;
             if (e < NT4 || (e < NALL && !upd)) dst[e] = st[k];
+        }
+    }
+    if (A.v_nat) {                                     // plain FVP of a natural-order direction
+        for (int ve = tid; ve < C::VLEN; ve += C::THREADS) {
+            const int m = vmap_at(net, Tc, ve);
+            const double v = A.v_nat[max(m, 0)];
+            vw[ve] = m >= 0 ? (float)v : 0.0f;
         }
     }
     STAMP(7);
@@ -1183,6 +1191,16 @@ __global__ void build_imap_coop_kernel(Net n, int T0, int TH, int p64, int *imap
     if (j < len) imap[j] = imap_coop_at(n, T0, TH, j, p64 != 0);
 }
 
+// direction-pack element e of the cooperative kernel's tile shape, from a natural-order vector
+// (pack arithmetic in registers: measured slightly faster than a table lookup round)
+template <typename T, int T0, int TH>
+__device__ __forceinline__ T coop_vgather(const Net &net, const double *src, int e) {
+    constexpr int Tc[4] = {T0, TH, TH, 1};
+    const int m = vmap_at(net, Tc, e, sizeof(T) == 8);
+    const double v = src[max(m, 0)];                   // unconditional load (no branch, no drain)
+    return m >= 0 ? (T)v : (T)0;
+}
+
 template <typename T, int T0, int TH, int ACT, int MODE>
 __global__ void __launch_bounds__((CoopCfg<T, T0, TH>::THREADS))
 fvp_coop_kernel(IterArgs A, Net net) {
@@ -1287,11 +1305,7 @@ fvp_coop_kernel(IterArgs A, Net net) {
         if (done) return;                                  // block-uniform
         __syncthreads();
         // this wave's direction fragments gathered from p_j (pack order -> parameter: vmap_at)
-        constexpr int Tc[4] = {T0, TH, TH, 1};
-        auto vget = [&](int e) -> T {
-            const int m = vmap_at(net, Tc, e, Q::F64);
-            return m >= 0 ? (T)sp[m] : (T)0;
-        };
+        auto vget = [&](int e) -> T { return coop_vgather<T, T0, TH>(net, sp, e); };
 #pragma unroll
         for (int kt = 0; kt < T0; ++kt)
 #pragma unroll
@@ -1308,6 +1322,23 @@ fvp_coop_kernel(IterArgs A, Net net) {
             vb2[s] = vget(C::VB2 + PT<T>::neu(g, s));
         }
         __syncthreads();                                   // LDS goes back to the tile exchanges
+    } else if (FV && A.v_nat) {                            // plain FVP of a natural-order direction
+        auto vget = [&](int e) -> T { return coop_vgather<T, T0, TH>(net, A.v_nat, e); };
+#pragma unroll
+        for (int kt = 0; kt < T0; ++kt)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) vfa0[kt][s] = vget(C::VFA0 + ((w * T0 + kt) * 64 + lane) * 4 + s);
+#pragma unroll
+        for (int kt = 0; kt < T1; ++kt)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) vfa1[kt][s] = vget(C::VFA1 + ((w * T1 + kt) * 64 + lane) * 4 + s);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            vfa2[s] = vget(C::VFA2 + (w * 64 + lane) * 4 + s);
+            vb0w[s] = vget(C::VB0 + 16 * w + PT<T>::neu(g, s));
+            vb1w[s] = vget(C::VB1 + 16 * w + PT<T>::neu(g, s));
+            vb2[s] = vget(C::VB2 + PT<T>::neu(g, s));
+        }
     } else {
 #pragma unroll
         for (int kt = 0; kt < T0; ++kt) vfa0[kt] = FV ? VP[C::VFA0 / 4 + (w * T0 + kt) * 64 + lane] : zero4;
@@ -1629,7 +1660,8 @@ constexpr int RS_POS = 32, RS_THREADS = 256;
 template <typename ST>
 __global__ void __launch_bounds__(RS_THREADS)
 reduce_slabs_kernel(const ST *__restrict__ slabs, int G, int slab, const int *__restrict__ imap,
-                    double *__restrict__ zacc, const int *__restrict__ skip) {
+                    double *__restrict__ zacc, const int *__restrict__ skip, const double *__restrict__ vin,
+                    double *__restrict__ zout, const Ctl *__restrict__ ctl, int nw, int P) {
     constexpr int VE = 16 / sizeof(ST), LP = RS_POS / VE, SG = RS_THREADS / LP, NLD = 256 / SG;
     typedef ST VT __attribute__((ext_vector_type(VE)));
     __shared__ double part[SG][RS_POS + 1];
@@ -1659,7 +1691,12 @@ reduce_slabs_kernel(const ST *__restrict__ slabs, int G, int slab, const int *__
         double a = 0.0;
 #pragma unroll 8
         for (int k = 0; k < SG; ++k) a += part[k][t];
-        zacc[m] = a;
+        if (zout) zout[m] = a / ctl->n_total + ctl->damping * vin[m];   // fused FVP epilogue
+        else zacc[m] = a;
+    }
+    if (zout && blockIdx.x == 0 && t < P - nw) {      // log-std block: 2 v + damping v
+        const double vq = vin[nw + t];
+        zout[nw + t] = 2.0 * vq + ctl->damping * vq;
     }
 }
 
@@ -2417,6 +2454,7 @@ static IterArgs plain_args(trpo_dev *d, const int *skip) {
     a.tpack = (const float *)d->tpack;      // fp64 mode: the kernel reinterprets (element type T)
     a.vpack = (const float *)d->vpack;
     a.slabs = (float *)d->slabs;
+    a.vmap = d->vmap;
     a.imap = d->imap;
     a.skip = skip;
     a.R_out = 1;
@@ -2424,14 +2462,17 @@ static IterArgs plain_args(trpo_dev *d, const int *skip) {
     return a;
 }
 
-// block partials (fp32, or fp64 in the fp64 mode) -> d->zacc, fixed order
-static void launch_reduce(trpo_dev *d, const int *skip) {
+// block partials (fp32, or fp64 in the fp64 mode) -> d->zacc, fixed order; with zout the FVP
+// epilogue (z = sum / N + damping v, log-std block 2 v + damping v) is applied on the way
+static void launch_reduce(trpo_dev *d, const int *skip, const double *vin = nullptr, double *zout = nullptr) {
     if (d->f64)
         hipLaunchKernelGGL(reduce_slabs_kernel<double>, dim3(d->slab / RS_POS), dim3(RS_THREADS), 0, d->stream,
-                           (const double *)d->slabs, d->grid, d->slab, d->imap, d->zacc, skip);
+                           (const double *)d->slabs, d->grid, d->slab, d->imap, d->zacc, skip, vin, zout, d->ctl,
+                           d->nw, d->P);
     else
         hipLaunchKernelGGL(reduce_slabs_kernel<float>, dim3(d->slab / RS_POS), dim3(RS_THREADS), 0, d->stream,
-                           (const float *)d->slabs, d->grid, d->slab, d->imap, d->zacc, skip);
+                           (const float *)d->slabs, d->grid, d->slab, d->imap, d->zacc, skip, vin, zout, d->ctl,
+                           d->nw, d->P);
 }
 
 // enqueue: partial sums of F*src into d->zacc (global over ranks)
@@ -2460,6 +2501,16 @@ extern "C" int trpo_dev_fvp(trpo_dev *d) {
     if (!d) return -1;
     if (d->n_total <= 0) return -1;
     HCHK(hipSetDevice(d->device));
+    if (d->fast && !d->comm) {
+        // two launches: the tile kernel gathers its direction fragments from v itself, and the
+        // slab reduce applies the epilogue (with RCCL the epilogue must follow the all-reduce)
+        IterArgs a = plain_args(d, &d->ctl->zero);
+        a.v_nat = d->vec[TRPO_VEC_V];
+        d->k_fvp(dim3(d->grid), d->k_lds, d->stream, a, d->net);
+        launch_reduce(d, &d->ctl->zero, d->vec[TRPO_VEC_V], d->vec[TRPO_VEC_Z]);
+        HCHK(hipGetLastError());
+        return 0;
+    }
     if (d->fast)
         hipLaunchKernelGGL(gather_pack_kernel, dim3(cdiv(d->pack.vlen, 256)), dim3(256), 0, d->stream, d->vpack,
                            d->vec[TRPO_VEC_V], d->vmap, d->pack.vlen, d->f64);
