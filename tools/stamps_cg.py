@@ -12,8 +12,10 @@ L = trpo_amd.lib()
 L.trpo_dev_read_stamps.restype = C.c_int
 L.trpo_dev_read_stamps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 order = [0, 7, 8, 9, 10, 11, 12, 1, 13, 14, 2, 15, 3, 4, 5, 6]
-cfgs = [("arm", [15,16,16,3], 50000, g, r) for g in os.environ.get("GRIDS", "0").split(",") for r in os.environ.get("REPL", "8").split(",")]
-cfgs += [("2x64", [15,64,64,3], 50000, "0", "8")]
+NS = [int(x) for x in os.environ.get("NS", "50000").split(",")]
+cfgs = [("arm", [15,16,16,3], n, g, r) for n in NS for g in os.environ.get("GRIDS", "0").split(",") for r in os.environ.get("REPL", "8").split(",")]
+if os.environ.get("WIDE", "1") == "1":
+    cfgs += [("2x64", [15,64,64,3], 50000, "0", "8")]
 for name, layers, n, grid, repl in cfgs:
     os.environ["TRPO_REPLICAS"] = repl
     if grid != "0": os.environ["TRPO_FVP_BLOCKS"] = grid

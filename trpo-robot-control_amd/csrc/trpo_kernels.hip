@@ -306,6 +306,27 @@ __device__ __forceinline__ int imap_at(const Net &n, const int (&T)[4], int j) {
     return -1;
 }
 
+// natural weight/bias parameter q -> accumulator-order slab position (the inverse of imap_at),
+// or -1 for LogStd / out of range.  Lets the epilogue issue its cross-block atomics in natural
+// order: contiguous, fully populated wave instructions instead of the sparse accumulator rows.
+__device__ __forceinline__ int islot_at(const Net &n, const int (&T)[4], int q) {
+    int kw[3], kb[3], k = 0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { kw[i] = k; k += T[i] * T[i + 1]; }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { kb[i] = k; k += T[i + 1]; }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int lo = n.L[i + 1], w = q - n.woff[i], b = q - n.boff[i];
+        if (w >= 0 && w < n.L[i] * lo) {
+            const int a = w / lo, o = w - a * lo;
+            return (kw[i] + (a >> 4) * T[i + 1] + (o >> 4)) * 256 + (((a & 15) >> 2) * 16 + (o & 15)) * 4 + (a & 3);
+        }
+        if (b >= 0 && b < lo) return (kb[i] + (b >> 4)) * 256 + ((b & 15) >> 2) * 64 + (b & 3);
+    }
+    return -1;
+}
+
 __global__ void build_maps_kernel(Net n, Pack pk, int *tmap, int *vmap, int p64) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e < pk.tlen) {
@@ -393,6 +414,15 @@ __device__ unsigned long long g_stamps[1024 * 32];
 // ---------------------------------------------------------------------------
 // The fused FVP kernel, 3 weight layers (NumLayers == 4), MFMA path.
 // ---------------------------------------------------------------------------
+#ifndef TRPO_TILE_ILV
+#define TRPO_TILE_ILV 0      // 1: tile t -> block t % grid (waves of a block spread over the sample range)
+#endif
+#ifndef TRPO_NAT_ATOMICS
+#define TRPO_NAT_ATOMICS 1  // cross-block fp64 atomics in natural parameter order
+#endif
+#ifndef TRPO_PF_PIN
+#define TRPO_PF_PIN 1       // pin the next-tile observation prefetch to the top of the tile loop
+#endif
 constexpr int SCR_LD = 20;            // scratch row stride (floats): conflict-free b32 writes
 
 template <int T0, int T1, int T2, int T3>
@@ -521,7 +551,11 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
             st[k] = e < NT4 ? tp4[e] : vp4[e - NT4];
         }
     }
+#if TRPO_TILE_ILV
+    int tile = wave * gridDim.x + blockIdx.x;
+#else
     int tile = blockIdx.x * C::WAVES + wave;
+#endif
     f4 xn[T0];
     {
         const int tl = max(0, min(tile, ntiles - 1));
@@ -719,6 +753,11 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
             const int tn = min(tile + NT * nwaves, ntiles - 1);
 #pragma unroll
             for (int kt = 0; kt < T0; ++kt) xn[kt] = obs4[(long)(tn * 16 + c) * (4 * T0) + kt * 4 + g];
+#if TRPO_PF_PIN
+            // keep the prefetch at the top of the trip: left to itself the scheduler sinks it to
+            // the loop latch, where the x0 = xn copy then waits out a full memory round trip
+            __builtin_amdgcn_sched_barrier(0);
+#endif
         }
 
         // ---- layer 0: x1 = W0^T x0 + b0 ; Rx1 = VW0^T x0 + vb0 (Ry0 = 0) ----
@@ -1007,6 +1046,35 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
         for (int a = 0; a < T3; ++a) acc[k++] = sB3[a];
     }
     f4 *red = reinterpret_cast<f4 *>(lds);
+#if TRPO_NAT_ATOMICS
+    if constexpr (C::RW == C::WAVES) {
+        if (A.acc_out) {
+            // all wave dumps fit at once: each thread sums its natural parameters straight from
+            // the dumps (fixed wave order, as below) and adds them with contiguous fp64 atomics
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < C::NACC / 4; ++k) red[wave * (C::SLAB / 4) + k * 64 + lane] = acc[k];
+            __syncthreads();
+            STAMP(5);
+            double *dst = A.acc_out + (long)(blockIdx.x % A.R_out) * A.P;
+#pragma unroll
+            for (int e = 0; e < C::EMAX; ++e) {
+                const int q = tid + e * C::THREADS;
+                if (q < A.nw) {
+                    const int j = islot_at(net, Tc, q);
+                    float t = 0.0f;
+#pragma unroll
+                    for (int w = 0; w < C::WAVES; ++w) t += lds[w * C::SLAB + j];
+                    unsafeAtomicAdd(dst + q, (double)t);
+                }
+            }
+            if (blockIdx.x == 0)
+                for (int e = tid; e < A.zero_len; e += C::THREADS) A.acc_zero[e] = 0.0;
+            STAMP(6);
+            return;
+        }
+    }
+#endif
     f4 part[C::EPT];
 #pragma unroll
     for (int j = 0; j < C::EPT; ++j) part[j] = zero4;
@@ -1221,6 +1289,15 @@ fvp_coop_kernel(IterArgs A, Net net) {
     const V *VP = reinterpret_cast<const V *>(A.vpack);
     const T *TPs = reinterpret_cast<const T *>(A.tpack);
     const T *VPs = reinterpret_cast<const T *>(A.vpack);
+    // the first tile's observations are issued with the prologue loads; later tiles are
+    // prefetched one step ahead (clamped: every load unconditional)
+    const int gstride = gridDim.x * Q::NG;
+    V xn[T0];
+    {
+        const int tc0 = min(blockIdx.x * Q::NG + grp, ntiles - 1);
+#pragma unroll
+        for (int kt = 0; kt < T0; ++kt) xn[kt] = obs4[(long)(tc0 * 16 + c) * (4 * T0) + kt * 4 + g];
+    }
     if (*A.skip) return;                                   // grid-uniform
 
     const V zero4 = {0, 0, 0, 0};
@@ -1362,7 +1439,6 @@ fvp_coop_kernel(IterArgs A, Net net) {
     for (int k = 0; k < T1; ++k) accW1[k] = zero4;
 
     // every wave of the block runs the same number of tile steps (barriers inside)
-    const int gstride = gridDim.x * Q::NG;
     const int nsteps = (ntiles + gstride - 1) / gstride;
     for (int step = 0; step < nsteps; ++step) {
         const int tile = step * gstride + blockIdx.x * Q::NG + grp;
@@ -1374,7 +1450,15 @@ fvp_coop_kernel(IterArgs A, Net net) {
         V *gb = LV + Q::GB + ((par * Q::NG + grp) * TH) * 64;
         V x0[T0];
 #pragma unroll
-        for (int kt = 0; kt < T0; ++kt) x0[kt] = obs4[(long)(tc * 16 + c) * (4 * T0) + kt * 4 + g];
+        for (int kt = 0; kt < T0; ++kt) x0[kt] = xn[kt];
+        {
+            const int tn = min(tile + gstride, ntiles - 1);
+#pragma unroll
+            for (int kt = 0; kt < T0; ++kt) xn[kt] = obs4[(long)(tn * 16 + c) * (4 * T0) + kt * 4 + g];
+#if TRPO_PF_PIN
+            __builtin_amdgcn_sched_barrier(0);             // keep the prefetch here (see fvp_mlp3_kernel)
+#endif
+        }
 
         // ---- layer 0, row tile w ----
         V a = b0w, ra = vb0w;
