@@ -95,6 +95,9 @@ struct IterArgs {
     const float4 *pg_d4;
     const float *pg_adv;
     const float4 *pg_iv4;
+    // forward-activation cache [tile][T1 + T2 + T3][lane] f4 (the per-tile y1, y2, y3 in D-layout):
+    // MODE 0 writes it when non-null, MODE 2 reads it instead of recomputing the forward pass
+    float4 *yc;
 };
 
 // fixed-order block-wide fp64 sum (every thread gets the result)
@@ -216,13 +219,23 @@ __device__ __forceinline__ float act_r(int a, float y, float rx) {
     default: return rx;
     }
 }
+// tanh' = 1 - y^2 as ONE explicit fma: left to the compiler, whether the product is fused
+// depends on what else uses y*y, so the recomputing (MODE 0) and cached (MODE 2) kernels could
+// round it differently -- they must agree bit for bit
+__device__ __forceinline__ float dtanh(float y) { return __builtin_fmaf(-y, y, 1.0f); }
+__device__ __forceinline__ f4 dtanh4(f4 y) {
+    f4 d;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) d[r] = dtanh(y[r]);
+    return d;
+}
 __device__ __forceinline__ f4 act_fwd(int a, f4 x, f4 rx, f4 &ry) {
     f4 y;
     if (a == ACT_T) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             y[r] = tanh_fast(x[r]);
-            ry[r] = rx[r] * (1.0f - y[r] * y[r]);
+            ry[r] = rx[r] * dtanh(y[r]);
         }
     } else if (a == ACT_S) {
 #pragma unroll
@@ -246,6 +259,13 @@ __device__ __forceinline__ f4 act_bwd(int a, f4 y, f4 g) {
     return g;
 }
 __device__ __forceinline__ bool act_needs_y(int a) { return a == ACT_T || a == ACT_S; }
+// R{y} of four rows from R{x} and the (cached) forward value y
+__device__ __forceinline__ f4 act_r4(int a, f4 y, f4 rx) {
+    if (a == ACT_T) return rx * dtanh4(y);
+    if (a == ACT_S) return rx * y * (1.0f - y);
+    if (a == ACT_O) return 0.1f * rx;
+    return rx;
+}
 
 // ---------------------------------------------------------------------------
 // pack-slot -> natural-parameter maps (built once per context)
@@ -516,11 +536,20 @@ __device__ __forceinline__ f4 scr_get(const float *scr, int row0, int c, int g) 
 // MODE 0: Fisher-vector product (R-forward + Pearlmutter backward, optionally fused with the
 // CG step).  MODE 1: policy gradient of TRPO_Update (plain forward, output seed
 // Adv (Action - Mean) / sigma^2, the same backward and contractions; no R chains).
+// MODE 2: MODE 0 with the forward activations y1, y2 (y3) read from the cache a MODE 0 launch
+// wrote for the same theta and observations: theta is fixed across the FVPs of a CG solve, so
+// only the R chains (linear in v) are recomputed -- 40 instead of 48 MFMAs and no tanh per tile.
 template <int T0, int T1, int T2, int T3, int ACT, int MODE>
 __global__ void __launch_bounds__((64 * FastCfg<T0, T1, T2, T3>::WAVES))
 fvp_mlp3_kernel(IterArgs A, Net net) {
-    constexpr bool FV = MODE == 0;
+    constexpr bool FV = MODE != 1;
+    constexpr bool YC = MODE == 2;                  // forward activations from the cache
+    constexpr int NYC = T1 + T2 + T3;               // cached f4 per lane per tile
     using C = FastCfg<T0, T1, T2, T3>;
+    static_assert(!YC || C::NT == 1, "forward cache with one tile in flight");
+    // the cache only for the register-resident small nets: on the wide shapes its extra registers
+    // push the kernel into scratch spills (and those runs were not bitwise reproducible)
+    static_assert(!YC || C::REGW, "forward cache only for the small-net kernels");
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ double sh64[20 * C::WAVES];      // 5 DPP block sums, 4 rows per wave
     float *tw = lds;                                   // theta pack
@@ -557,10 +586,20 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
     int tile = blockIdx.x * C::WAVES + wave;
 #endif
     f4 xn[T0];
+    [[maybe_unused]] f4 yn[YC ? NYC : 1];
+    const f4 *yc4 = reinterpret_cast<const f4 *>(A.yc);
+    const int a3c = ACT >= 0 ? ((ACT >> 4) & 3) : net.act[3];
     {
         const int tl = max(0, min(tile, ntiles - 1));
 #pragma unroll
         for (int kt = 0; kt < T0; ++kt) xn[kt] = obs4[(long)(tl * 16 + c) * (4 * T0) + kt * 4 + g];
+        if constexpr (YC) {
+#pragma unroll
+            for (int k = 0; k < T1 + T2; ++k) yn[k] = yc4[((long)tl * NYC + k) * 64 + lane];
+            if (act_needs_y(a3c))
+#pragma unroll
+                for (int k = T1 + T2; k < NYC; ++k) yn[k] = yc4[((long)tl * NYC + k) * 64 + lane];
+        }
     }
     constexpr int Tc[4] = {T0, T1, T2, T3};
     // CG state for the fused update (src/TRPO_CG.c:77-103), loaded in the same round
@@ -691,6 +730,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
     const int a2 = ACT >= 0 ? ((ACT >> 2) & 3) : net.act[2];
     const int a3 = ACT >= 0 ? ((ACT >> 4) & 3) : net.act[3];
     const bool y3_needed = act_needs_y(a3);
+    f4 *ycs = (MODE == 0 && C::REGW) ? reinterpret_cast<f4 *>(A.yc) : nullptr;   // cache writer (MODE 0)
     const f4 *TW = reinterpret_cast<const f4 *>(tw);
     const f4 *VW = reinterpret_cast<const f4 *>(vw);
 
@@ -735,6 +775,11 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
     for (; tile < ntiles; tile += NT * nwaves) {
         // input tiles: lane holds features 16kt+4g..+3 of its sample (D-layout rows)
         f4 x0[NT][T0];
+        [[maybe_unused]] f4 ycur[YC ? NYC : 1];
+        if constexpr (YC) {
+#pragma unroll
+            for (int k = 0; k < NYC; ++k) ycur[k] = yn[k];
+        }
         bool live[NT];
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
@@ -753,6 +798,13 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
             const int tn = min(tile + NT * nwaves, ntiles - 1);
 #pragma unroll
             for (int kt = 0; kt < T0; ++kt) xn[kt] = obs4[(long)(tn * 16 + c) * (4 * T0) + kt * 4 + g];
+            if constexpr (YC) {
+#pragma unroll
+                for (int k = 0; k < T1 + T2; ++k) yn[k] = yc4[((long)tn * NYC + k) * 64 + lane];
+                if (y3_needed)
+#pragma unroll
+                    for (int k = T1 + T2; k < NYC; ++k) yn[k] = yc4[((long)tn * NYC + k) * 64 + lane];
+            }
 #if TRPO_PF_PIN
             // keep the prefetch at the top of the trip: left to itself the scheduler sinks it to
             // the loop latch, where the x0 = xn copy then waits out a full memory round trip
@@ -779,12 +831,18 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
                 for (int s = 0; s < 4; ++s)
 #pragma unroll
                     for (int t = 0; t < NT; ++t) {
-                        a[t] = MFMA(w[s], x0[t][kt][s], a[t]);
+                        if constexpr (!YC) a[t] = MFMA(w[s], x0[t][kt][s], a[t]);
                         if constexpr (FV) ra[t] = MFMA(u[s], x0[t][kt][s], ra[t]);
                     }
             }
+            if constexpr (YC) {
+                y1[0][ot] = ycur[ot];
+                r1[0][ot] = act_r4(a1, y1[0][ot], ra[0]);
+            } else {
 #pragma unroll
-            for (int t = 0; t < NT; ++t) y1[t][ot] = act_fwd(a1, a[t], ra[t], r1[t][ot]);
+                for (int t = 0; t < NT; ++t) y1[t][ot] = act_fwd(a1, a[t], ra[t], r1[t][ot]);
+                if (ycs) ycs[((long)tile * NYC + ot) * 64 + lane] = y1[0][ot];
+            }
         }
 #ifdef TRPO_STAMPS
         if (first_tile) {
@@ -812,15 +870,21 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
                 for (int s = 0; s < 4; ++s)
 #pragma unroll
                     for (int t = 0; t < NT; ++t) {
-                        a[t] = MFMA(w[s], y1[t][kt][s], a[t]);
+                        if constexpr (!YC) a[t] = MFMA(w[s], y1[t][kt][s], a[t]);
                         if constexpr (FV) {
                             ra[t] = MFMA(w[s], r1[t][kt][s], ra[t]);
                             rb[t] = MFMA(u[s], y1[t][kt][s], rb[t]);
                         }
                     }
             }
+            if constexpr (YC) {
+                y2[0][ot] = ycur[T1 + ot];
+                r2[0][ot] = act_r4(a2, y2[0][ot], ra[0] + rb[0]);
+            } else {
 #pragma unroll
-            for (int t = 0; t < NT; ++t) y2[t][ot] = act_fwd(a2, a[t], ra[t] + rb[t], r2[t][ot]);
+                for (int t = 0; t < NT; ++t) y2[t][ot] = act_fwd(a2, a[t], ra[t] + rb[t], r2[t][ot]);
+                if (ycs) ycs[((long)tile * NYC + T1 + ot) * 64 + lane] = y2[0][ot];
+            }
         }
 #ifdef TRPO_STAMPS
         if (first_tile) {
@@ -849,7 +913,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
                 for (int s = 0; s < 4; ++s)
 #pragma unroll
                     for (int t = 0; t < NT; ++t) {
-                        if (y3_needed) a[t] = MFMA(w[s], y2[t][kt][s], a[t]);
+                        if (!YC && y3_needed) a[t] = MFMA(w[s], y2[t][kt][s], a[t]);
                         if constexpr (FV) {
                             ra[t] = MFMA(w[s], r2[t][kt][s], ra[t]);
                             rb[t] = MFMA(u[s], y2[t][kt][s], rb[t]);
@@ -858,8 +922,14 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
             }
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
-                f4 r3, gg;
-                const f4 y3 = act_fwd(a3, a[t], ra[t] + rb[t], r3);
+                f4 r3, gg, y3;
+                if constexpr (YC) {
+                    y3 = y3_needed ? ycur[T1 + T2 + ot] : zero4;
+                    r3 = act_r4(a3, y3, ra[t] + rb[t]);
+                } else {
+                    y3 = act_fwd(a3, a[t], ra[t] + rb[t], r3);
+                    if (ycs && y3_needed) ycs[((long)tile * NYC + T1 + T2 + ot) * 64 + lane] = y3;
+                }
                 if constexpr (FV) {
                     gg = act_bwd(a3, y3, r3 * iv);
                 } else {
@@ -1977,8 +2047,20 @@ static hipError_t fast_attr(int lds) {
     hipError_t e = hipFuncSetAttribute((const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 0>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
+    if constexpr (FastCfg<T0, T1, T2, T3>::REGW) {
+        e = hipFuncSetAttribute((const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 2>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return e;
+    }
     return hipFuncSetAttribute((const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 1>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+}
+
+// MODE 2 (forward cache) exists for the register-resident small-net shapes only
+template <int T0, int T1, int T2, int T3, int ACT>
+static constexpr fast_launch_fn yc_launch() {
+    if constexpr (FastCfg<T0, T1, T2, T3>::REGW) return fast_launch<T0, T1, T2, T3, ACT, 2>;
+    else return nullptr;
 }
 
 struct FastEntry {
@@ -1986,6 +2068,7 @@ struct FastEntry {
     int act;                     // -1: run-time activations
     fast_launch_fn launch;
     fast_launch_fn launch_pg;    // MODE 1: policy gradient
+    fast_launch_fn launch_yc;    // MODE 2: FVP on the cached forward activations
     hipError_t (*attr)(int);
     int lds, tlen, vlen, slab, emax, waves;
 };
@@ -1993,7 +2076,7 @@ struct FastEntry {
 #define ACT_TTL (ACT_T | (ACT_T << 2) | (ACT_L << 4))
 #define FAST_ENTRY(a, b, c, d, act)                                                                               \
     {{a, b, c, d}, act, fast_launch<a, b, c, d, act, 0>, fast_launch<a, b, c, d, act, 1>,                         \
-     fast_attr<a, b, c, d, act>,                                                                                  \
+     yc_launch<a, b, c, d, act>(), fast_attr<a, b, c, d, act>,                                                    \
      FastCfg<a, b, c, d>::lds_bytes(), FastCfg<a, b, c, d>::TLEN, FastCfg<a, b, c, d>::VLEN,                      \
      FastCfg<a, b, c, d>::SLAB, FastCfg<a, b, c, d>::EMAX, FastCfg<a, b, c, d>::WAVES}
 #define FAST_SHAPE(a, b, c, d) FAST_ENTRY(a, b, c, d, ACT_TTL), FAST_ENTRY(a, b, c, d, -1)
@@ -2056,6 +2139,11 @@ struct trpo_dev {
     int *imap;                  // slab position -> natural parameter (reduce kernel)
     int slab;                   // floats per block partial
     void *obs4;
+    // forward-activation cache of the one-wave-per-tile kernel (MODE 0 writes, MODE 2 reads):
+    // f4 [ntiles][T1 + T2 + T3][64]; valid for the current theta / observations when yc_valid
+    void *yc;
+    size_t yc_cap;              // bytes
+    int yc_on, yc_valid;
     // generic path
     float *th32, *v32, *iv32, *obs32, *scratch;
     int srows;
@@ -2283,6 +2371,10 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
             hipLaunchKernelGGL(build_imap_kernel, dim3(cdiv(d->slab, 256)), dim3(256), 0, d->stream, n, pk, d->imap,
                                d->slab);
         }
+        {
+            const char *ey = getenv("TRPO_YCACHE");
+            d->yc_on = d->fast->launch_yc && !d->coop && !d->f64 && !(ey && atoi(ey) == 0);
+        }
         snprintf(d->name, sizeof d->name, "mfma-mlp3 %dx%dx%dx%d%s%s%s", T[0], T[1], T[2], T[3],
                  d->fast->act >= 0 ? " ttl" : "", d->coop ? " coop" : "", d->f64 ? " fp64" : "");
     } else {
@@ -2318,7 +2410,7 @@ extern "C" void trpo_dev_destroy(trpo_dev *d) {
     if (d->cg_exec) hipGraphExecDestroy(d->cg_exec);
     if (d->comm) ncclCommDestroy(d->comm);
     trpo_update_state_free(d->upd);
-    void *ptrs[] = {d->obs64, d->pg_d, d->pg_adv, d->pg_iv, d->st, d->pbuf[0], d->pbuf[1], d->rbuf[0], d->rbuf[1], d->accbuf, d->imap, d->tpack, d->vpack, d->tmap, d->vmap, d->obs4, d->th32, d->v32, d->iv32, d->obs32, d->scratch,
+    void *ptrs[] = {d->obs64, d->pg_d, d->pg_adv, d->pg_iv, d->st, d->pbuf[0], d->pbuf[1], d->rbuf[0], d->rbuf[1], d->accbuf, d->imap, d->tpack, d->vpack, d->tmap, d->vmap, d->obs4, d->yc, d->th32, d->v32, d->iv32, d->obs32, d->scratch,
                     d->theta64, d->std64, d->r, d->zacc, d->slabs, d->ctl, d->hist};
     for (void *p : ptrs)
         if (p) hipFree(p);
@@ -2349,6 +2441,7 @@ extern "C" int trpo_dev_set_theta(trpo_dev *d, const double *theta) {
     if (!d || !theta) return -1;
     HCHK(hipSetDevice(d->device));
     HCHK(hipMemcpyAsync(d->theta64, theta, sizeof(double) * d->P, hipMemcpyHostToDevice, d->stream));
+    d->yc_valid = 0;
     if (d->fast) {
         hipLaunchKernelGGL(gather_pack_kernel, dim3(cdiv(d->pack.iv, 256)), dim3(256), 0, d->stream, d->tpack,
                            d->theta64, d->tmap, d->pack.iv, d->f64);
@@ -2434,6 +2527,18 @@ extern "C" int trpo_dev_set_obs(trpo_dev *d, const double *obs, size_t n) {
         if (n)
             hipLaunchKernelGGL(obs_pad_kernel, dim3(cdiv((long)npad * ld, 256)), dim3(256), 0, d->stream,
                                d->obs4, tmp, (int)n, (int)npad, L0, ld, d->f64);
+        d->yc_valid = 0;
+        if (d->yc_on) {
+            const int *T = d->pack.T;
+            const size_t bytes = (size_t)(npad / 16) * (T[1] + T[2] + T[3]) * 64 * 16;
+            if (bytes > d->yc_cap) {
+                if (d->yc) hipFree(d->yc);
+                d->yc = NULL;
+                d->yc_cap = 0;
+                HCHK(hipMalloc(&d->yc, bytes));
+                d->yc_cap = bytes;
+            }
+        }
     } else {
         if ((size_t)n * L0 > d->npad_cap) {
             if (d->obs32) hipFree(d->obs32);
@@ -2559,13 +2664,26 @@ static void launch_reduce(trpo_dev *d, const int *skip, const double *vin = null
                            d->nw, d->P);
 }
 
+// a standalone (never skipped) tile-kernel FVP: the first one after theta / the observations
+// changed writes the forward-activation cache (MODE 0), later ones read it (MODE 2)
+static void launch_fvp_plain(trpo_dev *d, IterArgs &a) {
+    if (d->yc_on) {
+        a.yc = reinterpret_cast<float4 *>(d->yc);
+        (d->yc_valid ? d->fast->launch_yc : d->k_fvp)(dim3(d->grid), d->k_lds, d->stream, a, d->net);
+        d->yc_valid = 1;
+    } else {
+        d->k_fvp(dim3(d->grid), d->k_lds, d->stream, a, d->net);
+    }
+}
+
 // enqueue: partial sums of F*src into d->zacc (global over ranks)
 static int enqueue_fvp_core(trpo_dev *d, const double *src, const int *skip) {
     const Net &n = d->net;
     if (d->fast) {
         // src has already been packed into d->vpack (by the caller or the CG kernels)
         IterArgs a = plain_args(d, skip);
-        d->k_fvp(dim3(d->grid), d->k_lds, d->stream, a, n);
+        if (skip == &d->ctl->zero) launch_fvp_plain(d, a);
+        else d->k_fvp(dim3(d->grid), d->k_lds, d->stream, a, n);
         HCHK(hipGetLastError());
     } else {
         hipLaunchKernelGGL(to_f32_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, d->v32, src, d->P);
@@ -2590,7 +2708,7 @@ extern "C" int trpo_dev_fvp(trpo_dev *d) {
         // slab reduce applies the epilogue (with RCCL the epilogue must follow the all-reduce)
         IterArgs a = plain_args(d, &d->ctl->zero);
         a.v_nat = d->vec[TRPO_VEC_V];
-        d->k_fvp(dim3(d->grid), d->k_lds, d->stream, a, d->net);
+        launch_fvp_plain(d, a);
         launch_reduce(d, &d->ctl->zero, d->vec[TRPO_VEC_V], d->vec[TRPO_VEC_Z]);
         HCHK(hipGetLastError());
         return 0;
@@ -2611,7 +2729,7 @@ extern "C" int trpo_dev_fvp_kernel(trpo_dev *d) {
     HCHK(hipSetDevice(d->device));
     if (d->fast) {
         IterArgs a = plain_args(d, &d->ctl->zero);
-        d->k_fvp(dim3(d->grid), d->k_lds, d->stream, a, d->net);
+        launch_fvp_plain(d, a);
     } else {
         hipLaunchKernelGGL(fvp_generic_kernel, dim3(d->grid), dim3(GEN_T), 0, d->stream, d->obs32, (int)d->n,
                            d->th32, d->v32, d->iv32, d->scratch, d->srows, (float *)d->slabs, d->slab, d->net,
@@ -2679,7 +2797,9 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
                 a.hist = d->hist;
                 a.vmap = d->vmap;
             }
-            d->k_fvp(dim3(d->grid), d->k_lds, d->stream, a, d->net);
+            // K_0 refreshes the forward-activation cache, K_1.. read it (theta is fixed in a solve)
+            if (d->yc_on) a.yc = reinterpret_cast<float4 *>(d->yc);
+            (j > 0 && d->yc_on ? d->fast->launch_yc : d->k_fvp)(dim3(d->grid), d->k_lds, d->stream, a, d->net);
             int rc;
             if (d->atomic) {
                 rc = allreduce(d, acc_slot(d, j), (size_t)RP);
