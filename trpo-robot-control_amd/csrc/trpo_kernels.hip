@@ -98,6 +98,12 @@ struct IterArgs {
     // forward-activation cache [tile][T1 + T2 + T3][lane] f4 (the per-tile y1, y2, y3 in D-layout):
     // MODE 0 writes it when non-null, MODE 2 reads it instead of recomputing the forward pass
     float4 *yc;
+    // CG start fused into the first FVP of a solve (init != 0, src/TRPO_CG.c:24-40): the direction
+    // is p0 = b (b_init, natural order); the last block writes x = 0, r = p = b, rdotr = b.b, the
+    // state and the control block (maxiter, resth, done) -- replaces a separate init launch
+    int init, init_maxiter;
+    double init_resth;
+    const double *b_init;
 };
 
 // fixed-order block-wide fp64 sum (every thread gets the result)
@@ -564,6 +570,8 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
 
     // ---- prologue: ONE round of global loads (flags, theta pack, [v pack | CG state], first tile) ----
     const bool upd = A.update != 0;
+    const bool ini = !upd && A.init != 0;
+    const bool vnat = !upd && !ini && A.v_nat != nullptr;   // plain FVP of a natural-order direction
     constexpr int NT4 = C::TLEN / 4, NALL = (C::TLEN + C::VLEN) / 4;
     constexpr int PER = (NALL + C::THREADS - 1) / C::THREADS;
     const int skipv = *A.skip;
@@ -639,6 +647,25 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
         }
 #pragma unroll
         for (int e = 0; e < C::VEMAX; ++e) vm[e] = vmap_at(net, Tc, tid + e * C::THREADS);
+    } else if (ini) {
+#pragma unroll
+        for (int e = 0; e < C::EMAX; ++e) {
+            const int q = tid + e * C::THREADS;
+            const double b0 = A.b_init[min(q, A.P - 1)];
+            pv[e] = q < A.P ? b0 : 0.0;
+        }
+#pragma unroll
+        for (int e = 0; e < C::VEMAX; ++e) vm[e] = vmap_at(net, Tc, tid + e * C::THREADS);
+    }
+    // plain FVP: the direction fragments gathered from v in the same load round
+    float vg[C::VEMAX];
+    if (vnat) {
+#pragma unroll
+        for (int e = 0; e < C::VEMAX; ++e) {
+            const int m = vmap_at(net, Tc, tid + e * C::THREADS);      // -1 past VLEN
+            const double v = A.v_nat[max(m, 0)];
+            vg[e] = m >= 0 ? (float)v : 0.0f;
+        }
     }
     if (skipv) return;                                 // grid-uniform
     {
@@ -646,17 +673,59 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
 #pragma unroll
         for (int k = 0; k < PER; ++k) {
             const int e = tid + k * C::THREADS;
-            if (e < NT4 || (e < NALL && !upd)) dst[e] = st[k];
+            if (e < NT4 || (e < NALL && !upd && !ini && !vnat)) dst[e] = st[k];
         }
     }
-    if (A.v_nat) {                                     // plain FVP of a natural-order direction
-        for (int ve = tid; ve < C::VLEN; ve += C::THREADS) {
-            const int m = vmap_at(net, Tc, ve);
-            const double v = A.v_nat[max(m, 0)];
-            vw[ve] = m >= 0 ? (float)v : 0.0f;
+    if (vnat) {
+#pragma unroll
+        for (int e = 0; e < C::VEMAX; ++e) {
+            const int ve = tid + e * C::THREADS;
+            if (ve < C::VLEN) vw[ve] = vg[e];
         }
     }
     STAMP(7);
+    if (ini) {
+        double *stage = reinterpret_cast<double *>(lds + C::TLEN + C::VLEN);
+#pragma unroll
+        for (int e = 0; e < C::EMAX; ++e) {
+            const int q = tid + e * C::THREADS;
+            if (q < A.P) stage[q] = pv[e];
+        }
+        if (blockIdx.x == gridDim.x - 1) {             // block-uniform; the block with the fewest tiles
+            double red[1] = {0.0};
+#pragma unroll
+            for (int e = 0; e < C::EMAX; ++e) red[0] += pv[e] * pv[e];
+            block_sums_dpp<1>(red, sh64);
+            const double rr = red[0];
+#pragma unroll
+            for (int e = 0; e < C::EMAX; ++e) {
+                const int q = tid + e * C::THREADS;
+                if (q < A.P) {
+                    A.p_out[q] = pv[e];
+                    A.r_out[q] = pv[e];
+                    A.x[q] = 0.0;
+                }
+            }
+            if (tid == 0) {
+                A.st_out->rdotr = rr;
+                A.st_out->xx = 0.0;
+                A.st_out->iter = 0;
+                A.hist[0] = rr;
+                A.hist[1] = 0.0;
+                A.ctl->maxiter = A.init_maxiter;
+                A.ctl->resth = A.init_resth;
+                A.ctl->rdotr = rr;
+                A.ctl->iter = 0;
+                A.ctl->done = (rr < A.init_resth || A.init_maxiter == 0) ? 1 : 0;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < C::VEMAX; ++e) {
+            const int ve = tid + e * C::THREADS;
+            if (ve < C::VLEN) vw[ve] = vm[e] >= 0 ? (float)stage[vm[e]] : 0.0f;
+        }
+    }
     if (upd) {
         // every block runs the identical fp64 CG step (fixed-order sums => bitwise-equal
         // results in all blocks); block 0 publishes the new state
@@ -1863,6 +1932,21 @@ __global__ void fvp_epilogue_kernel(const double *__restrict__ zacc, const doubl
     z[q] = (q < nw ? zacc[q] / ctl->n_total : 2.0 * vq) + ctl->damping * vq;
 }
 
+// the same epilogue from R atomic replicas of the un-normalised sum (fixed replica order)
+__global__ void acc_epilogue_kernel(const double *__restrict__ acc, int R, const double *__restrict__ v,
+                                    double *__restrict__ z, int P, int nw, const Ctl *__restrict__ ctl) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= P) return;
+    double a[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) a[r] = acc[(long)min(r, R - 1) * P + min(q, nw - 1)];
+    double s = a[0];
+#pragma unroll
+    for (int r = 1; r < 8; ++r) s += r < R ? a[r] : 0.0;
+    const double vq = v[q];
+    z[q] = (q < nw ? s / ctl->n_total : 2.0 * vq) + ctl->damping * vq;
+}
+
 // ---------------------------------------------------------------------------
 // CG (src/TRPO_CG.c:11-113), one 1024-thread block, all fp64, fixed-order sums
 // ---------------------------------------------------------------------------
@@ -1943,7 +2027,10 @@ __global__ void __launch_bounds__(1024)
 cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restrict__ p_in,
                  const double *__restrict__ r_in, double *p_out, double *r_out, double *x, int P, int nw, Ctl *ctl,
                  const CgSt *st_in, CgSt *st_out, double *hist,
-                 const int *__restrict__ vmap, void *vpack, int vlen, int f64) {
+                 const int *__restrict__ vmap, void *vpack, int vlen, int f64,
+                 double *acc_zero = nullptr, int zero_len = 0) {
+    // acc_zero: the atomic target of the NEXT solve's first FVP (which also runs the CG start),
+    // zeroed here once this step has consumed its input
     __shared__ double sh[64 + 128];                  // block_sums_dpp<1> and <2> regions (16 waves)
     const int done = ctl->done;
     const double n = ctl->n_total, lam = ctl->damping, th = ctl->resth;
@@ -1965,7 +2052,10 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
             if (k < R_in && q < nw) z += acc[(long)k * P + q];
         zv[e] = z;
     }
-    if (done) return;
+    if (done) {
+        for (int e = threadIdx.x; e < zero_len; e += 1024) acc_zero[e] = 0.0;   // inputs unused
+        return;
+    }
     double pz = 0.0;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
@@ -2015,6 +2105,8 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
         hist[2 * it + 1] = sqrt(xn);
         ctl->done = (nr < th || it >= maxiter) ? 1 : 0;
     }
+    // every thread's reads of acc were consumed before block_sums_dpp's barriers
+    for (int e = threadIdx.x; e < zero_len; e += 1024) acc_zero[e] = 0.0;
 }
 
 // ===========================================================================
@@ -2160,6 +2252,8 @@ struct trpo_dev {
     double *pbuf[2], *rbuf[2];  // ping-ponged CG direction / residual
     CgSt *st;                   // 2 ping-ponged CG scalar states
     double *accbuf;             // atomic mode: 3 x R fp64 replicas of the P-vector
+    double *pacc;               // atomic mode, standalone FVPs: 2 x R replicas, ping-ponged
+    int pacc_k;                 // the zeroed pacc set the next standalone FVP accumulates into
     int atomic, R;
     void *slabs;
     int slab_blocks;            // capacity
@@ -2306,6 +2400,7 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
         if (d->R > 8) d->R = 8;
     }
     DMALLOC(d->accbuf, sizeof(double) * 3 * d->R * d->P);
+    DMALLOC(d->pacc, sizeof(double) * 2 * d->R * d->P);
     if (d->fast) {
         Pack &pk = d->pack;
         for (int i = 0; i < 4; ++i) pk.T[i] = d->fast->T[i];
@@ -2410,7 +2505,7 @@ extern "C" void trpo_dev_destroy(trpo_dev *d) {
     if (d->cg_exec) hipGraphExecDestroy(d->cg_exec);
     if (d->comm) ncclCommDestroy(d->comm);
     trpo_update_state_free(d->upd);
-    void *ptrs[] = {d->obs64, d->pg_d, d->pg_adv, d->pg_iv, d->st, d->pbuf[0], d->pbuf[1], d->rbuf[0], d->rbuf[1], d->accbuf, d->imap, d->tpack, d->vpack, d->tmap, d->vmap, d->obs4, d->yc, d->th32, d->v32, d->iv32, d->obs32, d->scratch,
+    void *ptrs[] = {d->obs64, d->pg_d, d->pg_adv, d->pg_iv, d->st, d->pbuf[0], d->pbuf[1], d->rbuf[0], d->rbuf[1], d->accbuf, d->pacc, d->imap, d->tpack, d->vpack, d->tmap, d->vmap, d->obs4, d->yc, d->th32, d->v32, d->iv32, d->obs32, d->scratch,
                     d->theta64, d->std64, d->r, d->zacc, d->slabs, d->ctl, d->hist};
     for (void *p : ptrs)
         if (p) hipFree(p);
@@ -2666,7 +2761,22 @@ static void launch_reduce(trpo_dev *d, const int *skip, const double *vin = null
 
 // a standalone (never skipped) tile-kernel FVP: the first one after theta / the observations
 // changed writes the forward-activation cache (MODE 0), later ones read it (MODE 2)
-static void launch_fvp_plain(trpo_dev *d, IterArgs &a) {
+static int allreduce(trpo_dev *d, double *buf, size_t count);
+
+// Returns the atomic replica set it accumulated into (atomic mode) or NULL (block slabs).
+static double *launch_fvp_plain(trpo_dev *d, IterArgs &a) {
+    double *acc = NULL;
+    if (d->atomic) {
+        // fp64 atomics into R replicas, like the CG kernels (no slab round trip through HBM); block 0
+        // zeroes the other set for the next standalone FVP
+        const long RP = (long)d->R * d->P;
+        acc = d->pacc + (d->pacc_k & 1) * RP;
+        a.acc_out = acc;
+        a.R_out = d->R;
+        a.acc_zero = d->pacc + ((d->pacc_k + 1) & 1) * RP;
+        a.zero_len = (int)RP;
+        d->pacc_k ^= 1;
+    }
     if (d->yc_on) {
         a.yc = reinterpret_cast<float4 *>(d->yc);
         (d->yc_valid ? d->fast->launch_yc : d->k_fvp)(dim3(d->grid), d->k_lds, d->stream, a, d->net);
@@ -2674,6 +2784,7 @@ static void launch_fvp_plain(trpo_dev *d, IterArgs &a) {
     } else {
         d->k_fvp(dim3(d->grid), d->k_lds, d->stream, a, d->net);
     }
+    return acc;
 }
 
 // enqueue: partial sums of F*src into d->zacc (global over ranks)
@@ -2682,7 +2793,7 @@ static int enqueue_fvp_core(trpo_dev *d, const double *src, const int *skip) {
     if (d->fast) {
         // src has already been packed into d->vpack (by the caller or the CG kernels)
         IterArgs a = plain_args(d, skip);
-        if (skip == &d->ctl->zero) launch_fvp_plain(d, a);
+        if (skip == &d->ctl->zero && !d->atomic) launch_fvp_plain(d, a);
         else d->k_fvp(dim3(d->grid), d->k_lds, d->stream, a, n);
         HCHK(hipGetLastError());
     } else {
@@ -2703,13 +2814,19 @@ extern "C" int trpo_dev_fvp(trpo_dev *d) {
     if (!d) return -1;
     if (d->n_total <= 0) return -1;
     HCHK(hipSetDevice(d->device));
-    if (d->fast && !d->comm) {
-        // two launches: the tile kernel gathers its direction fragments from v itself, and the
-        // slab reduce applies the epilogue (with RCCL the epilogue must follow the all-reduce)
+    if (d->fast && (d->atomic || !d->comm)) {
+        // two launches: the tile kernel gathers its direction fragments from v itself, then the
+        // atomic-replica or slab reduce applies the epilogue (under RCCL after the all-reduce)
         IterArgs a = plain_args(d, &d->ctl->zero);
         a.v_nat = d->vec[TRPO_VEC_V];
-        launch_fvp_plain(d, a);
-        launch_reduce(d, &d->ctl->zero, d->vec[TRPO_VEC_V], d->vec[TRPO_VEC_Z]);
+        double *acc = launch_fvp_plain(d, a);
+        if (acc) {
+            if (allreduce(d, acc, (size_t)d->R * d->P)) return -4;
+            hipLaunchKernelGGL(acc_epilogue_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, acc, d->R,
+                               d->vec[TRPO_VEC_V], d->vec[TRPO_VEC_Z], d->P, d->nw, d->ctl);
+        } else {
+            launch_reduce(d, &d->ctl->zero, d->vec[TRPO_VEC_V], d->vec[TRPO_VEC_Z]);
+        }
         HCHK(hipGetLastError());
         return 0;
     }
@@ -2729,6 +2846,7 @@ extern "C" int trpo_dev_fvp_kernel(trpo_dev *d) {
     HCHK(hipSetDevice(d->device));
     if (d->fast) {
         IterArgs a = plain_args(d, &d->ctl->zero);
+        a.v_nat = d->vec[TRPO_VEC_V];                  // the same launch as the FVP call's
         launch_fvp_plain(d, a);
     } else {
         hipLaunchKernelGGL(fvp_generic_kernel, dim3(d->grid), dim3(GEN_T), 0, d->stream, d->obs32, (int)d->n,
@@ -2769,12 +2887,29 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
     const int *done = &d->ctl->done;
     const long M = (long)maxiter;
     const int RP = d->R * d->P;
-    CG_DISPATCH(E, cg_init_kernel, dim3(1), dim3(1024), shm, d->stream, b, x, d->rbuf[0], d->pbuf[0], d->P, d->ctl,
-                d->st, d->hist, (int)maxiter, resth, d->vmap, d->vpack, vlen, d->f64, d->atomic ? acc_slot(d, 0) : nullptr,
-                d->atomic ? RP : 0);
+    // the one-wave-per-tile kernel runs the CG start inside K_0 (IterArgs::init): no init launch.
+    // Its atomic target acc_slot(0) is zero on entry: zeroed at allocation and by every solve's
+    // final cg_update
+    const bool fused_init = d->fast && !d->coop && M > 0;
+    if (!fused_init)
+        CG_DISPATCH(E, cg_init_kernel, dim3(1), dim3(1024), shm, d->stream, b, x, d->rbuf[0], d->pbuf[0], d->P,
+                    d->ctl, d->st, d->hist, (int)maxiter, resth, d->vmap, d->vpack, vlen, d->f64,
+                    d->atomic ? acc_slot(d, 0) : nullptr, d->atomic ? RP : 0);
     if (d->fast && !d->coop) {
         for (long j = 0; j < M; ++j) {
-            IterArgs a = plain_args(d, done);
+            IterArgs a = plain_args(d, j == 0 ? &d->ctl->zero : done);
+            if (j == 0) {
+                a.init = 1;
+                a.b_init = b;
+                a.init_maxiter = (int)maxiter;
+                a.init_resth = resth;
+                a.p_out = d->pbuf[0];
+                a.r_out = d->rbuf[0];
+                a.x = x;
+                a.st_out = d->st;
+                a.ctl = d->ctl;
+                a.hist = d->hist;
+            }
             if (d->atomic) {
                 a.acc_out = acc_slot(d, j);
                 a.R_out = d->R;
@@ -2814,7 +2949,8 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
             CG_DISPATCH(E, cg_update_kernel, dim3(1), dim3(1024), 0, d->stream,
                         d->atomic ? acc_slot(d, M - 1) : d->zacc, d->atomic ? d->R : 1, d->pbuf[in], d->rbuf[in],
                         d->pbuf[out], d->rbuf[out], x, d->P, d->nw, d->ctl, d->st + in, d->st + out, d->hist,
-                        (const int *)nullptr, (void *)nullptr, 0, 0);
+                        (const int *)nullptr, (void *)nullptr, 0, 0, d->atomic ? acc_slot(d, 0) : nullptr,
+                        d->atomic ? RP : 0);
         }
     } else if (d->coop_fused) {
         // cooperative kernel: K_0 = FVP of p_0 (packed by cg_init); K_j (j >= 1) = CG step j-1 -> j
