@@ -274,7 +274,7 @@ def main():
     hbm_bound = bytes_alg / (PEAK_HBM_GBS * 1e9) >= flops / (PEAK_FP32_TFLOPS * 1e12)
 
     traffic = None
-    tpath = os.path.join(ROOT, "profiles", "r01_fvp_traffic.json")
+    tpath = os.environ.get("TRPO_TRAFFIC_JSON", os.path.join(ROOT, "profiles", "r01_fvp_traffic.json"))
     if os.path.exists(tpath) and dist.world == 1:
         # HBM bytes per launch of this kernel at this workload, from the committed rocprofv3 PMC passes
         traffic = json.load(open(tpath))["traffic_bytes"]

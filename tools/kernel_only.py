@@ -9,7 +9,7 @@ n = int(os.environ.get("N", "50000"))
 th = synth.make_theta(L); P = synth.num_params(L)
 with trpo_amd.Context(L, "lttl", th, synth.make_obs(n, L[0]), np.ones(L[-1])) as ctx:
     ctx.upload_v(synth.make_v(P))
-    ctx.enqueue_fvp()          # packs v
+    ctx.enqueue_fvp()          # first FVP: writes the forward-activation cache (MODE 0); the rest run MODE 2
     for _ in range(int(os.environ.get("REPS", "50"))):
         ctx.enqueue_fvp_kernel()
     ctx.synchronize()

@@ -545,11 +545,13 @@ __device__ __forceinline__ f4 scr_get(const float *scr, int row0, int c, int g) 
 // MODE 2: MODE 0 with the forward activations y1, y2 (y3) read from the cache a MODE 0 launch
 // wrote for the same theta and observations: theta is fixed across the FVPs of a CG solve, so
 // only the R chains (linear in v) are recomputed -- 40 instead of 48 MFMAs and no tanh per tile.
+// MODE 3: MODE 2 as launched inside the CG graph (K_1 ..): identical code under its own name, so a
+// kernel trace separates the standalone FVP kernel from the fused CG-iteration kernels.
 template <int T0, int T1, int T2, int T3, int ACT, int MODE>
 __global__ void __launch_bounds__((64 * FastCfg<T0, T1, T2, T3>::WAVES))
 fvp_mlp3_kernel(IterArgs A, Net net) {
     constexpr bool FV = MODE != 1;
-    constexpr bool YC = MODE == 2;                  // forward activations from the cache
+    constexpr bool YC = MODE == 2 || MODE == 3;     // forward activations from the cache
     constexpr int NYC = T1 + T2 + T3;               // cached f4 per lane per tile
     using C = FastCfg<T0, T1, T2, T3>;
     static_assert(!YC || C::NT == 1, "forward cache with one tile in flight");
@@ -2143,15 +2145,18 @@ static hipError_t fast_attr(int lds) {
         e = hipFuncSetAttribute((const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 2>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return e;
+        e = hipFuncSetAttribute((const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 3>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return e;
     }
     return hipFuncSetAttribute((const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 1>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 }
 
 // MODE 2 (forward cache) exists for the register-resident small-net shapes only
-template <int T0, int T1, int T2, int T3, int ACT>
+template <int T0, int T1, int T2, int T3, int ACT, int MODE>
 static constexpr fast_launch_fn yc_launch() {
-    if constexpr (FastCfg<T0, T1, T2, T3>::REGW) return fast_launch<T0, T1, T2, T3, ACT, 2>;
+    if constexpr (FastCfg<T0, T1, T2, T3>::REGW) return fast_launch<T0, T1, T2, T3, ACT, MODE>;
     else return nullptr;
 }
 
@@ -2161,6 +2166,7 @@ struct FastEntry {
     fast_launch_fn launch;
     fast_launch_fn launch_pg;    // MODE 1: policy gradient
     fast_launch_fn launch_yc;    // MODE 2: FVP on the cached forward activations
+    fast_launch_fn launch_yc_cg; // MODE 3: the same inside the CG graph
     hipError_t (*attr)(int);
     int lds, tlen, vlen, slab, emax, waves;
 };
@@ -2168,7 +2174,7 @@ struct FastEntry {
 #define ACT_TTL (ACT_T | (ACT_T << 2) | (ACT_L << 4))
 #define FAST_ENTRY(a, b, c, d, act)                                                                               \
     {{a, b, c, d}, act, fast_launch<a, b, c, d, act, 0>, fast_launch<a, b, c, d, act, 1>,                         \
-     yc_launch<a, b, c, d, act>(), fast_attr<a, b, c, d, act>,                                                    \
+     yc_launch<a, b, c, d, act, 2>(), yc_launch<a, b, c, d, act, 3>(), fast_attr<a, b, c, d, act>,                \
      FastCfg<a, b, c, d>::lds_bytes(), FastCfg<a, b, c, d>::TLEN, FastCfg<a, b, c, d>::VLEN,                      \
      FastCfg<a, b, c, d>::SLAB, FastCfg<a, b, c, d>::EMAX, FastCfg<a, b, c, d>::WAVES}
 #define FAST_SHAPE(a, b, c, d) FAST_ENTRY(a, b, c, d, ACT_TTL), FAST_ENTRY(a, b, c, d, -1)
@@ -2934,7 +2940,7 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
             }
             // K_0 refreshes the forward-activation cache, K_1.. read it (theta is fixed in a solve)
             if (d->yc_on) a.yc = reinterpret_cast<float4 *>(d->yc);
-            (j > 0 && d->yc_on ? d->fast->launch_yc : d->k_fvp)(dim3(d->grid), d->k_lds, d->stream, a, d->net);
+            (j > 0 && d->yc_on ? d->fast->launch_yc_cg : d->k_fvp)(dim3(d->grid), d->k_lds, d->stream, a, d->net);
             int rc;
             if (d->atomic) {
                 rc = allreduce(d, acc_slot(d, j), (size_t)RP);
