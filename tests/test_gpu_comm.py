@@ -11,6 +11,7 @@ import pytest
 
 import cases
 import trpo_amd
+from trpo_amd import synth
 
 pytestmark = pytest.mark.gpu
 
@@ -46,3 +47,22 @@ def test_one_rank_communicator_matches_plain_context(layers, precision):
     assert cases.rel_l2(x1, x0) <= 1e-12
     assert cases.rel_l2(r1["theta"], r0["theta"]) <= 1e-12
     assert r1["accepted"] == r0["accepted"]
+
+
+@pytest.mark.parametrize("used", ["1", "2", "5"])
+def test_fewer_replicas_same_result(used, monkeypatch):
+    """Under RCCL the CG uses fewer atomic replicas (sized from the largest shard) so the per-FVP
+    all-reduce stays small.  fp32 block partials are added into fp64 exactly, so the replica count
+    must not change the result: forced on one GPU, FVP and CG agree bit for bit."""
+    L = [15, 16, 16, 3]
+    P = synth.num_params(L)
+    th, obs = synth.make_theta(L), synth.make_obs(20000, 15)
+    v, b = synth.make_v(P), synth.make_b(P)
+    out = []
+    for env in (None, used):
+        if env:
+            monkeypatch.setenv("TRPO_REPLICAS_USED", env)
+        with trpo_amd.Context(L, "lttl", th, obs, np.ones(3), 0.1) as ctx:
+            out.append((ctx.fvp(v), ctx.fvp(v), ctx.cg(b, 10, 0.0)))
+    for a, c in zip(out[0], out[1]):
+        np.testing.assert_array_equal(a, c)

@@ -104,6 +104,7 @@ struct IterArgs {
     int init, init_maxiter;
     double init_resth;
     const double *b_init;
+    const int *pslot;             // natural parameter -> v-pack slot (pslot_at), -1 for LogStd
 };
 
 // fixed-order block-wide fp64 sum (every thread gets the result)
@@ -306,6 +307,25 @@ __device__ __forceinline__ int vmap_at(const Net &n, const int (&T)[4], int e, b
     return -1;
 }
 
+// natural weight / bias parameter q -> its v-pack slot (the inverse of vmap_at), or -1 for LogStd:
+// lets the CG step scatter p' from natural-order registers straight into the fragment LDS
+__device__ __forceinline__ int pslot_at(const Net &n, const int (&T)[4], int q) {
+    const int vfa[3] = {0, 256 * T[0] * T[1], 256 * (T[0] * T[1] + T[1] * T[2])};
+    const int vb0 = 256 * (T[0] * T[1] + T[1] * T[2] + T[2] * T[3]);
+    const int vb[3] = {vb0, vb0 + 16 * T[1], vb0 + 16 * (T[1] + T[2])};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const int lo = n.L[i + 1], w = q - n.woff[i], b = q - n.boff[i];
+        if (w >= 0 && w < n.L[i] * lo) {
+            const int a = w / lo, o = w - a * lo;          // W_i[a][o]: k-tile a >> 4, out-tile o >> 4
+            const int lane = (o & 15) + 16 * ((a & 15) >> 2);
+            return vfa[i] + (((o >> 4) * T[i] + (a >> 4)) * 64 + lane) * 4 + (a & 3);
+        }
+        if (b >= 0 && b < lo) return vb[i] + b;
+    }
+    return -1;
+}
+
 // accumulator-order slab position -> natural parameter (or -1): f4 k over
 // [W0 tiles (T0 x T1), W1 (T1 x T2), W2 (T2 x T3), B1 (T1), B2 (T2), B3 (T3)], then lane, r.
 __device__ __forceinline__ int imap_at(const Net &n, const int (&T)[4], int j) {
@@ -373,6 +393,12 @@ __global__ void build_maps_kernel(Net n, Pack pk, int *tmap, int *vmap, int p64)
 }
 
 // packs are fp32 or (f64 != 0) fp64
+__global__ void build_pslot_kernel(Net n, Pack pk, int *ps, int P) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    const int T[4] = {pk.T[0], pk.T[1], pk.T[2], pk.T[3]};
+    if (q < P) ps[q] = pslot_at(n, T, q);
+}
+
 __global__ void gather_pack_kernel(void *dst, const double *src, const int *map, int len, int f64) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e < len) {
@@ -614,7 +640,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
     constexpr int Tc[4] = {T0, T1, T2, T3};
     // CG state for the fused update (src/TRPO_CG.c:77-103), loaded in the same round
     double pv[C::EMAX], rv[C::EMAX], zv[C::EMAX], xv[C::EMAX];
-    int vm[C::VEMAX];
+    int vm[C::VEMAX], ps[C::EMAX];
     CgSt sin = {0.0, 0.0, 0, 0};
     double cn = 1.0, clam = 0.0, cth = 0.0;
     int cmax = 0;
@@ -649,6 +675,11 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
         }
 #pragma unroll
         for (int e = 0; e < C::VEMAX; ++e) vm[e] = vmap_at(net, Tc, tid + e * C::THREADS);
+#pragma unroll
+        for (int e = 0; e < C::EMAX; ++e) {
+            const int q = tid + e * C::THREADS, m = A.pslot[min(q, A.P - 1)];
+            ps[e] = q < A.P ? m : -1;
+        }
     } else if (ini) {
 #pragma unroll
         for (int e = 0; e < C::EMAX; ++e) {
@@ -658,6 +689,11 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
         }
 #pragma unroll
         for (int e = 0; e < C::VEMAX; ++e) vm[e] = vmap_at(net, Tc, tid + e * C::THREADS);
+#pragma unroll
+        for (int e = 0; e < C::EMAX; ++e) {
+            const int q = tid + e * C::THREADS, m = A.pslot[min(q, A.P - 1)];
+            ps[e] = q < A.P ? m : -1;
+        }
     }
     // plain FVP: the direction fragments gathered from v in the same load round
     float vg[C::VEMAX];
@@ -687,11 +723,13 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
     }
     STAMP(7);
     if (ini) {
-        double *stage = reinterpret_cast<double *>(lds + C::TLEN + C::VLEN);
 #pragma unroll
-        for (int e = 0; e < C::EMAX; ++e) {
-            const int q = tid + e * C::THREADS;
-            if (q < A.P) stage[q] = pv[e];
+        for (int e = 0; e < C::EMAX; ++e)
+            if (ps[e] >= 0) vw[ps[e]] = (float)pv[e];
+#pragma unroll
+        for (int e = 0; e < C::VEMAX; ++e) {
+            const int ve = tid + e * C::THREADS;
+            if (ve < C::VLEN && vm[e] < 0) vw[ve] = 0.0f;
         }
         if (blockIdx.x == gridDim.x - 1) {             // block-uniform; the block with the fewest tiles
             double red[1] = {0.0};
@@ -720,12 +758,6 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
                 A.ctl->iter = 0;
                 A.ctl->done = (rr < A.init_resth || A.init_maxiter == 0) ? 1 : 0;
             }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int e = 0; e < C::VEMAX; ++e) {
-            const int ve = tid + e * C::THREADS;
-            if (ve < C::VLEN) vw[ve] = vm[e] >= 0 ? (float)stage[vm[e]] : 0.0f;
         }
     }
     if (upd) {
@@ -757,18 +789,14 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
         const double xn2 = sin.xx + 2.0 * alpha * red[3] + alpha * alpha * red[4];
         STAMP(10);
         const double beta = nr / sin.rdotr;
-        double *stage = reinterpret_cast<double *>(lds + C::TLEN + C::VLEN);
 #pragma unroll
         for (int e = 0; e < C::EMAX; ++e) {
             const int q = tid + e * C::THREADS;
             pv[e] = rv[e] + beta * pv[e];
-            if (q < A.P) {
-                stage[q] = pv[e];
-                if (blockIdx.x == 0) {
-                    A.p_out[q] = pv[e];
-                    A.r_out[q] = rv[e];
-                    A.x[q] = xv[e];
-                }
+            if (q < A.P && blockIdx.x == 0) {
+                A.p_out[q] = pv[e];
+                A.r_out[q] = rv[e];
+                A.x[q] = xv[e];
             }
         }
         const int it = sin.iter + 1;
@@ -785,13 +813,17 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
         }
         if (done) return;                              // block-uniform (identical in every block)
         STAMP(11);
-        __syncthreads();
-        STAMP(12);
+        // p' straight into the fragment LDS: natural element q -> its pack slot (an LDS scatter),
+        // the padding slots zeroed by their owners -- disjoint writes, so no staging barrier
+#pragma unroll
+        for (int e = 0; e < C::EMAX; ++e)
+            if (ps[e] >= 0) vw[ps[e]] = (float)pv[e];
 #pragma unroll
         for (int e = 0; e < C::VEMAX; ++e) {
             const int ve = tid + e * C::THREADS;
-            if (ve < C::VLEN) vw[ve] = vm[e] >= 0 ? (float)stage[vm[e]] : 0.0f;
+            if (ve < C::VLEN && vm[e] < 0) vw[ve] = 0.0f;
         }
+        STAMP(12);
     }
     __syncthreads();
     STAMP(1);
@@ -2234,6 +2266,7 @@ struct trpo_dev {
     size_t esz;                 // pack / observation / slab element bytes (4 or 8)
     void *tpack, *vpack;
     int *tmap, *vmap;
+    int *pslot;                 // natural parameter -> v-pack slot (-1: LogStd)
     int *imap;                  // slab position -> natural parameter (reduce kernel)
     int slab;                   // floats per block partial
     void *obs4;
@@ -2261,6 +2294,8 @@ struct trpo_dev {
     double *pacc;               // atomic mode, standalone FVPs: 2 x R replicas, ping-ponged
     int pacc_k;                 // the zeroed pacc set the next standalone FVP accumulates into
     int atomic, R;
+    int Rc;                     // replicas in use: R on one GPU; under RCCL sized from the global shard
+                                // geometry (identical on every rank) to keep the all-reduce small
     void *slabs;
     int slab_blocks;            // capacity
     int grid;                   // FVP blocks for the current n
@@ -2407,6 +2442,7 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
     }
     DMALLOC(d->accbuf, sizeof(double) * 3 * d->R * d->P);
     DMALLOC(d->pacc, sizeof(double) * 2 * d->R * d->P);
+    d->Rc = d->R;
     if (d->fast) {
         Pack &pk = d->pack;
         for (int i = 0; i < 4; ++i) pk.T[i] = d->fast->T[i];
@@ -2436,6 +2472,8 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
         DMALLOC(d->vpack, d->esz * pk.vlen);
         DMALLOC(d->tmap, sizeof(int) * pk.tlen);
         DMALLOC(d->vmap, sizeof(int) * pk.vlen);
+        DMALLOC(d->pslot, sizeof(int) * d->P);
+        hipLaunchKernelGGL(build_pslot_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, n, pk, d->pslot, d->P);
         const int len = pk.tlen > pk.vlen ? pk.tlen : pk.vlen;
         hipLaunchKernelGGL(build_maps_kernel, dim3(cdiv(len, 256)), dim3(256), 0, d->stream, n, pk, d->tmap, d->vmap,
                            d->f64);
@@ -2511,7 +2549,7 @@ extern "C" void trpo_dev_destroy(trpo_dev *d) {
     if (d->cg_exec) hipGraphExecDestroy(d->cg_exec);
     if (d->comm) ncclCommDestroy(d->comm);
     trpo_update_state_free(d->upd);
-    void *ptrs[] = {d->obs64, d->pg_d, d->pg_adv, d->pg_iv, d->st, d->pbuf[0], d->pbuf[1], d->rbuf[0], d->rbuf[1], d->accbuf, d->pacc, d->imap, d->tpack, d->vpack, d->tmap, d->vmap, d->obs4, d->yc, d->th32, d->v32, d->iv32, d->obs32, d->scratch,
+    void *ptrs[] = {d->obs64, d->pg_d, d->pg_adv, d->pg_iv, d->st, d->pbuf[0], d->pbuf[1], d->rbuf[0], d->rbuf[1], d->accbuf, d->pacc, d->imap, d->tpack, d->vpack, d->tmap, d->vmap, d->pslot, d->obs4, d->yc, d->th32, d->v32, d->iv32, d->obs32, d->scratch,
                     d->theta64, d->std64, d->r, d->zacc, d->slabs, d->ctl, d->hist};
     for (void *p : ptrs)
         if (p) hipFree(p);
@@ -2671,6 +2709,40 @@ extern "C" int trpo_dev_set_obs(trpo_dev *d, const double *obs, size_t n) {
     return refresh_n_total(d);
 }
 
+// Replicas of the atomic partial sums in use.  One GPU: R (8; 32 block adds per address at 256
+// blocks measured best).  Under RCCL every rank all-reduces Rc x P values per FVP, so Rc is sized
+// for ~32 adds per address from the LARGEST shard's grid -- computed from global quantities only,
+// so it is identical on every rank (the collective's count must match).
+static int choose_replicas(trpo_dev *d) {
+    int rc = d->R;
+    if (d->world > 1 && d->fast) {
+        int cus = 256;
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, d->device) == hipSuccess && prop.multiProcessorCount > 0)
+            cus = prop.multiProcessorCount;
+        const long nmax = (long)ceil(d->n_total / d->world);
+        long g = cdiv(cdiv(nmax, 16), d->k_tiles);
+        if (g > cus) g = cus;
+        rc = (int)cdiv(g, 32);
+    }
+    const char *eu = getenv("TRPO_REPLICAS_USED");      // testing: force the multi-rank sizing on one GPU
+    if (eu && atoi(eu) > 0) rc = atoi(eu);
+    if (rc < 1) rc = 1;
+    if (rc > d->R) rc = d->R;
+    if (rc != d->Rc) {
+        // a different prefix of each replica set is used from now on: start from all-zero sets
+        HCHK(hipMemsetAsync(d->accbuf, 0, sizeof(double) * 3 * d->R * d->P, d->stream));
+        HCHK(hipMemsetAsync(d->pacc, 0, sizeof(double) * 2 * d->R * d->P, d->stream));
+        HCHK(hipStreamSynchronize(d->stream));
+        d->Rc = rc;
+        if (d->cg_exec) {
+            hipGraphExecDestroy(d->cg_exec);
+            d->cg_exec = NULL;
+        }
+    }
+    return 0;
+}
+
 // N is the global sample count: local n, or the all-reduced n under RCCL
 static int refresh_n_total(trpo_dev *d) {
     const size_t n = d->n;
@@ -2686,6 +2758,7 @@ static int refresh_n_total(trpo_dev *d) {
     } else {
         d->n_total = (double)n;
     }
+    if (choose_replicas(d)) return -2;
     return sync_ctl_scalars(d);
 }
 
@@ -2745,6 +2818,7 @@ static IterArgs plain_args(trpo_dev *d, const int *skip) {
     a.vpack = (const float *)d->vpack;
     a.slabs = (float *)d->slabs;
     a.vmap = d->vmap;
+    a.pslot = d->pslot;
     a.imap = d->imap;
     a.skip = skip;
     a.R_out = 1;
@@ -2775,11 +2849,11 @@ static double *launch_fvp_plain(trpo_dev *d, IterArgs &a) {
     if (d->atomic) {
         // fp64 atomics into R replicas, like the CG kernels (no slab round trip through HBM); block 0
         // zeroes the other set for the next standalone FVP
-        const long RP = (long)d->R * d->P;
-        acc = d->pacc + (d->pacc_k & 1) * RP;
+        const long RP = (long)d->Rc * d->P, stride = (long)d->R * d->P;
+        acc = d->pacc + (d->pacc_k & 1) * stride;
         a.acc_out = acc;
-        a.R_out = d->R;
-        a.acc_zero = d->pacc + ((d->pacc_k + 1) & 1) * RP;
+        a.R_out = d->Rc;
+        a.acc_zero = d->pacc + ((d->pacc_k + 1) & 1) * stride;
         a.zero_len = (int)RP;
         d->pacc_k ^= 1;
     }
@@ -2827,8 +2901,8 @@ extern "C" int trpo_dev_fvp(trpo_dev *d) {
         a.v_nat = d->vec[TRPO_VEC_V];
         double *acc = launch_fvp_plain(d, a);
         if (acc) {
-            if (allreduce(d, acc, (size_t)d->R * d->P)) return -4;
-            hipLaunchKernelGGL(acc_epilogue_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, acc, d->R,
+            if (allreduce(d, acc, (size_t)d->Rc * d->P)) return -4;
+            hipLaunchKernelGGL(acc_epilogue_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, acc, d->Rc,
                                d->vec[TRPO_VEC_V], d->vec[TRPO_VEC_Z], d->P, d->nw, d->ctl);
         } else {
             launch_reduce(d, &d->ctl->zero, d->vec[TRPO_VEC_V], d->vec[TRPO_VEC_Z]);
@@ -2892,7 +2966,7 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
     const size_t shm = d->fast ? sizeof(double) * d->P : 0;
     const int *done = &d->ctl->done;
     const long M = (long)maxiter;
-    const int RP = d->R * d->P;
+    const int RP = d->Rc * d->P;
     // the one-wave-per-tile kernel runs the CG start inside K_0 (IterArgs::init): no init launch.
     // Its atomic target acc_slot(0) is zero on entry: zeroed at allocation and by every solve's
     // final cg_update
@@ -2918,7 +2992,7 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
             }
             if (d->atomic) {
                 a.acc_out = acc_slot(d, j);
-                a.R_out = d->R;
+                a.R_out = d->Rc;
                 a.acc_zero = acc_slot(d, j + 1);
                 a.zero_len = RP;
             }
@@ -2926,7 +3000,7 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
                 const int in = (int)((j - 1) & 1), out = (int)(j & 1);
                 a.update = 1;
                 a.acc_in = d->atomic ? acc_slot(d, j - 1) : d->zacc;
-                a.R_in = d->atomic ? d->R : 1;
+                a.R_in = d->atomic ? d->Rc : 1;
                 a.p_in = d->pbuf[in];
                 a.r_in = d->rbuf[in];
                 a.p_out = d->pbuf[out];
@@ -2953,7 +3027,7 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
         if (M > 0) {
             const int in = (int)((M - 1) & 1), out = (int)(M & 1);
             CG_DISPATCH(E, cg_update_kernel, dim3(1), dim3(1024), 0, d->stream,
-                        d->atomic ? acc_slot(d, M - 1) : d->zacc, d->atomic ? d->R : 1, d->pbuf[in], d->rbuf[in],
+                        d->atomic ? acc_slot(d, M - 1) : d->zacc, d->atomic ? d->Rc : 1, d->pbuf[in], d->rbuf[in],
                         d->pbuf[out], d->rbuf[out], x, d->P, d->nw, d->ctl, d->st + in, d->st + out, d->hist,
                         (const int *)nullptr, (void *)nullptr, 0, 0, d->atomic ? acc_slot(d, 0) : nullptr,
                         d->atomic ? RP : 0);
