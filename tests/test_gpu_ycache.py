@@ -1,4 +1,4 @@
-"""MI355X: the forward-activation cache of the one-wave-per-tile kernel.
+"""MI355X: the forward-activation cache of the tile kernels (one-wave-per-tile and cooperative).
 
 Within a CG solve theta and the observations are fixed, so the first FVP (MODE 0) writes the
 per-tile forward activations y1, y2 (y3) and every later FVP (MODE 2) reads them and recomputes
@@ -124,3 +124,27 @@ def test_cache_invalidated_by_theta_and_obs():
         np.testing.assert_array_equal(x3, fresh.cg(b, 10, 0.0))
     zr, _ = oracle.fvp(L, "lttl", th2, obs2, std, v)
     assert cases.rel_l2(z3, zr) <= FVP_TOL
+
+
+@pytest.mark.parametrize("layers,acf,n", [([15, 64, 64, 3], "lttl", 4096), ([15, 32, 32, 3], "lttl", 3000),
+                                          ([15, 64, 64, 3], "lsso", 2000), ([15, 64, 64, 3], "lttt", 2000),
+                                          ([20, 64, 64, 3], "lttl", 1000)])
+def test_cooperative_kernel_cache(layers, acf, n, monkeypatch):
+    """The fp32 cooperative kernel (wide hidden layers) on the cache: MODE 3 (standalone FVP) and
+    MODE 4 (CG iteration) bit-identical to the recomputing kernel; tanh output (y3 needed) and the
+    T0 = 2, TH = 4 shape run without the cache and must be unaffected."""
+    P = synth.num_params(layers)
+    th, obs = synth.make_theta(layers), synth.make_obs(n, layers[0])
+    std = np.array([0.7, 1.0, 1.4])
+    v, b = synth.make_v(P), synth.make_b(P)
+
+    def run():
+        with trpo_amd.Context(layers, acf, th, obs, std, 0.1) as ctx:
+            assert "coop" in ctx.kernel_name
+            return [ctx.fvp(v), ctx.fvp(v), ctx.cg(b, 10, 0.0), ctx.cg(b, 10, 0.0)]
+
+    got, ref = _both(monkeypatch, run)
+    for a, r in zip(got, ref):
+        np.testing.assert_array_equal(a, r)
+    zr, _ = oracle.fvp(layers, acf, th, obs, std, v)
+    assert cases.rel_l2(got[1], zr) <= FVP_TOL

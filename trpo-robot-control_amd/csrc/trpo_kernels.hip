@@ -1333,6 +1333,8 @@ template <> struct PT<double> {
     static __device__ __forceinline__ double sg(double x) { return 1.0 / (1.0 + exp(-x)); }
 };
 
+__device__ __forceinline__ float fma_t(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+__device__ __forceinline__ double fma_t(double a, double b, double c) { return __builtin_fma(a, b, c); }
 template <typename T, typename V>
 __device__ __forceinline__ V actv_fwd(int a, V x, V rx, V &ry) {
     V y;
@@ -1340,7 +1342,7 @@ __device__ __forceinline__ V actv_fwd(int a, V x, V rx, V &ry) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             y[r] = PT<T>::th(x[r]);
-            ry[r] = rx[r] * ((T)1 - y[r] * y[r]);
+            ry[r] = rx[r] * fma_t(-y[r], y[r], (T)1);   // one rounding, as actv_r
         }
     } else if (a == ACT_S) {
 #pragma unroll
@@ -1356,6 +1358,23 @@ __device__ __forceinline__ V actv_fwd(int a, V x, V rx, V &ry) {
         ry = rx;
     }
     return y;
+}
+// R{y} from R{x} and a cached forward value y (the actv_fwd formulas)
+template <typename T, typename V>
+__device__ __forceinline__ V actv_r(int a, V y, V rx) {
+    V ry;
+    if (a == ACT_T) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ry[r] = rx[r] * fma_t(-y[r], y[r], (T)1);
+    } else if (a == ACT_S) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ry[r] = rx[r] * y[r] * ((T)1 - y[r]);
+    } else if (a == ACT_O) {
+        ry = (T)0.1 * rx;
+    } else {
+        ry = rx;
+    }
+    return ry;
 }
 template <typename T, typename V>
 __device__ __forceinline__ V actv_bwd(int a, V y, V g) {
@@ -1448,7 +1467,10 @@ fvp_coop_kernel(IterArgs A, Net net) {
     using Q = CoopCfg<T, T0, TH>;
     using C = FastCfg<T0, TH, TH, 1>;                      // pack offsets (same fragment packs)
     using V = typename PT<T>::V;
-    constexpr bool FV = MODE != 1, UPD = MODE == 2;
+    // MODE 3 / 4: MODE 0 / 2 on the forward-activation cache (fp32; output activation without y):
+    // a wave's y1, y2 row tiles come from the cache a MODE 0 launch wrote, the forward MFMAs are skipped
+    constexpr bool FV = MODE != 1, UPD = MODE == 2 || MODE == 4, YC = MODE == 3 || MODE == 4;
+    static_assert(!YC || !Q::F64, "forward cache: fp32 kernels only");
     constexpr int T1 = TH, T2 = TH;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     T *ldsT = reinterpret_cast<T *>(lds);
@@ -1466,10 +1488,17 @@ fvp_coop_kernel(IterArgs A, Net net) {
     // prefetched one step ahead (clamped: every load unconditional)
     const int gstride = gridDim.x * Q::NG;
     V xn[T0];
+    [[maybe_unused]] V yn1, yn2;                          // cached y1, y2 row tiles of the next tile
+    const V *ycl = reinterpret_cast<const V *>(A.yc);
+    V *ycs = (MODE == 0 && !Q::F64) ? reinterpret_cast<V *>(A.yc) : nullptr;   // cache writer
     {
         const int tc0 = min(blockIdx.x * Q::NG + grp, ntiles - 1);
 #pragma unroll
         for (int kt = 0; kt < T0; ++kt) xn[kt] = obs4[(long)(tc0 * 16 + c) * (4 * T0) + kt * 4 + g];
+        if constexpr (YC) {
+            yn1 = ycl[((long)tc0 * 2 * TH + w) * 64 + lane];
+            yn2 = ycl[((long)tc0 * 2 * TH + TH + w) * 64 + lane];
+        }
     }
     if (*A.skip) return;                                   // grid-uniform
 
@@ -1624,10 +1653,19 @@ fvp_coop_kernel(IterArgs A, Net net) {
         V x0[T0];
 #pragma unroll
         for (int kt = 0; kt < T0; ++kt) x0[kt] = xn[kt];
+        [[maybe_unused]] V yc1, yc2;
+        if constexpr (YC) {
+            yc1 = yn1;
+            yc2 = yn2;
+        }
         {
             const int tn = min(tile + gstride, ntiles - 1);
 #pragma unroll
             for (int kt = 0; kt < T0; ++kt) xn[kt] = obs4[(long)(tn * 16 + c) * (4 * T0) + kt * 4 + g];
+            if constexpr (YC) {
+                yn1 = ycl[((long)tn * 2 * TH + w) * 64 + lane];
+                yn2 = ycl[((long)tn * 2 * TH + TH + w) * 64 + lane];
+            }
 #if TRPO_PF_PIN
             __builtin_amdgcn_sched_barrier(0);             // keep the prefetch here (see fvp_mlp3_kernel)
 #endif
@@ -1639,11 +1677,17 @@ fvp_coop_kernel(IterArgs A, Net net) {
         for (int kt = 0; kt < T0; ++kt)
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
-                a = PT<T>::mfma(fa0[kt][s], x0[kt][s], a);
+                if constexpr (!YC) a = PT<T>::mfma(fa0[kt][s], x0[kt][s], a);
                 if constexpr (FV) ra = PT<T>::mfma(vfa0[kt][s], x0[kt][s], ra);
             }
-        V r1w;
-        const V y1w = actv_fwd<T>(a1, a, ra, r1w);
+        V r1w, y1w;
+        if constexpr (YC) {
+            y1w = yc1;
+            r1w = actv_r<T>(a1, y1w, ra);
+        } else {
+            y1w = actv_fwd<T>(a1, a, ra, r1w);
+            if (ycs && tile < ntiles) ycs[((long)tile * 2 * TH + w) * 64 + lane] = y1w;
+        }
         V y1[T1], r1[T1];
         if constexpr (Q::GW > 1) {
             xb[w * 128 + lane] = y1w;
@@ -1667,20 +1711,26 @@ fvp_coop_kernel(IterArgs A, Net net) {
         for (int kt = 0; kt < T1; ++kt)
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
-                a = PT<T>::mfma(fa1[kt][s], y1[kt][s], a);
+                if constexpr (!YC) a = PT<T>::mfma(fa1[kt][s], y1[kt][s], a);
                 if constexpr (FV) {
                     ra = PT<T>::mfma(fa1[kt][s], r1[kt][s], ra);
                     rb = PT<T>::mfma(vfa1[kt][s], y1[kt][s], rb);
                 }
             }
-        V r2w;
-        const V y2w = actv_fwd<T>(a2, a, ra + rb, r2w);
+        V r2w, y2w;
+        if constexpr (YC) {
+            y2w = yc2;
+            r2w = actv_r<T>(a2, y2w, ra + rb);
+        } else {
+            y2w = actv_fwd<T>(a2, a, ra + rb, r2w);
+            if (ycs && tile < ntiles) ycs[((long)tile * 2 * TH + TH + w) * 64 + lane] = y2w;
+        }
 
         // ---- layer 2: this wave's share (input row tile w), summed over the group ----
         V a3p = zero4, r3p = zero4, r3q = zero4;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-            if (y3_needed) a3p = PT<T>::mfma(fa2[s], y2w[s], a3p);
+            if (!YC && y3_needed) a3p = PT<T>::mfma(fa2[s], y2w[s], a3p);   // YC: y3 never needed
             if constexpr (FV) {
                 r3p = PT<T>::mfma(fa2[s], r2w[s], r3p);
                 r3q = PT<T>::mfma(vfa2[s], y2w[s], r3q);
@@ -2222,6 +2272,10 @@ static void coop_launch(dim3 g, int lds, hipStream_t st, const IterArgs &a, cons
     hipLaunchKernelGGL((fvp_coop_kernel<T, T0, TH, ACT, MODE>), g, dim3(CoopCfg<T, T0, TH>::THREADS), lds, st, a,
                        net);
 }
+template <typename T, int T0, int TH>
+struct CoopYC {
+    static constexpr bool ok = sizeof(T) == 4 && !(T0 == 2 && TH == 4);
+};
 template <typename T, int T0, int TH, int ACT>
 static hipError_t coop_attr(int lds) {
     hipError_t e = hipFuncSetAttribute((const void *)fvp_coop_kernel<T, T0, TH, ACT, 0>,
@@ -2230,18 +2284,35 @@ static hipError_t coop_attr(int lds) {
     e = hipFuncSetAttribute((const void *)fvp_coop_kernel<T, T0, TH, ACT, 1>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
+    if constexpr (CoopYC<T, T0, TH>::ok) {
+        e = hipFuncSetAttribute((const void *)fvp_coop_kernel<T, T0, TH, ACT, 3>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return e;
+        e = hipFuncSetAttribute((const void *)fvp_coop_kernel<T, T0, TH, ACT, 4>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return e;
+    }
     return hipFuncSetAttribute((const void *)fvp_coop_kernel<T, T0, TH, ACT, 2>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+}
+// MODE 3 / 4 (forward cache) exist for the fp32 kernels only, and not for T0 = 2, TH = 4, where the
+// cache registers push the CG-iteration kernel into scratch spills
+template <typename T, int T0, int TH, int ACT, int MODE>
+static constexpr fast_launch_fn coop_yc_launch() {
+    if constexpr (CoopYC<T, T0, TH>::ok) return coop_launch<T, T0, TH, ACT, MODE>;
+    else return nullptr;
 }
 struct CoopEntry {
     int f64, T0, TH, act;
     fast_launch_fn launch, launch_pg, launch_cg;   // MODE 0 FVP, 1 policy gradient, 2 CG iteration
+    fast_launch_fn launch_yc, launch_cg_yc;        // MODE 3 / 4: 0 / 2 on the forward cache (fp32)
     hipError_t (*attr)(int);
     int lds, slab, ng, threads, main_bytes;
 };
 #define COOP_ENTRY(T, t0, th, act)                                                                                \
     {sizeof(T) == 8, t0, th, act, coop_launch<T, t0, th, act, 0>, coop_launch<T, t0, th, act, 1>,                \
-     coop_launch<T, t0, th, act, 2>, coop_attr<T, t0, th, act>, CoopCfg<T, t0, th>::LDS_BYTES,                    \
+     coop_launch<T, t0, th, act, 2>, coop_yc_launch<T, t0, th, act, 3>(), coop_yc_launch<T, t0, th, act, 4>(),    \
+     coop_attr<T, t0, th, act>, CoopCfg<T, t0, th>::LDS_BYTES,                                                    \
      CoopCfg<T, t0, th>::SLAB, CoopCfg<T, t0, th>::NG, CoopCfg<T, t0, th>::THREADS, CoopCfg<T, t0, th>::MAIN_BYTES}
 #define COOP_SHAPE(T, t0, th) COOP_ENTRY(T, t0, th, ACT_TTL), COOP_ENTRY(T, t0, th, -1)
 static const CoopEntry kCoop[] = {
@@ -2260,6 +2331,7 @@ struct trpo_dev {
     int coop;
     int coop_fused;             // CG step fused into the cooperative FVP kernel (MODE 2)
     fast_launch_fn k_fvp, k_pg; // the tile kernel serving this shape, FVP and policy-gradient modes
+    fast_launch_fn k_fvp_yc, k_cg_yc;   // the same kernel on the forward cache: standalone FVP, CG iteration
     int k_lds, k_tiles;         // its dynamic LDS bytes and tiles per block per step
     Pack pack;
     int f64;                    // fp64 precision mode: fp64 packs/observations/slabs, fp64 MFMA kernel
@@ -2511,8 +2583,18 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
                                d->slab);
         }
         {
+            // forward cache: small-net one-wave kernel (MODE 2/3), or the fp32 cooperative kernel
+            // (MODE 3/4) when the output activation needs no y (its y3 is not cached)
             const char *ey = getenv("TRPO_YCACHE");
-            d->yc_on = d->fast->launch_yc && !d->coop && !d->f64 && !(ey && atoi(ey) == 0);
+            if (d->coop) {
+                d->k_fvp_yc = d->coop_e->launch_yc;
+                d->k_cg_yc = d->coop_e->launch_cg_yc;
+                if (n.act[3] == ACT_T || n.act[3] == ACT_S) d->k_fvp_yc = d->k_cg_yc = NULL;
+            } else {
+                d->k_fvp_yc = d->fast->launch_yc;
+                d->k_cg_yc = d->fast->launch_yc_cg;
+            }
+            d->yc_on = d->k_fvp_yc && d->k_cg_yc && !d->f64 && !(ey && atoi(ey) == 0);
         }
         snprintf(d->name, sizeof d->name, "mfma-mlp3 %dx%dx%dx%d%s%s%s", T[0], T[1], T[2], T[3],
                  d->fast->act >= 0 ? " ttl" : "", d->coop ? " coop" : "", d->f64 ? " fp64" : "");
@@ -2859,7 +2941,7 @@ static double *launch_fvp_plain(trpo_dev *d, IterArgs &a) {
     }
     if (d->yc_on) {
         a.yc = reinterpret_cast<float4 *>(d->yc);
-        (d->yc_valid ? d->fast->launch_yc : d->k_fvp)(dim3(d->grid), d->k_lds, d->stream, a, d->net);
+        (d->yc_valid ? d->k_fvp_yc : d->k_fvp)(dim3(d->grid), d->k_lds, d->stream, a, d->net);
         d->yc_valid = 1;
     } else {
         d->k_fvp(dim3(d->grid), d->k_lds, d->stream, a, d->net);
@@ -3014,7 +3096,7 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
             }
             // K_0 refreshes the forward-activation cache, K_1.. read it (theta is fixed in a solve)
             if (d->yc_on) a.yc = reinterpret_cast<float4 *>(d->yc);
-            (j > 0 && d->yc_on ? d->fast->launch_yc_cg : d->k_fvp)(dim3(d->grid), d->k_lds, d->stream, a, d->net);
+            (j > 0 && d->yc_on ? d->k_cg_yc : d->k_fvp)(dim3(d->grid), d->k_lds, d->stream, a, d->net);
             int rc;
             if (d->atomic) {
                 rc = allreduce(d, acc_slot(d, j), (size_t)RP);
@@ -3052,7 +3134,10 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
                 a.ctl = d->ctl;
                 a.hist = d->hist;
             }
-            (j > 0 ? d->coop_e->launch_cg : d->k_fvp)(dim3(d->grid), d->k_lds, d->stream, a, d->net);
+            // K_0 refreshes the forward-activation cache (fp32), K_1.. read it
+            if (d->yc_on) a.yc = reinterpret_cast<float4 *>(d->yc);
+            (j > 0 ? (d->yc_on ? d->k_cg_yc : d->coop_e->launch_cg) : d->k_fvp)(dim3(d->grid), d->k_lds, d->stream, a,
+                                                                             d->net);
             launch_reduce(d, done);
             int rc = allreduce(d, d->zacc, d->nw);
             if (rc) return rc;
