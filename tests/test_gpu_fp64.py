@@ -20,6 +20,7 @@ import pytest
 
 import cases
 import trpo_amd
+from trpo_amd import synth
 
 pytestmark = pytest.mark.gpu
 
@@ -140,3 +141,20 @@ def test_fp64_fused_and_unfused_cg_agree(name, monkeypatch):
             assert ctx.cg_history()[2] == c["iters"]
     assert cases.rel_l2(out["1"], out["0"]) <= 1e-9
     assert cases.rel_l2(out["1"], cases.expected(c)) <= CG_TOL
+
+
+@pytest.mark.parametrize("layers,n", [([15, 64, 64, 3], 3000), ([15, 32, 32, 3], 2000), ([15, 16, 16, 3], 2000)])
+def test_fp64_forward_cache_bitwise(layers, n, monkeypatch):
+    """fp64 mode on the forward-activation cache (cooperative kernel, TH > 1; TH = 1 runs without
+    it): repeated FVPs and CG solves bit-identical to TRPO_YCACHE=0."""
+    monkeypatch.setenv("TRPO_PRECISION", "fp64")
+    P = synth.num_params(layers)
+    th, obs = synth.make_theta(layers), synth.make_obs(n, layers[0])
+    v, b = synth.make_v(P), synth.make_b(P)
+    out = []
+    for yc in ("0", "1"):
+        monkeypatch.setenv("TRPO_YCACHE", yc)
+        with trpo_amd.Context(layers, "lttl", th, obs, np.ones(3), 0.1) as ctx:
+            out.append([ctx.fvp(v), ctx.fvp(v), ctx.cg(b, 10, 0.0), ctx.cg(b, 10, 0.0)])
+    for a, r in zip(out[1], out[0]):
+        np.testing.assert_array_equal(a, r)

@@ -1404,7 +1404,10 @@ __device__ __forceinline__ typename PT<T>::V dvec(const T *base, int g) {
 template <typename T, int T0, int TH>
 struct CoopCfg {
     static constexpr bool F64 = sizeof(T) == 8;
-    static constexpr int WAVES = (F64 && TH > 1) ? 4 : 8;   // fp64 exchanges are twice the bytes
+#ifndef TRPO_F64_TH1_WAVES
+#define TRPO_F64_TH1_WAVES 4      // one wave per SIMD: room for the forward cache without spills
+#endif
+    static constexpr int WAVES = F64 ? (TH > 1 ? 4 : TRPO_F64_TH1_WAVES) : 8;   // fp64 exchanges: twice the bytes
     static constexpr int GW = TH, NG = WAVES / GW, THREADS = 64 * WAVES;
     static constexpr int NW = T0 + TH + 4;                 // accumulator vectors per lane per wave
     static constexpr int SLAB = TH * NW * 256;             // T per block partial
@@ -1470,7 +1473,6 @@ fvp_coop_kernel(IterArgs A, Net net) {
     // MODE 3 / 4: MODE 0 / 2 on the forward-activation cache (fp32; output activation without y):
     // a wave's y1, y2 row tiles come from the cache a MODE 0 launch wrote, the forward MFMAs are skipped
     constexpr bool FV = MODE != 1, UPD = MODE == 2 || MODE == 4, YC = MODE == 3 || MODE == 4;
-    static_assert(!YC || !Q::F64, "forward cache: fp32 kernels only");
     constexpr int T1 = TH, T2 = TH;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     T *ldsT = reinterpret_cast<T *>(lds);
@@ -1490,7 +1492,7 @@ fvp_coop_kernel(IterArgs A, Net net) {
     V xn[T0];
     [[maybe_unused]] V yn1, yn2;                          // cached y1, y2 row tiles of the next tile
     const V *ycl = reinterpret_cast<const V *>(A.yc);
-    V *ycs = (MODE == 0 && !Q::F64) ? reinterpret_cast<V *>(A.yc) : nullptr;   // cache writer
+    V *ycs = MODE == 0 ? reinterpret_cast<V *>(A.yc) : nullptr;   // cache writer
     {
         const int tc0 = min(blockIdx.x * Q::NG + grp, ntiles - 1);
 #pragma unroll
@@ -2274,7 +2276,7 @@ static void coop_launch(dim3 g, int lds, hipStream_t st, const IterArgs &a, cons
 }
 template <typename T, int T0, int TH>
 struct CoopYC {
-    static constexpr bool ok = sizeof(T) == 4 && !(T0 == 2 && TH == 4);
+    static constexpr bool ok = sizeof(T) == 4 ? !(T0 == 2 && TH == 4) : (TH > 1 || TRPO_F64_TH1_WAVES <= 4);
 };
 template <typename T, int T0, int TH, int ACT>
 static hipError_t coop_attr(int lds) {
@@ -2295,8 +2297,8 @@ static hipError_t coop_attr(int lds) {
     return hipFuncSetAttribute((const void *)fvp_coop_kernel<T, T0, TH, ACT, 2>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 }
-// MODE 3 / 4 (forward cache) exist for the fp32 kernels only, and not for T0 = 2, TH = 4, where the
-// cache registers push the CG-iteration kernel into scratch spills
+// MODE 3 / 4 (forward cache): not where the cache registers push the kernel into scratch spills
+// (fp32 T0 = 2, TH = 4; fp64 TH = 1, whose 8-wave blocks cap a wave at 256 VGPRs)
 template <typename T, int T0, int TH, int ACT, int MODE>
 static constexpr fast_launch_fn coop_yc_launch() {
     if constexpr (CoopYC<T, T0, TH>::ok) return coop_launch<T, T0, TH, ACT, MODE>;
@@ -2594,7 +2596,7 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
                 d->k_fvp_yc = d->fast->launch_yc;
                 d->k_cg_yc = d->fast->launch_yc_cg;
             }
-            d->yc_on = d->k_fvp_yc && d->k_cg_yc && !d->f64 && !(ey && atoi(ey) == 0);
+            d->yc_on = d->k_fvp_yc && d->k_cg_yc && !(ey && atoi(ey) == 0);
         }
         snprintf(d->name, sizeof d->name, "mfma-mlp3 %dx%dx%dx%d%s%s%s", T[0], T[1], T[2], T[3],
                  d->fast->act >= 0 ? " ttl" : "", d->coop ? " coop" : "", d->f64 ? " fp64" : "");
@@ -2751,7 +2753,7 @@ extern "C" int trpo_dev_set_obs(trpo_dev *d, const double *obs, size_t n) {
         d->yc_valid = 0;
         if (d->yc_on) {
             const int *T = d->pack.T;
-            const size_t bytes = (size_t)(npad / 16) * (T[1] + T[2] + T[3]) * 64 * 16;
+            const size_t bytes = (size_t)(npad / 16) * (T[1] + T[2] + T[3]) * 64 * 4 * d->esz;
             if (bytes > d->yc_cap) {
                 if (d->yc) hipFree(d->yc);
                 d->yc = NULL;
