@@ -51,6 +51,8 @@ struct trpo_dev_view {
     double n_total;            // global samples (all ranks)
     double *vec_b;             // CG right-hand side slot (TRPO_VEC_B)
     double *vec_x, *vec_v, *vec_z;
+    const int *cg_iter;        // device: iterations of the last CG solve
+    const double *cg_hist;     // device: its (rdotr, |x|) history, 2 per iteration
 };
 void trpo_dev_get_view(trpo_dev *d, trpo_dev_view *v);
 // in-place fp64 sum over the attached RCCL communicator (no-op without one)
@@ -58,7 +60,9 @@ int trpo_dev_allreduce64(trpo_dev *d, double *buf, size_t count);
 // policy-gradient weight/bias sums (unnormalised, all ranks) by the MFMA tile kernel in MODE 1;
 // roll64 = [n][2A+1] Mean, Action, Adv.  *zacc receives the device vector (P - A entries).
 // Returns 1 when the shape has no tile kernel (caller uses the generic fp64 kernel).
-int trpo_dev_pg_sums_fast(trpo_dev *d, const double *roll64, const double **zacc);
+// roll_gen: the rollout's upload generation -- its fp32 (Action - Mean) / Adv rows are rebuilt only
+// when it changes.
+int trpo_dev_pg_sums_fast(trpo_dev *d, const double *roll64, unsigned roll_gen, const double **zacc);
 // per-context storage of the update path (owned by trpo_update.hip)
 void **trpo_dev_update_state(trpo_dev *d);
 void trpo_update_state_free(void *state);

@@ -50,9 +50,11 @@ int trpo_dev_set_rollout(trpo_dev *d, const double *mean, const double *action, 
 int trpo_dev_policy_gradient(trpo_dev *d, double *b_host, double *adv_sum);
 int trpo_dev_surrogate(trpo_dev *d, const double *fullstep, int k0, int nk, double *surr_host);
 /* The device phase of one update with ONE host synchronisation: policy gradient -> slot B,
- * CG(maxiter, resth) -> slot X, FVP(x) -> slot Z; then b, x, z and sum(Adv) to the host. */
+ * CG(maxiter, resth) -> slot X, FVP(x) -> slot Z; then b, x, z, sum(Adv), the CG iteration count and
+ * (optional, capacity maxiter + 1) its rdotr / |x| history to the host, written by one kernel into
+ * pinned host memory. */
 int trpo_dev_update_solve(trpo_dev *d, size_t maxiter, double resth, double *b, double *x, double *z,
-                          double *adv_sum);
+                          double *adv_sum, size_t *iters, double *rdotr_hist, double *xnorm_hist);
 
 /* Value-baseline objective (src/TRPO_Baseline.c), its own small device object. */
 typedef struct trpo_bdev trpo_bdev;

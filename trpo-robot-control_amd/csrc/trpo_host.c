@@ -213,19 +213,6 @@ int trpo_ctx_set_rollout(trpo_ctx *c, const double *mean, const double *action, 
     return rc;
 }
 
-static void print_cg_lines(trpo_ctx *c, size_t max_iter, size_t *iters_out) {
-    size_t iters = 0;
-    double *rr = (double *)malloc(sizeof(double) * (max_iter + 1));
-    double *xn = (double *)malloc(sizeof(double) * (max_iter + 1));
-    if (rr && xn && !trpo_dev_cg_history(c->dev, rr, xn, max_iter + 1, &iters)) {
-        for (size_t i = 0; i <= iters; ++i)
-            printf("CG Iter[%zu] Residual Norm=%.12e, Soln Norm=%.12e\n", i, rr[i], xn[i]);
-    }
-    if (iters_out) *iters_out = iters;
-    free(rr);
-    free(xn);
-}
-
 double trpo_ctx_update(trpo_ctx *c, size_t max_iter, double resth, double max_kl, int max_bt, double accept,
                        double *theta_out, double *b_out, double *x_out, trpo_update_info *info, int verbose) {
     if (!c || !theta_out || max_bt < 0 || max_bt > TRPO_MAX_BACKTRACKS || !(max_kl > 0)) return TRPO_E_INVALID;
@@ -244,9 +231,16 @@ double trpo_ctx_update(trpo_ctx *c, size_t max_iter, double resth, double max_kl
     const double t0 = now_s();
     double adv_sum = 0.0;
     /* policy gradient (:254-378), CG (:383-628) and FVP(x) (:633-832) on the device, one sync */
-    int rc = trpo_dev_update_solve(c->dev, max_iter, resth, b, x, z, &adv_sum);
-    if (!rc && verbose) print_cg_lines(c, max_iter, &inf.cg_iters);
-    else if (!rc && info) trpo_dev_cg_history(c->dev, NULL, NULL, 0, &inf.cg_iters);
+    double *rr = verbose ? (double *)malloc(sizeof(double) * (max_iter + 1)) : NULL;
+    double *xn = verbose ? (double *)malloc(sizeof(double) * (max_iter + 1)) : NULL;
+    int rc = (verbose && (!rr || !xn)) ? TRPO_E_NOMEM
+                                       : trpo_dev_update_solve(c->dev, max_iter, resth, b, x, z, &adv_sum,
+                                                               &inf.cg_iters, rr, xn);
+    if (!rc && verbose) /* src/TRPO_CG.c:56 -- one line per iteration */
+        for (size_t i = 0; i <= inf.cg_iters && i <= max_iter; ++i)
+            printf("CG Iter[%zu] Residual Norm=%.12e, Soln Norm=%.12e\n", i, rr[i], xn[i]);
+    free(rr);
+    free(xn);
     if (rc) {
         set_err("TRPO update failed on the device (code %d)", rc);
         ret = rc < 0 ? rc : TRPO_E_DEVICE;

@@ -2358,6 +2358,8 @@ struct trpo_dev {
     double *obs64;              // local observations [n][L0], fp64 (TRPO_Update path)
     void *pg_d, *pg_adv, *pg_iv;    // policy-gradient mode inputs (element esz, padded like obs4)
     size_t pg_cap;
+    unsigned pg_gen;                // rollout generation pg_d / pg_adv were built from
+    size_t pg_n;
     void *upd;                  // TRPO_Update path state (trpo_update.hip)
     double *std64;
     double *vec[5];             // V, Z, X, B, P
@@ -3297,6 +3299,8 @@ void trpo_dev_get_view(trpo_dev *d, trpo_dev_view *v) {
     v->vec_x = d->vec[TRPO_VEC_X];
     v->vec_v = d->vec[TRPO_VEC_V];
     v->vec_z = d->vec[TRPO_VEC_Z];
+    v->cg_iter = &d->ctl->iter;
+    v->cg_hist = d->hist;
 }
 
 int trpo_dev_allreduce64(trpo_dev *d, double *buf, size_t count) { return allreduce(d, buf, count); }
@@ -3329,7 +3333,7 @@ __global__ void pg_iv_kernel(const double *__restrict__ theta, int P, int A, int
     }
 }
 
-int trpo_dev_pg_sums_fast(trpo_dev *d, const double *roll64, const double **zacc) {
+int trpo_dev_pg_sums_fast(trpo_dev *d, const double *roll64, unsigned roll_gen, const double **zacc) {
     if (!d->fast) return 1;
     HCHK(hipSetDevice(d->device));
     const int ld = 16 * d->pack.T[3];
@@ -3342,16 +3346,24 @@ int trpo_dev_pg_sums_fast(trpo_dev *d, const double *roll64, const double **zacc
         HCHK(hipMalloc((void **)&d->pg_d, d->esz * npad * ld));
         HCHK(hipMalloc((void **)&d->pg_adv, d->esz * npad));
         d->pg_cap = npad;
+        d->pg_gen = 0;
     }
+    // the (Action - Mean) / Adv rows depend on the rollout only: rebuilt when it was re-uploaded
+    // (generation 0 never matches a real upload) or the sample count changed
+    const bool prep = d->pg_gen != roll_gen || d->pg_n != d->n;
+    d->pg_gen = roll_gen;
+    d->pg_n = d->n;
     if (!d->pg_iv) HCHK(hipMalloc((void **)&d->pg_iv, d->esz * ld));
     if (d->f64) {
-        hipLaunchKernelGGL(pg_prep_kernel<double>, dim3(cdiv((long)npad * ld, 256)), dim3(256), 0, d->stream, roll64,
-                           (int)d->n, (int)npad, d->net.A, ld, (double *)d->pg_d, (double *)d->pg_adv);
+        if (prep)
+            hipLaunchKernelGGL(pg_prep_kernel<double>, dim3(cdiv((long)npad * ld, 256)), dim3(256), 0, d->stream,
+                               roll64, (int)d->n, (int)npad, d->net.A, ld, (double *)d->pg_d, (double *)d->pg_adv);
         hipLaunchKernelGGL(pg_iv_kernel<double>, dim3(1), dim3(cdiv(ld, 64) * 64), 0, d->stream, d->theta64, d->P,
                            d->net.A, ld, (double *)d->pg_iv);
     } else {
-        hipLaunchKernelGGL(pg_prep_kernel<float>, dim3(cdiv((long)npad * ld, 256)), dim3(256), 0, d->stream, roll64,
-                           (int)d->n, (int)npad, d->net.A, ld, (float *)d->pg_d, (float *)d->pg_adv);
+        if (prep)
+            hipLaunchKernelGGL(pg_prep_kernel<float>, dim3(cdiv((long)npad * ld, 256)), dim3(256), 0, d->stream,
+                               roll64, (int)d->n, (int)npad, d->net.A, ld, (float *)d->pg_d, (float *)d->pg_adv);
         hipLaunchKernelGGL(pg_iv_kernel<float>, dim3(1), dim3(cdiv(ld, 64) * 64), 0, d->stream, d->theta64, d->P,
                            d->net.A, ld, (float *)d->pg_iv);
     }

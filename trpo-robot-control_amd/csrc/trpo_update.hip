@@ -41,6 +41,11 @@ struct UpdState {
     double *tpad = nullptr;                // register path: padded parameters [nk][PADW]
     size_t tpad_cap = 0;
     int lds_set = 0;
+    // pinned, device-mapped host buffer: results are written into it by a kernel (no copy-engine
+    // round trips through pageable memory); fullstep goes the other way through it
+    double *hst = nullptr, *hst_dev = nullptr;
+    size_t hst_cap = 0;
+    unsigned roll_gen = 0;                 // bumped by every rollout upload
 };
 
 void trpo_update_state_free(void *state) {
@@ -49,6 +54,7 @@ void trpo_update_state_free(void *state) {
     void *ptrs[] = {u->roll, u->ws, u->slabs, u->sum, u->fs, u->sums, u->tpad};
     for (void *p : ptrs)
         if (p) hipFree(p);
+    if (u->hst) hipHostFree(u->hst);
     delete u;
 }
 
@@ -446,6 +452,41 @@ static int ensure(double **p, size_t *cap, size_t count, hipStream_t st) {
     return 0;
 }
 
+static int ensure_host(UpdState *u, size_t count) {
+    if (count <= u->hst_cap && u->hst) return 0;
+    if (u->hst) hipHostFree(u->hst);
+    u->hst = u->hst_dev = nullptr;
+    u->hst_cap = 0;
+    HCHK(hipHostMalloc((void **)&u->hst, sizeof(double) * count, hipHostMallocDefault));
+    HCHK(hipHostGetDevicePointer((void **)&u->hst_dev, u->hst, 0));
+    u->hst_cap = count;
+    return 0;
+}
+
+// b, x, z (P each), sum(Adv), the CG iteration count and 2 (H) history values -> mapped host memory
+__global__ void export_solve_kernel(const double *__restrict__ b, const double *__restrict__ x,
+                                    const double *__restrict__ z, const double *__restrict__ adv,
+                                    const int *__restrict__ iter, const double *__restrict__ hist, int P, int H,
+                                    double *out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < P) {
+        out[i] = b[i];
+        out[P + i] = x[i];
+        out[2 * P + i] = z[i];
+    }
+    if (i == 0) {
+        out[3 * P] = *adv;
+        out[3 * P + 1] = (double)*iter;
+    }
+    if (i < H) out[3 * P + 2 + i] = hist[i];
+}
+
+// small vector copies to / from the mapped host buffer by a kernel (no copy-engine latency)
+__global__ void copy64_kernel(const double *__restrict__ src, double *__restrict__ dst, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[i];
+}
+
 static int rows_for(const Net &net, bool grads) {
     int tot = 0;
     for (int i = 0; i < net.nl; ++i) tot += net.L[i];
@@ -507,6 +548,7 @@ extern "C" int trpo_dev_set_rollout(trpo_dev *d, const double *mean, const doubl
     if (rc) return rc;
     u->roll_n = n;
     u->have_roll = 1;
+    ++u->roll_gen;
     return 0;
 }
 
@@ -525,7 +567,7 @@ static int enqueue_policy_gradient(trpo_dev *d, const double **adv_dev) {
     if (!u->sum) HCHK(hipMalloc((void **)&u->sum, sizeof(double) * (P + 1)));
     const char *eg = getenv("TRPO_UPDATE_GENERIC");
     const double *wsum = nullptr;
-    int fast = (eg && atoi(eg)) ? 1 : trpo_dev_pg_sums_fast(d, u->roll, &wsum);
+    int fast = (eg && atoi(eg)) ? 1 : trpo_dev_pg_sums_fast(d, u->roll, u->roll_gen, &wsum);
     if (fast < 0) return fast;
     if (fast == 0) {
         // weights / biases by the MFMA tile kernel (fp32 per sample, fp64 sums); LogStd + Adv in fp64
@@ -571,7 +613,7 @@ extern "C" int trpo_dev_policy_gradient(trpo_dev *d, double *b_host, double *adv
 }
 
 extern "C" int trpo_dev_update_solve(trpo_dev *d, size_t maxiter, double resth, double *b, double *x, double *z,
-                                     double *adv_sum) {
+                                     double *adv_sum, size_t *iters, double *rdotr_hist, double *xnorm_hist) {
     if (!d || !b || !x || !z || !adv_sum) return -1;
     const double *adv_dev = nullptr;
     int rc = enqueue_policy_gradient(d, &adv_dev);            // :254-378
@@ -583,11 +625,24 @@ extern "C" int trpo_dev_update_solve(trpo_dev *d, size_t maxiter, double resth, 
     HCHK(hipMemcpyAsync(v.vec_v, v.vec_x, bytes, hipMemcpyDeviceToDevice, v.stream));
     rc = trpo_dev_fvp(d);                                       // :633-832, z = F x
     if (rc) return rc;
-    HCHK(hipMemcpyAsync(b, v.vec_b, bytes, hipMemcpyDeviceToHost, v.stream));
-    HCHK(hipMemcpyAsync(x, v.vec_x, bytes, hipMemcpyDeviceToHost, v.stream));
-    HCHK(hipMemcpyAsync(z, v.vec_z, bytes, hipMemcpyDeviceToHost, v.stream));
-    HCHK(hipMemcpyAsync(adv_sum, adv_dev, sizeof(double), hipMemcpyDeviceToHost, v.stream));
+    UpdState *u = state(d);
+    const int P = v.net.P, H = 2 * ((int)maxiter + 1);
+    if (ensure_host(u, (size_t)3 * P + 2 + H)) return -2;
+    hipLaunchKernelGGL(export_solve_kernel, dim3(cdiv(P > H ? P : H, 256)), dim3(256), 0, v.stream, v.vec_b, v.vec_x,
+                       v.vec_z, adv_dev, v.cg_iter, v.cg_hist, P, H, u->hst_dev);
+    HCHK(hipGetLastError());
     HCHK(hipStreamSynchronize(v.stream));
+    const double *h = u->hst;
+    memcpy(b, h, bytes);
+    memcpy(x, h + P, bytes);
+    memcpy(z, h + 2 * P, bytes);
+    *adv_sum = h[3 * P];
+    const size_t it = (size_t)h[3 * P + 1];
+    if (iters) *iters = it;
+    for (size_t i = 0; i <= it && i <= maxiter; ++i) {
+        if (rdotr_hist) rdotr_hist[i] = h[3 * P + 2 + 2 * i];
+        if (xnorm_hist) xnorm_hist[i] = h[3 * P + 3 + 2 * i];
+    }
     return 0;
 }
 
@@ -605,7 +660,10 @@ extern "C" int trpo_dev_surrogate(trpo_dev *d, const double *fullstep, int k0, i
     if (!u->fs) HCHK(hipMalloc((void **)&u->fs, sizeof(double) * P));
     if (ensure(&u->slabs, &u->slab_cap, (size_t)Gs * nk, v.stream)) return -2;
     if (!u->sums) HCHK(hipMalloc((void **)&u->sums, sizeof(double) * 64));
-    HCHK(hipMemcpyAsync(u->fs, fullstep, sizeof(double) * P, hipMemcpyHostToDevice, v.stream));
+    // fullstep in through the mapped host buffer, the sums out through it
+    if (ensure_host(u, (size_t)P + 64)) return -2;
+    memcpy(u->hst, fullstep, sizeof(double) * P);
+    hipLaunchKernelGGL(copy64_kernel, dim3(cdiv(P, 256)), dim3(256), 0, v.stream, (const double *)u->hst_dev, u->fs, P);
     if (reg_path(net)) {
         if (ensure(&u->tpad, &u->tpad_cap, (size_t)PADW * nk, v.stream)) return -2;
         hipLaunchKernelGGL(pad_theta_kernel, dim3(cdiv(PADW, 256), nk), dim3(256), 0, v.stream, net, v.theta64,
@@ -623,8 +681,10 @@ extern "C" int trpo_dev_surrogate(trpo_dev *d, const double *fullstep, int k0, i
     hipLaunchKernelGGL(sum_slabs64_kernel, dim3(cdiv(nk, 16)), dim3(256), 0, v.stream, u->slabs, Gs, nk, u->sums);
     HCHK(hipGetLastError());
     if (trpo_dev_allreduce64(d, u->sums, (size_t)nk)) return -4;
-    HCHK(hipMemcpyAsync(surr_host, u->sums, sizeof(double) * nk, hipMemcpyDeviceToHost, v.stream));
+    hipLaunchKernelGGL(copy64_kernel, dim3(1), dim3(64), 0, v.stream, (const double *)u->sums, u->hst_dev + P, nk);
+    HCHK(hipGetLastError());
     HCHK(hipStreamSynchronize(v.stream));
+    memcpy(surr_host, u->hst + P, sizeof(double) * nk);
     return 0;
 }
 
