@@ -2388,6 +2388,9 @@ struct trpo_dev {
     size_t cg_graph_iters;
     double cg_graph_resth;
     hipEvent_t ev0, ev1;
+    // pinned, device-mapped host staging for the host <-> device vector moves (kernel copies)
+    double *hst, *hst_dev;
+    size_t hst_cap;
     // RCCL
     ncclComm_t comm;
     int rank, world;
@@ -2641,6 +2644,7 @@ extern "C" void trpo_dev_destroy(trpo_dev *d) {
         if (p) hipFree(p);
     for (int i = 0; i < 5; ++i)
         if (d->vec[i]) hipFree(d->vec[i]);
+    if (d->hst) hipHostFree(d->hst);
     if (d->ev0) hipEventDestroy(d->ev0);
     if (d->ev1) hipEventDestroy(d->ev1);
     if (d->stream) hipStreamDestroy(d->stream);
@@ -2876,19 +2880,44 @@ extern "C" int trpo_dev_set_comm(trpo_dev *d, int rank, int world, const void *i
     return refresh_n_total(d);
 }
 
+// Host <-> device vector moves through a pinned, device-mapped host buffer and a copy kernel: a
+// pageable hipMemcpyAsync costs ~20 us per call (staged through a driver bounce buffer), this ~5.
+__global__ void vcopy64_kernel(const double *__restrict__ src, double *__restrict__ dst, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[i];
+}
+static int ensure_hst(trpo_dev *d, size_t count) {
+    if (count <= d->hst_cap && d->hst) return 0;
+    if (d->hst) hipHostFree(d->hst);
+    d->hst = d->hst_dev = NULL;
+    d->hst_cap = 0;
+    HCHK(hipHostMalloc((void **)&d->hst, sizeof(double) * count, hipHostMallocDefault));
+    HCHK(hipHostGetDevicePointer((void **)&d->hst_dev, d->hst, 0));
+    d->hst_cap = count;
+    return 0;
+}
+
 extern "C" int trpo_dev_upload(trpo_dev *d, int slot, const double *host) {
     if (!d || slot < 0 || slot > 4 || !host) return -1;
     HCHK(hipSetDevice(d->device));
-    HCHK(hipMemcpyAsync(d->vec[slot], host, sizeof(double) * d->P, hipMemcpyHostToDevice, d->stream));
-    HCHK(hipStreamSynchronize(d->stream));
+    if (ensure_hst(d, (size_t)d->P + 2 * (size_t)(d->hist_cap + 8))) return -2;
+    memcpy(d->hst, host, sizeof(double) * d->P);
+    hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, (const double *)d->hst_dev,
+                       d->vec[slot], d->P);
+    HCHK(hipGetLastError());
+    HCHK(hipStreamSynchronize(d->stream));        // the staging buffer is reused by the next move
     return 0;
 }
 
 extern "C" int trpo_dev_download(trpo_dev *d, int slot, double *host) {
     if (!d || slot < 0 || slot > 4 || !host) return -1;
     HCHK(hipSetDevice(d->device));
-    HCHK(hipMemcpyAsync(host, d->vec[slot], sizeof(double) * d->P, hipMemcpyDeviceToHost, d->stream));
+    if (ensure_hst(d, (size_t)d->P + 2 * (size_t)(d->hist_cap + 8))) return -2;
+    hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, (const double *)d->vec[slot],
+                       d->hst_dev, d->P);
+    HCHK(hipGetLastError());
     HCHK(hipStreamSynchronize(d->stream));
+    memcpy(host, d->hst, sizeof(double) * d->P);
     return 0;
 }
 
@@ -3211,15 +3240,23 @@ extern "C" int trpo_dev_cg(trpo_dev *d, size_t maxiter, double resth) {
 extern "C" int trpo_dev_cg_history(trpo_dev *d, double *rdotr, double *xnorm, size_t cap, size_t *iters) {
     if (!d || !d->hist) return -1;
     HCHK(hipSetDevice(d->device));
+    // the control block and the whole history in one move (mapped host memory, copy kernels)
+    static_assert(sizeof(Ctl) % sizeof(double) == 0, "Ctl moves as 8-byte words");
+    const int cw = (int)(sizeof(Ctl) / sizeof(double)), hw = 2 * d->hist_cap;
+    if (ensure_hst(d, (size_t)d->P + 2 * (size_t)(d->hist_cap + 8))) return -2;
+    hipLaunchKernelGGL(vcopy64_kernel, dim3(1), dim3(64), 0, d->stream, (const double *)(const void *)d->ctl,
+                       d->hst_dev, cw);
+    hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv(hw, 256)), dim3(256), 0, d->stream, (const double *)d->hist,
+                       d->hst_dev + cw, hw);
+    HCHK(hipGetLastError());
     HCHK(hipStreamSynchronize(d->stream));
     Ctl c;
-    HCHK(hipMemcpyAsync(&c, d->ctl, sizeof c, hipMemcpyDeviceToHost, d->stream));
-    HCHK(hipStreamSynchronize(d->stream));
+    memcpy(&c, d->hst, sizeof c);
     const size_t n = (size_t)c.iter + 1;
+    if ((int)n > d->hist_cap) return -2;
     double *h = (double *)malloc(sizeof(double) * 2 * n);
     if (!h) return -3;
-    HCHK(hipMemcpyAsync(h, d->hist, sizeof(double) * 2 * n, hipMemcpyDeviceToHost, d->stream));
-    HCHK(hipStreamSynchronize(d->stream));
+    memcpy(h, d->hst + cw, sizeof(double) * 2 * n);
     for (size_t i = 0; i < n && i < cap; ++i) {
         if (rdotr) rdotr[i] = h[2 * i];
         if (xnorm) xnorm[i] = h[2 * i + 1];

@@ -755,6 +755,8 @@ struct trpo_bdev {
     size_t slab_cap = 0;
     double *sum = nullptr;
     int G = 1, rows = 0, use_lds = 0, lds = 0;
+    double *hst = nullptr, *hst_dev = nullptr;   // pinned mapped host buffer: theta in, sums (+ predictions) out
+    size_t hst_cap = 0;
 };
 
 static int act_code64(char a) {
@@ -773,6 +775,7 @@ extern "C" void trpo_bdev_destroy(trpo_bdev *b) {
     void *ptrs[] = {b->theta, b->obs, b->target, b->pred, b->ws, b->slabs, b->sum};
     for (void *p : ptrs)
         if (p) hipFree(p);
+    if (b->hst) hipHostFree(b->hst);
     if (b->stream) hipStreamDestroy(b->stream);
     delete b;
 }
@@ -872,15 +875,34 @@ extern "C" int trpo_bdev_eval(trpo_bdev *b, const double *theta, double *gsum, d
     HCHK(hipSetDevice(b->device));
     const Net &net = b->net;
     const int P = net.P;
-    HCHK(hipMemcpyAsync(b->theta, theta, sizeof(double) * (P - net.A), hipMemcpyHostToDevice, b->stream));
+    // x in and (f, g[, predictions]) out through pinned device-mapped host memory, moved by small
+    // kernels: no pageable copies on the L-BFGS callback's critical path
+    const size_t need = (size_t)P + 1 + b->n + (size_t)(P - net.A);   // [f, g | predictions | theta in]
+    if (need > b->hst_cap) {
+        if (b->hst) hipHostFree(b->hst);
+        b->hst = b->hst_dev = nullptr;
+        b->hst_cap = 0;
+        HCHK(hipHostMalloc((void **)&b->hst, sizeof(double) * need, hipHostMallocDefault));
+        HCHK(hipHostGetDevicePointer((void **)&b->hst_dev, b->hst, 0));
+        b->hst_cap = need;
+    }
+    double *hin = b->hst + P + 1 + b->n;                   // theta staging after the outputs
+    memcpy(hin, theta, sizeof(double) * (P - net.A));
+    hipLaunchKernelGGL(copy64_kernel, dim3(cdiv(P - net.A, 256)), dim3(256), 0, b->stream,
+                       (const double *)(b->hst_dev + P + 1 + b->n), b->theta, P - net.A);
     hipLaunchKernelGGL(baseline_kernel, dim3(b->G), dim3(UT), b->lds, b->stream, net, (const double *)b->theta,
                        (const double *)b->obs, (const double *)b->target, (int)b->n, b->ws, b->rows, b->use_lds,
                        b->slabs, b->pred);
     hipLaunchKernelGGL(sum_slabs64_kernel, dim3(cdiv(P + 1, 16)), dim3(256), 0, b->stream, b->slabs, b->G, P + 1,
                        b->sum);
+    hipLaunchKernelGGL(copy64_kernel, dim3(cdiv(P + 1, 256)), dim3(256), 0, b->stream, (const double *)b->sum,
+                       b->hst_dev, P + 1);
+    if (pred)
+        hipLaunchKernelGGL(copy64_kernel, dim3(cdiv((long)b->n, 256)), dim3(256), 0, b->stream, (const double *)b->pred,
+                           b->hst_dev + P + 1, (int)b->n);
     HCHK(hipGetLastError());
-    HCHK(hipMemcpyAsync(gsum, b->sum, sizeof(double) * (P + 1), hipMemcpyDeviceToHost, b->stream));
-    if (pred) HCHK(hipMemcpyAsync(pred, b->pred, sizeof(double) * b->n, hipMemcpyDeviceToHost, b->stream));
     HCHK(hipStreamSynchronize(b->stream));
+    memcpy(gsum, b->hst, sizeof(double) * (P + 1));
+    if (pred) memcpy(pred, b->hst + P + 1, sizeof(double) * b->n);
     return 0;
 }
