@@ -314,19 +314,30 @@ def main():
     if args.extra and dist.world == 1:
         extra = {}
         L2 = [15, 64, 64, 3]
-        c2, th2, obs2 = make_ctx(L2, 4096, dist, device)
-        c2.upload_v(synth.make_v(synth.num_params(L2)))
-        k2 = c2.time_ms(0, reps)
-        f2 = c2.time_ms(1, reps)
-        extra["C2_fvp_2x64_N4096"] = {"fvp_ms": f2, "kernel_ms": k2, "fvp_samples_per_s": 4096 / (f2 * 1e-3),
-                                      "kernel_tflops": flops_per_sample(L2) * 4096 / (k2 * 1e-3) / 1e12}
-        c2.close()
+        # C2: repeated FVP calls on one context reuse the forward-activation cache (theta unchanged);
+        # a first call after set_theta recomputes the forward pass -- timed too (TRPO_YCACHE=0)
+        c2res = {}
+        for tag, env in (("", None), ("_recompute", "0")):
+            if env is not None:
+                os.environ["TRPO_YCACHE"] = env
+            c2, th2, obs2 = make_ctx(L2, 4096, dist, device)
+            os.environ.pop("TRPO_YCACHE", None)
+            c2.upload_v(synth.make_v(synth.num_params(L2)))
+            k2 = c2.time_ms(0, reps)
+            f2 = c2.time_ms(1, reps)
+            fl = flops_per_sample_cached(L2) if env is None else flops_per_sample(L2)
+            c2res.update({"fvp_ms" + tag: f2, "kernel_ms" + tag: k2, "fvp_samples_per_s" + tag: 4096 / (f2 * 1e-3),
+                          "kernel_tflops" + tag: fl * 4096 / (k2 * 1e-3) / 1e12})
+            c2.close()
+        extra["C2_fvp_2x64_N4096"] = c2res
         c3, th3, obs3 = make_ctx(L2, N_TOTAL, dist, device)
         t3 = time_steps(c3, dist, 20, 3, synth.make_b(synth.num_params(L2)))
         k3 = c3.time_ms(0, reps)
         extra["C3_cg10_2x64_N50000"] = {"cg_wall_ms": 1e3 * t3 / 20, "fvp_samples_per_s": CG_ITERS * N_TOTAL / (t3 / 20),
-                                        "kernel_ms": k3,
-                                        "kernel_tflops": flops_per_sample(L2) * N_TOTAL / (k3 * 1e-3) / 1e12}
+                                        "kernel_ms": k3, "kernel": c3.kernel_name + " (cached forward)",
+                                        "kernel_tflops": flops_per_sample_cached(L2) * N_TOTAL / (k3 * 1e-3) / 1e12,
+                                        "kernel_tflops_recompute_equiv":
+                                            flops_per_sample(L2) * N_TOTAL / (k3 * 1e-3) / 1e12}
         c3.close()
         # fp64 precision mode (the reference's arithmetic, fp64 MFMA): same CG(10) workloads
         for key, L in (("C1_cg10_armDOF_0_N50000_fp64", [15, 16, 16, 3]), ("C3_cg10_2x64_N50000_fp64", L2)):
@@ -334,8 +345,9 @@ def main():
             tf = time_steps(cf, dist, 20, 3, synth.make_b(synth.num_params(L)))
             kf = cf.time_ms(0, reps)
             extra[key] = {"cg_wall_ms": 1e3 * tf / 20, "fvp_samples_per_s": CG_ITERS * N_TOTAL / (tf / 20),
-                          "kernel": cf.kernel_name, "kernel_ms": kf,
-                          "kernel_tflops": flops_per_sample(L) * N_TOTAL / (kf * 1e-3) / 1e12,
+                          "kernel": cf.kernel_name + " (cached forward)", "kernel_ms": kf,
+                          "kernel_tflops": flops_per_sample_cached(L) * N_TOTAL / (kf * 1e-3) / 1e12,
+                          "kernel_tflops_recompute_equiv": flops_per_sample(L) * N_TOTAL / (kf * 1e-3) / 1e12,
                           "peak_fp64_mfma_tflops": PEAK_FP64_TFLOPS}
             cf.close()
         extra["C5_update_armDOF_0_N50000"] = bench_update(device)
