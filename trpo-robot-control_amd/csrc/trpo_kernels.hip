@@ -2869,7 +2869,13 @@ extern "C" int trpo_dev_set_comm(trpo_dev *d, int rank, int world, const void *i
     if (world > 1) {
         ncclUniqueId id;
         memcpy(&id, id128, sizeof(id));
-        if (ncclCommInitRank(&d->comm, world, id, rank) != ncclSuccess) return -4;
+        const ncclResult_t nr = ncclCommInitRank(&d->comm, world, id, rank);
+        if (nr != ncclSuccess) {
+            fprintf(stderr, "[trpo_mi355x] ncclCommInitRank(rank %d of %d, device %d): %s\n", rank, world, d->device,
+                    ncclGetErrorString(nr));
+            d->comm = NULL;
+            return -4;
+        }
     }
     d->rank = rank;
     d->world = world;
