@@ -35,6 +35,7 @@ int trpo_dev_upload(trpo_dev *d, int slot, const double *host);
 int trpo_dev_download(trpo_dev *d, int slot, double *host);
 
 int trpo_dev_fvp(trpo_dev *d);                 /* enqueue z = F v  (slots V -> Z) */
+int trpo_dev_fvp_src(trpo_dev *d, const double *src);   /* enqueue z = F src (any device vector) -> Z */
 int trpo_dev_fvp_kernel(trpo_dev *d);          /* enqueue the dominant kernel alone */
 int trpo_dev_cg(trpo_dev *d, size_t maxiter, double resth); /* enqueue CG on slot B -> X */
 int trpo_dev_cg_history(trpo_dev *d, double *rdotr, double *xnorm, size_t cap, size_t *iters);
@@ -54,7 +55,10 @@ int trpo_dev_surrogate(trpo_dev *d, const double *fullstep, int k0, int nk, doub
  * (optional, capacity maxiter + 1) its rdotr / |x| history to the host, written by one kernel into
  * pinned host memory. */
 int trpo_dev_update_solve(trpo_dev *d, size_t maxiter, double resth, double *b, double *x, double *z,
-                          double *adv_sum, size_t *iters, double *rdotr_hist, double *xnorm_hist);
+                          double *adv_sum, size_t *iters, double *rdotr_hist, double *xnorm_hist,
+                          double max_kl, double *surr0);
+/* surr0 (optional): also the step size (host arithmetic, bit for bit) and the surrogate sum of the full
+ * step theta + fullstep, the line search's first candidate, in the same synchronisation. */
 
 /* Value-baseline objective (src/TRPO_Baseline.c), its own small device object. */
 typedef struct trpo_bdev trpo_bdev;

@@ -229,13 +229,14 @@ double trpo_ctx_update(trpo_ctx *c, size_t max_iter, double resth, double max_kl
     double ret = TRPO_E_NOMEM;
     if (!b || !x || !z || !fullstep) goto out;
     const double t0 = now_s();
-    double adv_sum = 0.0;
+    double adv_sum = 0.0, surr0 = 0.0;
     /* policy gradient (:254-378), CG (:383-628) and FVP(x) (:633-832) on the device, one sync */
     double *rr = verbose ? (double *)malloc(sizeof(double) * (max_iter + 1)) : NULL;
     double *xn = verbose ? (double *)malloc(sizeof(double) * (max_iter + 1)) : NULL;
     int rc = (verbose && (!rr || !xn)) ? TRPO_E_NOMEM
                                        : trpo_dev_update_solve(c->dev, max_iter, resth, b, x, z, &adv_sum,
-                                                               &inf.cg_iters, rr, xn);
+                                                               &inf.cg_iters, rr, xn, max_kl,
+                                                               max_bt > 0 ? &surr0 : NULL);
     if (!rc && verbose) /* src/TRPO_CG.c:56 -- one line per iteration */
         for (size_t i = 0; i <= inf.cg_iters && i <= max_iter; ++i)
             printf("CG Iter[%zu] Residual Norm=%.12e, Soln Norm=%.12e\n", i, rr[i], xn[i]);
@@ -275,7 +276,10 @@ double trpo_ctx_update(trpo_ctx *c, size_t max_iter, double resth, double max_kl
     for (int k0 = 0; k0 < max_bt && inf.accepted < 0;) {
         const int nk = k0 == 0 ? 1 : max_bt - k0;
         double surr[TRPO_MAX_BACKTRACKS];
-        rc = trpo_dev_surrogate(c->dev, fullstep, k0, nk, surr);
+        if (k0 == 0)
+            surr[0] = surr0;       /* evaluated by the device with the solve (same fullstep, bit for bit) */
+        else
+            rc = trpo_dev_surrogate(c->dev, fullstep, k0, nk, surr);
         if (rc) {
             set_err("line search failed on the device (code %d)", rc);
             ret = rc < 0 ? rc : TRPO_E_DEVICE;

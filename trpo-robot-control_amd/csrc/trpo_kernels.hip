@@ -3011,36 +3011,39 @@ static int enqueue_fvp_core(trpo_dev *d, const double *src, const int *skip) {
     return 0;
 }
 
-extern "C" int trpo_dev_fvp(trpo_dev *d) {
-    if (!d) return -1;
+// z = F src into slot Z (src: any device P-vector, e.g. slot X for the update's FVP(x))
+extern "C" int trpo_dev_fvp_src(trpo_dev *d, const double *src) {
+    if (!d || !src) return -1;
     if (d->n_total <= 0) return -1;
     HCHK(hipSetDevice(d->device));
     if (d->fast && (d->atomic || !d->comm)) {
         // two launches: the tile kernel gathers its direction fragments from v itself, then the
         // atomic-replica or slab reduce applies the epilogue (under RCCL after the all-reduce)
         IterArgs a = plain_args(d, &d->ctl->zero);
-        a.v_nat = d->vec[TRPO_VEC_V];
+        a.v_nat = src;
         double *acc = launch_fvp_plain(d, a);
         if (acc) {
             if (allreduce(d, acc, (size_t)d->Rc * d->P)) return -4;
             hipLaunchKernelGGL(acc_epilogue_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, acc, d->Rc,
-                               d->vec[TRPO_VEC_V], d->vec[TRPO_VEC_Z], d->P, d->nw, d->ctl);
+                               src, d->vec[TRPO_VEC_Z], d->P, d->nw, d->ctl);
         } else {
-            launch_reduce(d, &d->ctl->zero, d->vec[TRPO_VEC_V], d->vec[TRPO_VEC_Z]);
+            launch_reduce(d, &d->ctl->zero, src, d->vec[TRPO_VEC_Z]);
         }
         HCHK(hipGetLastError());
         return 0;
     }
     if (d->fast)
         hipLaunchKernelGGL(gather_pack_kernel, dim3(cdiv(d->pack.vlen, 256)), dim3(256), 0, d->stream, d->vpack,
-                           d->vec[TRPO_VEC_V], d->vmap, d->pack.vlen, d->f64);
-    int rc = enqueue_fvp_core(d, d->vec[TRPO_VEC_V], &d->ctl->zero);
+                           src, d->vmap, d->pack.vlen, d->f64);
+    int rc = enqueue_fvp_core(d, src, &d->ctl->zero);
     if (rc) return rc;
     hipLaunchKernelGGL(fvp_epilogue_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, d->zacc,
-                       d->vec[TRPO_VEC_V], d->vec[TRPO_VEC_Z], d->P, d->nw, d->ctl);
+                       src, d->vec[TRPO_VEC_Z], d->P, d->nw, d->ctl);
     HCHK(hipGetLastError());
     return 0;
 }
+
+extern "C" int trpo_dev_fvp(trpo_dev *d) { return d ? trpo_dev_fvp_src(d, d->vec[TRPO_VEC_V]) : -1; }
 
 extern "C" int trpo_dev_fvp_kernel(trpo_dev *d) {
     if (!d || d->n == 0) return -1;

@@ -481,6 +481,30 @@ __global__ void export_solve_kernel(const double *__restrict__ b, const double *
     if (i < H) out[3 * P + 2 + i] = hist[i];
 }
 
+// Step size of src/TRPO_Update.c:834-868 on the device, in the host code's exact arithmetic
+// (sequential, unfused fp64: the host recomputes the same values from b, x, z bit for bit):
+// shs = 0.5 sum z_i x_i, lm = sqrt(shs / max_kl), fullstep = x / lm
+constexpr int STEP_PMAX = 4096;                  // LDS-staged products; larger P reads them from memory
+__global__ void step_kernel(const double *__restrict__ x, const double *__restrict__ z, int P, double max_kl,
+                            double *__restrict__ fs) {
+    __shared__ double lm_s;
+    __shared__ double prod[STEP_PMAX];
+    // the products in parallel (each correctly rounded, as the host's z[i] * x[i]), then ONE thread
+    // sums them in index order (the host's order) out of LDS
+    for (int i = threadIdx.x; i < P && i < STEP_PMAX; i += blockDim.x) prod[i] = __dmul_rn(z[i], x[i]);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double shs = 0.0;
+        int i = 0;
+        for (; i < P && i < STEP_PMAX; ++i) shs = __dadd_rn(shs, prod[i]);
+        for (; i < P; ++i) shs = __dadd_rn(shs, __dmul_rn(z[i], x[i]));
+        shs = __dmul_rn(shs, 0.5);
+        lm_s = sqrt(__ddiv_rn(shs, max_kl));
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < P; i += blockDim.x) fs[i] = __ddiv_rn(x[i], lm_s);
+}
+
 // small vector copies to / from the mapped host buffer by a kernel (no copy-engine latency)
 __global__ void copy64_kernel(const double *__restrict__ src, double *__restrict__ dst, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -612,8 +636,11 @@ extern "C" int trpo_dev_policy_gradient(trpo_dev *d, double *b_host, double *adv
     return 0;
 }
 
+static int enqueue_surrogate(trpo_dev *d, const double *fs, int k0, int nk);
+
 extern "C" int trpo_dev_update_solve(trpo_dev *d, size_t maxiter, double resth, double *b, double *x, double *z,
-                                     double *adv_sum, size_t *iters, double *rdotr_hist, double *xnorm_hist) {
+                                     double *adv_sum, size_t *iters, double *rdotr_hist, double *xnorm_hist,
+                                     double max_kl, double *surr0) {
     if (!d || !b || !x || !z || !adv_sum) return -1;
     const double *adv_dev = nullptr;
     int rc = enqueue_policy_gradient(d, &adv_dev);            // :254-378
@@ -622,16 +649,27 @@ extern "C" int trpo_dev_update_solve(trpo_dev *d, size_t maxiter, double resth, 
     trpo_dev_view v;
     trpo_dev_get_view(d, &v);
     const size_t bytes = sizeof(double) * v.net.P;
-    HCHK(hipMemcpyAsync(v.vec_v, v.vec_x, bytes, hipMemcpyDeviceToDevice, v.stream));
-    rc = trpo_dev_fvp(d);                                       // :633-832, z = F x
+    rc = trpo_dev_fvp_src(d, v.vec_x);                          // :633-832, z = F x (x read in place)
     if (rc) return rc;
     UpdState *u = state(d);
     const int P = v.net.P, H = 2 * ((int)maxiter + 1);
-    if (ensure_host(u, (size_t)3 * P + 2 + H)) return -2;
+    if (ensure_host(u, (size_t)3 * P + 3 + H)) return -2;
+    if (surr0) {
+        // the step size and the full-step surrogate (the usual outcome of the line search) in the same
+        // submission: no host round trip between the solve and the first line-search candidate
+        if (!u->fs) HCHK(hipMalloc((void **)&u->fs, sizeof(double) * P));
+        hipLaunchKernelGGL(step_kernel, dim3(1), dim3(256), 0, v.stream, (const double *)v.vec_x,
+                           (const double *)v.vec_z, P, max_kl, u->fs);
+        rc = enqueue_surrogate(d, u->fs, 0, 1);
+        if (rc) return rc;
+        hipLaunchKernelGGL(copy64_kernel, dim3(1), dim3(64), 0, v.stream, (const double *)u->sums,
+                           u->hst_dev + 3 * P + 2 + H, 1);
+    }
     hipLaunchKernelGGL(export_solve_kernel, dim3(cdiv(P > H ? P : H, 256)), dim3(256), 0, v.stream, v.vec_b, v.vec_x,
                        v.vec_z, adv_dev, v.cg_iter, v.cg_hist, P, H, u->hst_dev);
     HCHK(hipGetLastError());
     HCHK(hipStreamSynchronize(v.stream));
+    if (surr0) *surr0 = u->hst[3 * P + 2 + H];
     const double *h = u->hst;
     memcpy(b, h, bytes);
     memcpy(x, h + P, bytes);
@@ -646,28 +684,23 @@ extern "C" int trpo_dev_update_solve(trpo_dev *d, size_t maxiter, double resth, 
     return 0;
 }
 
-extern "C" int trpo_dev_surrogate(trpo_dev *d, const double *fullstep, int k0, int nk, double *surr_host) {
-    if (!d || !fullstep || !surr_host || k0 < 0 || nk < 1 || nk > 64 || k0 + nk > 1074) return -1;
+// enqueue the surrogate sums of candidates theta + 2^-k fs, k = k0 .. k0+nk-1 (fs on the device),
+// all-reduced over the ranks, into u->sums[0 .. nk)
+static int enqueue_surrogate(trpo_dev *d, const double *fs, int k0, int nk) {
     trpo_dev_view v;
     trpo_dev_get_view(d, &v);
     UpdState *u = state(d);
     if (!u->have_roll || u->roll_n != v.n) return -3;
-    HCHK(hipSetDevice(v.device));
     const Net &net = v.net;
-    const int P = net.P, n = (int)v.n;
+    const int n = (int)v.n;
     const int cap = 2048 / nk > 0 ? 2048 / nk : 1;
     const int Gs = n ? (cdiv(n, UT) < cap ? cdiv(n, UT) : cap) : 1;
-    if (!u->fs) HCHK(hipMalloc((void **)&u->fs, sizeof(double) * P));
     if (ensure(&u->slabs, &u->slab_cap, (size_t)Gs * nk, v.stream)) return -2;
     if (!u->sums) HCHK(hipMalloc((void **)&u->sums, sizeof(double) * 64));
-    // fullstep in through the mapped host buffer, the sums out through it
-    if (ensure_host(u, (size_t)P + 64)) return -2;
-    memcpy(u->hst, fullstep, sizeof(double) * P);
-    hipLaunchKernelGGL(copy64_kernel, dim3(cdiv(P, 256)), dim3(256), 0, v.stream, (const double *)u->hst_dev, u->fs, P);
     if (reg_path(net)) {
         if (ensure(&u->tpad, &u->tpad_cap, (size_t)PADW * nk, v.stream)) return -2;
-        hipLaunchKernelGGL(pad_theta_kernel, dim3(cdiv(PADW, 256), nk), dim3(256), 0, v.stream, net, v.theta64,
-                           (const double *)u->fs, k0, u->tpad);
+        hipLaunchKernelGGL(pad_theta_kernel, dim3(cdiv(PADW, 256), nk), dim3(256), 0, v.stream, net, v.theta64, fs, k0,
+                           u->tpad);
         hipLaunchKernelGGL(surr_reg_kernel, dim3(Gs, nk), dim3(UT), 0, v.stream, net, (const double *)u->tpad,
                            v.obs64, u->roll, v.std64, n, u->slabs);
     } else {
@@ -675,12 +708,30 @@ extern "C" int trpo_dev_surrogate(trpo_dev *d, const double *fullstep, int k0, i
         int use_lds = 0;
         const int lds = act_storage(u, rows, (long)Gs * nk, v.stream, &use_lds);
         if (lds < 0) return -2;
-        hipLaunchKernelGGL(surr_kernel, dim3(Gs, nk), dim3(UT), lds, v.stream, net, v.theta64, u->fs, k0, v.obs64,
+        hipLaunchKernelGGL(surr_kernel, dim3(Gs, nk), dim3(UT), lds, v.stream, net, v.theta64, fs, k0, v.obs64,
                            u->roll, v.std64, n, u->ws, rows, use_lds, u->slabs);
     }
     hipLaunchKernelGGL(sum_slabs64_kernel, dim3(cdiv(nk, 16)), dim3(256), 0, v.stream, u->slabs, Gs, nk, u->sums);
     HCHK(hipGetLastError());
     if (trpo_dev_allreduce64(d, u->sums, (size_t)nk)) return -4;
+    return 0;
+}
+
+extern "C" int trpo_dev_surrogate(trpo_dev *d, const double *fullstep, int k0, int nk, double *surr_host) {
+    if (!d || !fullstep || !surr_host || k0 < 0 || nk < 1 || nk > 64 || k0 + nk > 1074) return -1;
+    trpo_dev_view v;
+    trpo_dev_get_view(d, &v);
+    UpdState *u = state(d);
+    if (!u->have_roll || u->roll_n != v.n) return -3;
+    HCHK(hipSetDevice(v.device));
+    const int P = v.net.P;
+    if (!u->fs) HCHK(hipMalloc((void **)&u->fs, sizeof(double) * P));
+    // fullstep in through the mapped host buffer, the sums out through it
+    if (ensure_host(u, (size_t)P + 64)) return -2;
+    memcpy(u->hst, fullstep, sizeof(double) * P);
+    hipLaunchKernelGGL(copy64_kernel, dim3(cdiv(P, 256)), dim3(256), 0, v.stream, (const double *)u->hst_dev, u->fs, P);
+    int rc = enqueue_surrogate(d, u->fs, k0, nk);
+    if (rc) return rc;
     hipLaunchKernelGGL(copy64_kernel, dim3(1), dim3(64), 0, v.stream, (const double *)u->sums, u->hst_dev + P, nk);
     HCHK(hipGetLastError());
     HCHK(hipStreamSynchronize(v.stream));
