@@ -39,6 +39,27 @@ struct Net {
 
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
+// fp64 tanh for the device fp64 paths (precision mode, policy gradient, line search, baseline):
+// |x| < 0.55: x + x^3 Q(x^2), Q of degree 9 fitted in extended precision (tools/fit_tanh64.py,
+// max relative error 5.4e-16); else 1 - 2 / (e^{2|x|} + 1) (2.7e-16).  ~3x fewer instructions
+// than the device libm tanh, which is double-double throughout (it dominated the fp64 surrogate).
+__device__ __forceinline__ double tanh64(double x) {
+    const double a = fabs(x), u = x * x;
+    double q = 6.76744223569079683e-05;
+    q = fma(q, u, -2.34387837673838705e-04);
+    q = fma(q, u, 5.93821938760988777e-04);
+    q = fma(q, u, -1.45812091104440249e-03);
+    q = fma(q, u, 3.59269513652666532e-03);
+    q = fma(q, u, -8.86331213798425936e-03);
+    q = fma(q, u, 2.18694943489975979e-02);
+    q = fma(q, u, -5.39682542017260666e-02);
+    q = fma(q, u, 1.33333333337541271e-01);
+    q = fma(q, u, -3.33333333333355408e-01);
+    const double small = fma(a * u, q, a);
+    const double big = a > 22.0 ? 1.0 : 1.0 - 2.0 / (exp(2.0 * a) + 1.0);
+    return copysign(a < 0.55 ? small : big, x);
+}
+
 // What the TRPO_Update translation unit may see of a device context.
 struct trpo_dev_view {
     int device;

@@ -1329,7 +1329,7 @@ template <> struct PT<double> {
     }
     static __host__ __device__ __forceinline__ int neu(int g, int r) { return g + 4 * r; }
     static __device__ __forceinline__ double rsum16(double v) { return rowsum16_f64(v); }
-    static __device__ __forceinline__ double th(double x) { return tanh(x); }
+    static __device__ __forceinline__ double th(double x) { return tanh64(x); }
     static __device__ __forceinline__ double sg(double x) { return 1.0 / (1.0 + exp(-x)); }
 };
 

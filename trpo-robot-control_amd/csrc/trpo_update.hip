@@ -60,7 +60,7 @@ void trpo_update_state_free(void *state) {
 
 __device__ __forceinline__ double act_y64(int a, double x) {
     switch (a) {
-    case ACT_T: return tanh(x);
+    case ACT_T: return tanh64(x);
     case ACT_O: return 0.1 * x;
     case ACT_S: return 1.0 / (1.0 + exp(-x));
     default: return x;
@@ -251,7 +251,7 @@ __global__ void pad_theta_kernel(Net net, const double *__restrict__ th, const d
 __device__ __forceinline__ void act_vec(int a, double (&v)[RW]) {
     if (a == ACT_T) {
 #pragma unroll
-        for (int j = 0; j < RW; ++j) v[j] = tanh(v[j]);
+        for (int j = 0; j < RW; ++j) v[j] = tanh64(v[j]);
     } else if (a == ACT_S) {
 #pragma unroll
         for (int j = 0; j < RW; ++j) v[j] = 1.0 / (1.0 + exp(-v[j]));
