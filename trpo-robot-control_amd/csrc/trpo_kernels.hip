@@ -2019,7 +2019,9 @@ __global__ void fvp_epilogue_kernel(const double *__restrict__ zacc, const doubl
 }
 
 // the same epilogue from R atomic replicas of the un-normalised sum (fixed replica order)
-__global__ void acc_epilogue_kernel(const double *__restrict__ acc, int R, const double *__restrict__ v,
+// The replica set is left zeroed (each element by the thread that consumed it), so standalone FVPs
+// need no separate zeroing and the same launch sequence can be replayed from a graph.
+__global__ void acc_epilogue_kernel(double *__restrict__ acc, int R, const double *__restrict__ v,
                                     double *__restrict__ z, int P, int nw, const Ctl *__restrict__ ctl) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= P) return;
@@ -2031,6 +2033,8 @@ __global__ void acc_epilogue_kernel(const double *__restrict__ acc, int R, const
     for (int r = 1; r < 8; ++r) s += r < R ? a[r] : 0.0;
     const double vq = v[q];
     z[q] = (q < nw ? s / ctl->n_total : 2.0 * vq) + ctl->damping * vq;
+    if (q < nw)
+        for (int r = 0; r < R; ++r) acc[(long)r * P + q] = 0.0;
 }
 
 // ---------------------------------------------------------------------------
@@ -2367,8 +2371,8 @@ struct trpo_dev {
     double *pbuf[2], *rbuf[2];  // ping-ponged CG direction / residual
     CgSt *st;                   // 2 ping-ponged CG scalar states
     double *accbuf;             // atomic mode: 3 x R fp64 replicas of the P-vector
-    double *pacc;               // atomic mode, standalone FVPs: 2 x R replicas, ping-ponged
-    int pacc_k;                 // the zeroed pacc set the next standalone FVP accumulates into
+    double *pacc;               // atomic mode, standalone FVPs: R replicas (set 0; left zeroed by the
+                                // epilogue) + a sink set for epilogue-less kernel-only timing launches
     int atomic, R;
     int Rc;                     // replicas in use: R on one GPU; under RCCL sized from the global shard
                                 // geometry (identical on every rank) to keep the all-reduce small
@@ -2965,18 +2969,15 @@ static void launch_reduce(trpo_dev *d, const int *skip, const double *vin = null
 static int allreduce(trpo_dev *d, double *buf, size_t count);
 
 // Returns the atomic replica set it accumulated into (atomic mode) or NULL (block slabs).
-static double *launch_fvp_plain(trpo_dev *d, IterArgs &a) {
+// sink: a kernel-only launch whose result is never consumed (timing): accumulates into the sink set.
+static double *launch_fvp_plain(trpo_dev *d, IterArgs &a, bool sink = false) {
     double *acc = NULL;
     if (d->atomic) {
-        // fp64 atomics into R replicas, like the CG kernels (no slab round trip through HBM); block 0
-        // zeroes the other set for the next standalone FVP
-        const long RP = (long)d->Rc * d->P, stride = (long)d->R * d->P;
-        acc = d->pacc + (d->pacc_k & 1) * stride;
+        // fp64 atomics into R replicas, like the CG kernels (no slab round trip through HBM); the
+        // set is zero on entry because its consumer, acc_epilogue_kernel, leaves it zeroed
+        acc = d->pacc + (sink ? (long)d->R * d->P : 0);
         a.acc_out = acc;
         a.R_out = d->Rc;
-        a.acc_zero = d->pacc + ((d->pacc_k + 1) & 1) * stride;
-        a.zero_len = (int)RP;
-        d->pacc_k ^= 1;
     }
     if (d->yc_on) {
         a.yc = reinterpret_cast<float4 *>(d->yc);
@@ -3051,7 +3052,7 @@ extern "C" int trpo_dev_fvp_kernel(trpo_dev *d) {
     if (d->fast) {
         IterArgs a = plain_args(d, &d->ctl->zero);
         a.v_nat = d->vec[TRPO_VEC_V];                  // the same launch as the FVP call's
-        launch_fvp_plain(d, a);
+        launch_fvp_plain(d, a, true);                  // no epilogue follows: accumulate into the sink
     } else {
         hipLaunchKernelGGL(fvp_generic_kernel, dim3(d->grid), dim3(GEN_T), 0, d->stream, d->obs32, (int)d->n,
                            d->th32, d->v32, d->iv32, d->scratch, d->srows, (float *)d->slabs, d->slab, d->net,
