@@ -187,7 +187,8 @@ def bench_update(device, n=N_TOTAL, reps=20):
     mean, action, adv = synth.make_rollout(L, "lttl", theta, obs, std)
     ctx = trpo_amd.Context(L, "lttl", theta, obs, std, DAMPING, device=device)
     ctx.set_rollout(mean, action, adv)
-    r = ctx.update()
+    for _ in range(3):      # warm-up: eager first call, then the one-off capture of the update graph
+        r = ctx.update()
     t0 = time.perf_counter()
     for _ in range(reps):
         r = ctx.update()

@@ -149,3 +149,36 @@ def test_update_requires_rollout():
         ctx.set_obs(x["obs"][:100])                   # new samples invalidate the rollout
         with pytest.raises(trpo_amd.TRPOError):
             ctx.update()
+
+
+@pytest.mark.parametrize("layers", [[15, 16, 16, 3], [15, 64, 64, 3]])
+def test_repeated_updates_deterministic(layers, monkeypatch):
+    """A trainer-like sequence on one context -- several updates, set_theta / set_rollout between them,
+    a rejected full step, each update repeated -- is deterministic: two runs agree bit for bit (the
+    device state the update reuses across calls: forward cache, replica sets, rollout rows, graphs)."""
+    from trpo_amd import synth
+    n = 3000
+    th0, obs = synth.make_theta(layers), synth.make_obs(n, layers[0])
+    std = np.ones(layers[-1])
+
+    def run():
+        out = []
+        th = th0.copy()
+        with trpo_amd.Context(layers, "lttl", th, obs, std, 0.1) as ctx:
+            for it in range(4):
+                mean, action, adv = synth.make_rollout(layers, "lttl", th, obs, std)
+                if it == 3:
+                    adv = -adv              # sign-flipped advantages: the full step is rejected
+                ctx.set_rollout(mean, action, adv)
+                r = ctx.update()
+                r2 = ctx.update()          # same rollout and theta: the replayed graph
+                out.append((r["theta"], r["x"], r["b"], r2["theta"], r2["ratio"], r["accepted"], r2["accepted"]))
+                th = r["theta"]
+                ctx.set_theta(th)
+        return out
+
+    eager = run()
+    graph = run()
+    for a, e in zip(graph, eager):
+        for x, y in zip(a, e):
+            np.testing.assert_array_equal(x, y)

@@ -16,7 +16,8 @@ std = np.ones(3)
 mean, action, adv = synth.make_rollout(L, "lttl", th, obs, std)
 with trpo_amd.Context(L, "lttl", th, obs, std) as ctx:
     ctx.set_rollout(mean, action, adv)
-    ctx.update()
+    for _ in range(3):            # warm: the first call runs eagerly, the second captures the update graph
+        ctx.update()
     t0 = time.perf_counter()
     for _ in range(reps):
         r = ctx.update()

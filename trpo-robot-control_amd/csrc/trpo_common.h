@@ -84,6 +84,9 @@ int trpo_dev_allreduce64(trpo_dev *d, double *buf, size_t count);
 // roll_gen: the rollout's upload generation -- its fp32 (Action - Mean) / Adv rows are rebuilt only
 // when it changes.
 int trpo_dev_pg_sums_fast(trpo_dev *d, const double *roll64, unsigned roll_gen, const double **zacc);
+int trpo_dev_pg_prepare(trpo_dev *d, const double *roll64, unsigned roll_gen);
+// forward-cache bookkeeping after a CG solve
+void trpo_dev_ycache_written(trpo_dev *d);
 // per-context storage of the update path (owned by trpo_update.hip)
 void **trpo_dev_update_state(trpo_dev *d);
 void trpo_update_state_free(void *state);

@@ -3207,6 +3207,12 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
     return 0;
 }
 
+// after a CG solve the forward-activation cache holds the current theta's activations (its first FVP
+// writes them unconditionally), so the FVP(x) that follows may read it
+void trpo_dev_ycache_written(trpo_dev *d) {
+    if (d->yc_on) d->yc_valid = 1;
+}
+
 extern "C" int trpo_dev_cg(trpo_dev *d, size_t maxiter, double resth) {
     if (!d || d->n_total <= 0) return -1;
     HCHK(hipSetDevice(d->device));
@@ -3380,7 +3386,9 @@ __global__ void pg_iv_kernel(const double *__restrict__ theta, int P, int A, int
     }
 }
 
-int trpo_dev_pg_sums_fast(trpo_dev *d, const double *roll64, unsigned roll_gen, const double **zacc) {
+// allocation + the rollout rows of the tile kernel's policy-gradient mode (only when the rollout
+// changed); kept out of captured graphs
+int trpo_dev_pg_prepare(trpo_dev *d, const double *roll64, unsigned roll_gen) {
     if (!d->fast) return 1;
     HCHK(hipSetDevice(d->device));
     const int ld = 16 * d->pack.T[3];
@@ -3400,20 +3408,31 @@ int trpo_dev_pg_sums_fast(trpo_dev *d, const double *roll64, unsigned roll_gen, 
     const bool prep = d->pg_gen != roll_gen || d->pg_n != d->n;
     d->pg_gen = roll_gen;
     d->pg_n = d->n;
-    if (!d->pg_iv) HCHK(hipMalloc((void **)&d->pg_iv, d->esz * ld));
-    if (d->f64) {
-        if (prep)
+    if (!d->pg_iv) {
+        HCHK(hipMalloc((void **)&d->pg_iv, d->esz * ld));
+    }
+    if (prep) {
+        if (d->f64)
             hipLaunchKernelGGL(pg_prep_kernel<double>, dim3(cdiv((long)npad * ld, 256)), dim3(256), 0, d->stream,
                                roll64, (int)d->n, (int)npad, d->net.A, ld, (double *)d->pg_d, (double *)d->pg_adv);
-        hipLaunchKernelGGL(pg_iv_kernel<double>, dim3(1), dim3(cdiv(ld, 64) * 64), 0, d->stream, d->theta64, d->P,
-                           d->net.A, ld, (double *)d->pg_iv);
-    } else {
-        if (prep)
+        else
             hipLaunchKernelGGL(pg_prep_kernel<float>, dim3(cdiv((long)npad * ld, 256)), dim3(256), 0, d->stream,
                                roll64, (int)d->n, (int)npad, d->net.A, ld, (float *)d->pg_d, (float *)d->pg_adv);
+        HCHK(hipGetLastError());
+    }
+    return 0;
+}
+
+int trpo_dev_pg_sums_fast(trpo_dev *d, const double *roll64, unsigned roll_gen, const double **zacc) {
+    const int pr = trpo_dev_pg_prepare(d, roll64, roll_gen);
+    if (pr) return pr;
+    const int ld = 16 * d->pack.T[3];
+    if (d->f64)
+        hipLaunchKernelGGL(pg_iv_kernel<double>, dim3(1), dim3(cdiv(ld, 64) * 64), 0, d->stream, d->theta64, d->P,
+                           d->net.A, ld, (double *)d->pg_iv);
+    else
         hipLaunchKernelGGL(pg_iv_kernel<float>, dim3(1), dim3(cdiv(ld, 64) * 64), 0, d->stream, d->theta64, d->P,
                            d->net.A, ld, (float *)d->pg_iv);
-    }
     IterArgs a = plain_args(d, &d->ctl->zero);
     a.pg_d4 = reinterpret_cast<const float4 *>(d->pg_d);
     a.pg_adv = (const float *)d->pg_adv;
