@@ -36,7 +36,8 @@ int trpo_dev_download(trpo_dev *d, int slot, double *host);
 
 int trpo_dev_fvp(trpo_dev *d);                 /* enqueue z = F v  (slots V -> Z) */
 int trpo_dev_fvp_src(trpo_dev *d, const double *src);   /* enqueue z = F src (any device vector) -> Z */
-int trpo_dev_fvp_kernel(trpo_dev *d);          /* enqueue the dominant kernel alone */
+int trpo_dev_fvp_host(trpo_dev *d, double *host); /* z = F v (V -> Z) and z -> host, one wait */
+int trpo_dev_fvp_kernel(trpo_dev *d);         /* enqueue the dominant kernel alone */
 int trpo_dev_cg(trpo_dev *d, size_t maxiter, double resth); /* enqueue CG on slot B -> X */
 int trpo_dev_cg_history(trpo_dev *d, double *rdotr, double *xnorm, size_t cap, size_t *iters);
 int trpo_dev_sync(trpo_dev *d);

@@ -162,8 +162,7 @@ double trpo_ctx_fvp(trpo_ctx *c, const double *v, double *out) {
     if (!c || !v || !out) return TRPO_E_INVALID;
     const double t0 = now_s();
     int rc = trpo_dev_upload(c->dev, TRPO_VEC_V, v);
-    if (!rc) rc = trpo_dev_fvp(c->dev);
-    if (!rc) rc = trpo_dev_download(c->dev, TRPO_VEC_Z, out);
+    if (!rc) rc = trpo_dev_fvp_host(c->dev, out);
     if (rc) {
         set_err("FVP failed on the device (code %d)", rc);
         return rc < 0 ? rc : TRPO_E_DEVICE;

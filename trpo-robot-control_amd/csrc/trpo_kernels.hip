@@ -2021,8 +2021,11 @@ __global__ void fvp_epilogue_kernel(const double *__restrict__ zacc, const doubl
 // the same epilogue from R atomic replicas of the un-normalised sum (fixed replica order)
 // The replica set is left zeroed (each element by the thread that consumed it), so standalone FVPs
 // need no separate zeroing and the same launch sequence can be replayed from a graph.
+// zh (optional): a second copy of z into pinned, device-mapped host memory (the host-level FVP call
+// then needs no separate download copy)
 __global__ void acc_epilogue_kernel(double *__restrict__ acc, int R, const double *__restrict__ v,
-                                    double *__restrict__ z, int P, int nw, const Ctl *__restrict__ ctl) {
+                                    double *__restrict__ z, int P, int nw, const Ctl *__restrict__ ctl,
+                                    double *__restrict__ zh) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= P) return;
     double a[8];
@@ -2032,7 +2035,9 @@ __global__ void acc_epilogue_kernel(double *__restrict__ acc, int R, const doubl
 #pragma unroll
     for (int r = 1; r < 8; ++r) s += r < R ? a[r] : 0.0;
     const double vq = v[q];
-    z[q] = (q < nw ? s / ctl->n_total : 2.0 * vq) + ctl->damping * vq;
+    const double zq = (q < nw ? s / ctl->n_total : 2.0 * vq) + ctl->damping * vq;
+    z[q] = zq;
+    if (zh) zh[q] = zq;
     if (q < nw)
         for (int r = 0; r < R; ++r) acc[(long)r * P + q] = 0.0;
 }
@@ -2395,6 +2400,7 @@ struct trpo_dev {
     // pinned, device-mapped host staging for the host <-> device vector moves (kernel copies)
     double *hst, *hst_dev;
     size_t hst_cap;
+    int hst_pending;        // an upload's copy kernel may still read hst: sync before the host rewrites it
     // RCCL
     ncclComm_t comm;
     int rank, world;
@@ -2896,7 +2902,13 @@ __global__ void vcopy64_kernel(const double *__restrict__ src, double *__restric
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) dst[i] = src[i];
 }
-static int ensure_hst(trpo_dev *d, size_t count) {
+// host_writes: the caller is about to write the buffer from the host (an upload); device-side
+// writers (downloads) are ordered after a pending upload's copy by the stream and need no wait
+static int ensure_hst(trpo_dev *d, size_t count, bool host_writes = false) {
+    if (d->hst_pending && (host_writes || count > d->hst_cap || !d->hst)) {
+        HCHK(hipStreamSynchronize(d->stream));
+        d->hst_pending = 0;
+    }
     if (count <= d->hst_cap && d->hst) return 0;
     if (d->hst) hipHostFree(d->hst);
     d->hst = d->hst_dev = NULL;
@@ -2910,12 +2922,14 @@ static int ensure_hst(trpo_dev *d, size_t count) {
 extern "C" int trpo_dev_upload(trpo_dev *d, int slot, const double *host) {
     if (!d || slot < 0 || slot > 4 || !host) return -1;
     HCHK(hipSetDevice(d->device));
-    if (ensure_hst(d, (size_t)d->P + 2 * (size_t)(d->hist_cap + 8))) return -2;
+    if (ensure_hst(d, (size_t)d->P + 2 * (size_t)(d->hist_cap + 8), true)) return -2;
     memcpy(d->hst, host, sizeof(double) * d->P);
     hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, (const double *)d->hst_dev,
                        d->vec[slot], d->P);
     HCHK(hipGetLastError());
-    HCHK(hipStreamSynchronize(d->stream));        // the staging buffer is reused by the next move
+    // no wait here: the stream orders the copy before every later kernel, and the next host-side
+    // write to the staging buffer (ensure_hst) waits for it
+    d->hst_pending = 1;
     return 0;
 }
 
@@ -2927,6 +2941,7 @@ extern "C" int trpo_dev_download(trpo_dev *d, int slot, double *host) {
                        d->hst_dev, d->P);
     HCHK(hipGetLastError());
     HCHK(hipStreamSynchronize(d->stream));
+    d->hst_pending = 0;
     memcpy(host, d->hst, sizeof(double) * d->P);
     return 0;
 }
@@ -3012,11 +3027,15 @@ static int enqueue_fvp_core(trpo_dev *d, const double *src, const int *skip) {
     return 0;
 }
 
-// z = F src into slot Z (src: any device P-vector, e.g. slot X for the update's FVP(x))
-extern "C" int trpo_dev_fvp_src(trpo_dev *d, const double *src) {
+// z = F src into slot Z (src: any device P-vector, e.g. slot X for the update's FVP(x)); with
+// *zh != NULL the atomic-replica epilogue also writes z there (mapped host memory), otherwise
+// *zh is cleared and the caller downloads slot Z itself
+static int fvp_src(trpo_dev *d, const double *src, double **zh) {
     if (!d || !src) return -1;
     if (d->n_total <= 0) return -1;
     HCHK(hipSetDevice(d->device));
+    double *zhost = *zh;
+    *zh = NULL;
     if (d->fast && (d->atomic || !d->comm)) {
         // two launches: the tile kernel gathers its direction fragments from v itself, then the
         // atomic-replica or slab reduce applies the epilogue (under RCCL after the all-reduce)
@@ -3026,7 +3045,8 @@ extern "C" int trpo_dev_fvp_src(trpo_dev *d, const double *src) {
         if (acc) {
             if (allreduce(d, acc, (size_t)d->Rc * d->P)) return -4;
             hipLaunchKernelGGL(acc_epilogue_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, acc, d->Rc,
-                               src, d->vec[TRPO_VEC_Z], d->P, d->nw, d->ctl);
+                               src, d->vec[TRPO_VEC_Z], d->P, d->nw, d->ctl, zhost);
+            *zh = zhost;
         } else {
             launch_reduce(d, &d->ctl->zero, src, d->vec[TRPO_VEC_Z]);
         }
@@ -3044,7 +3064,28 @@ extern "C" int trpo_dev_fvp_src(trpo_dev *d, const double *src) {
     return 0;
 }
 
+extern "C" int trpo_dev_fvp_src(trpo_dev *d, const double *src) {
+    double *zh = NULL;
+    return fvp_src(d, src, &zh);
+}
+
 extern "C" int trpo_dev_fvp(trpo_dev *d) { return d ? trpo_dev_fvp_src(d, d->vec[TRPO_VEC_V]) : -1; }
+
+// z = F v (slot V -> slot Z) and z into host memory in one stream pass: the epilogue writes z
+// through the mapped staging buffer where it can, so the call waits once
+extern "C" int trpo_dev_fvp_host(trpo_dev *d, double *host) {
+    if (!d || !host) return -1;
+    HCHK(hipSetDevice(d->device));
+    if (ensure_hst(d, (size_t)d->P + 2 * (size_t)(d->hist_cap + 8))) return -2;
+    double *zh = d->hst_dev;                     // ordered after a pending upload's copy by the stream
+    int rc = fvp_src(d, d->vec[TRPO_VEC_V], &zh);
+    if (rc) return rc;
+    if (!zh) return trpo_dev_download(d, TRPO_VEC_Z, host);
+    HCHK(hipStreamSynchronize(d->stream));
+    d->hst_pending = 0;
+    memcpy(host, d->hst, sizeof(double) * d->P);
+    return 0;
+}
 
 extern "C" int trpo_dev_fvp_kernel(trpo_dev *d) {
     if (!d || d->n == 0) return -1;
@@ -3266,6 +3307,7 @@ extern "C" int trpo_dev_cg_history(trpo_dev *d, double *rdotr, double *xnorm, si
                        d->hst_dev + cw, hw);
     HCHK(hipGetLastError());
     HCHK(hipStreamSynchronize(d->stream));
+    d->hst_pending = 0;
     Ctl c;
     memcpy(&c, d->hst, sizeof c);
     const size_t n = (size_t)c.iter + 1;
