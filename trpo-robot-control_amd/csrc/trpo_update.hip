@@ -40,6 +40,8 @@ struct UpdState {
     double *sums = nullptr;                // [64]
     double *tpad = nullptr;                // register path: padded parameters [nk][PADW]
     size_t tpad_cap = 0;
+    double *tk = nullptr;                  // generic path: the line-search candidates [nk][P]
+    size_t tk_cap = 0;
     int lds_set = 0;
     // pinned, device-mapped host buffer: results are written into it by a kernel (no copy-engine
     // round trips through pageable memory); fullstep goes the other way through it
@@ -51,7 +53,7 @@ struct UpdState {
 void trpo_update_state_free(void *state) {
     UpdState *u = (UpdState *)state;
     if (!u) return;
-    void *ptrs[] = {u->roll, u->ws, u->slabs, u->sum, u->fs, u->sums, u->tpad};
+    void *ptrs[] = {u->roll, u->ws, u->slabs, u->sum, u->fs, u->sums, u->tpad, u->tk};
     for (void *p : ptrs)
         if (p) hipFree(p);
     if (u->hst) hipHostFree(u->hst);
@@ -95,6 +97,9 @@ constexpr int RS = UT + 1;
 
 // forward pass of sample s into Y rows (rows of layer i start at roff[i]);
 // src/TRPO_Update.c:262-293 / :954-976
+#ifndef FWD_JB
+#define FWD_JB 4            // outputs per sweep over a layer's inputs
+#endif
 template <class TH>
 __device__ void forward64(const Net &net, const TH &th, const double *__restrict__ obs, int s, bool live,
                           double *Y, const int *roff, int tid) {
@@ -103,7 +108,25 @@ __device__ void forward64(const Net &net, const TH &th, const double *__restrict
     for (int i = 0; i + 1 < net.nl; ++i) {
         const int in = net.L[i], out = net.L[i + 1], a = net.act[i + 1];
         const int wo = net.woff[i], bo = net.boff[i];
-        for (int j = 0; j < out; ++j) {
+        int j = 0;
+        // four outputs per sweep over the inputs: one LDS read of Y feeds four chains (each chain
+        // keeps the reference's bias-first, k-ascending order, so the sums are unchanged)
+        for (; j + FWD_JB <= out; j += FWD_JB) {
+            double x[FWD_JB];
+#pragma unroll
+            for (int jj = 0; jj < FWD_JB; ++jj) x[jj] = th[bo + j + jj];
+#pragma unroll 4
+            for (int k = 0; k < in; ++k) {
+                const double y = Y[(roff[i] + k) * RS + tid];
+                const int w = wo + k * out + j;
+#pragma unroll
+                for (int jj = 0; jj < FWD_JB; ++jj) x[jj] += y * th[w + jj];
+            }
+            double *Yo = Y + (roff[i + 1] + j) * RS + tid;
+#pragma unroll
+            for (int jj = 0; jj < FWD_JB; ++jj) Yo[jj * RS] = act_y64(a, x[jj]);
+        }
+        for (; j < out; ++j) {
             double x = th[bo + j];
 #pragma unroll 4
             for (int k = 0; k < in; ++k) x += Y[(roff[i] + k) * RS + tid] * th[wo + k * out + j];
@@ -305,11 +328,20 @@ __device__ __forceinline__ double lld_term(const double *rw, int A, int i, doubl
     return tx * tx - tn * tn + log(stdv) - logstd;
 }
 
-// Line-search surrogate: block (bx, k) sums Adv * exp(LLD) over its passes for candidate
-// theta + 2^-(k0+k) fullstep (src/TRPO_Update.c:951-981); parts[bx][k].
+// the nk line-search candidates theta + 2^-(k0+k) fullstep, k < nk, as [nk][P] (the same
+// ThetaStep expression the kernels would otherwise evaluate per weight access, once per element)
+__global__ void cand_theta_kernel(const double *__restrict__ th0, const double *__restrict__ fs, int k0, int P,
+                                  double *__restrict__ tk) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x, k = blockIdx.y;
+    const ThetaStep T{th0, fs, ldexp(1.0, -(k0 + k))};   // pow(0.5, k) exactly
+    if (i < P) tk[(long)k * P + i] = T[i];
+}
+
+// Line-search surrogate: block (bx, k) sums Adv * exp(LLD) over its passes for candidate k of
+// tk (src/TRPO_Update.c:951-981); parts[bx][k].
 __global__ void __launch_bounds__(UT)
-surr_kernel(Net net, const double *__restrict__ th0, const double *__restrict__ fs, int k0,
-            const double *__restrict__ obs, const double *__restrict__ roll, const double *__restrict__ stdv, int n,
+surr_kernel(Net net, const double *__restrict__ tk, const double *__restrict__ obs,
+            const double *__restrict__ roll, const double *__restrict__ stdv, int n,
             double *ws, int rows, int use_lds, double *__restrict__ parts) {
     extern __shared__ double lds64[];
     const int tid = threadIdx.x, k = blockIdx.y, nk = gridDim.y;
@@ -317,7 +349,7 @@ surr_kernel(Net net, const double *__restrict__ th0, const double *__restrict__ 
     int roff[MAXL + 1];
     row_offsets(net, roff);
     const int P = net.P, A = net.A, last = net.nl - 1;
-    const ThetaStep T{th0, fs, ldexp(1.0, -(k0 + k))};   // pow(0.5, k) exactly
+    const ThetaPlain T{tk + (long)k * P};
     double acc = 0.0;
     const int npass = (n + UT - 1) / UT;
     for (int pass = blockIdx.x; pass < npass; pass += gridDim.x) {
@@ -484,20 +516,32 @@ __global__ void export_solve_kernel(const double *__restrict__ b, const double *
 // Step size of src/TRPO_Update.c:834-868 on the device, in the host code's exact arithmetic
 // (sequential, unfused fp64: the host recomputes the same values from b, x, z bit for bit):
 // shs = 0.5 sum z_i x_i, lm = sqrt(shs / max_kl), fullstep = x / lm
-constexpr int STEP_PMAX = 4096;                  // LDS-staged products; larger P reads them from memory
+constexpr int STEP_CHUNK = 4096;                 // products staged in LDS per round
 __global__ void step_kernel(const double *__restrict__ x, const double *__restrict__ z, int P, double max_kl,
                             double *__restrict__ fs) {
     __shared__ double lm_s;
-    __shared__ double prod[STEP_PMAX];
-    // the products in parallel (each correctly rounded, as the host's z[i] * x[i]), then ONE thread
-    // sums them in index order (the host's order) out of LDS
-    for (int i = threadIdx.x; i < P && i < STEP_PMAX; i += blockDim.x) prod[i] = __dmul_rn(z[i], x[i]);
-    __syncthreads();
+    __shared__ double prod[STEP_CHUNK];
+    // per chunk: the products in parallel (each correctly rounded, as the host's z[i] * x[i]), then
+    // ONE thread adds them in index order (the host's order) out of LDS, 16 loads ahead of the adds
+    double shs = 0.0;
+    for (int c0 = 0; c0 < P; c0 += STEP_CHUNK) {
+        const int len = P - c0 < STEP_CHUNK ? P - c0 : STEP_CHUNK;
+        for (int i = threadIdx.x; i < len; i += blockDim.x) prod[i] = __dmul_rn(z[c0 + i], x[c0 + i]);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int i = 0;
+            for (; i + 16 <= len; i += 16) {
+                double t[16];
+#pragma unroll
+                for (int j = 0; j < 16; ++j) t[j] = prod[i + j];
+#pragma unroll
+                for (int j = 0; j < 16; ++j) shs = __dadd_rn(shs, t[j]);
+            }
+            for (; i < len; ++i) shs = __dadd_rn(shs, prod[i]);
+        }
+        __syncthreads();
+    }
     if (threadIdx.x == 0) {
-        double shs = 0.0;
-        int i = 0;
-        for (; i < P && i < STEP_PMAX; ++i) shs = __dadd_rn(shs, prod[i]);
-        for (; i < P; ++i) shs = __dadd_rn(shs, __dmul_rn(z[i], x[i]));
         shs = __dmul_rn(shs, 0.5);
         lm_s = sqrt(__ddiv_rn(shs, max_kl));
     }
@@ -723,12 +767,15 @@ static int enqueue_surrogate(trpo_dev *d, const double *fs, int k0, int nk) {
         hipLaunchKernelGGL(surr_reg_kernel, dim3(Gs, nk), dim3(UT), 0, v.stream, net, (const double *)u->tpad,
                            v.obs64, u->roll, v.std64, n, u->slabs);
     } else {
+        if (ensure(&u->tk, &u->tk_cap, (size_t)net.P * nk, v.stream)) return -2;
+        hipLaunchKernelGGL(cand_theta_kernel, dim3(cdiv(net.P, 256), nk), dim3(256), 0, v.stream, v.theta64, fs, k0,
+                           net.P, u->tk);
         const int rows = rows_for(net, false);
         int use_lds = 0;
         const int lds = act_storage(u, rows, (long)Gs * nk, v.stream, &use_lds);
         if (lds < 0) return -2;
-        hipLaunchKernelGGL(surr_kernel, dim3(Gs, nk), dim3(UT), lds, v.stream, net, v.theta64, fs, k0, v.obs64,
-                           u->roll, v.std64, n, u->ws, rows, use_lds, u->slabs);
+        hipLaunchKernelGGL(surr_kernel, dim3(Gs, nk), dim3(UT), lds, v.stream, net, (const double *)u->tk,
+                           v.obs64, u->roll, v.std64, n, u->ws, rows, use_lds, u->slabs);
     }
     hipLaunchKernelGGL(sum_slabs64_kernel, dim3(cdiv(nk, 16)), dim3(256), 0, v.stream, u->slabs, Gs, nk, u->sums);
     HCHK(hipGetLastError());
