@@ -175,19 +175,19 @@ def cpu_baseline(theta, obs_all, b, gpu_x):
     return res, rel
 
 
-def bench_update(device, n=N_TOTAL, reps=20):
+def bench_update(device, L=ARM, n=N_TOTAL, reps=20, cpu_ref=True):
     """One full TRPO policy update (src/TRPO_Update.c: policy gradient, 10-iteration CG, FVP(x),
-    line search) on a synthetic armDOF_0 rollout, host-visible wall time per update (includes the
-    host round trips of x / z / the line-search scalars); CPU reference TRPO_Update timed beside it."""
+    line search) on a synthetic rollout of policy L, host-visible wall time per update (includes the
+    host round trips of x / z / the line-search scalars); CPU reference TRPO_Update timed beside it
+    (cpu_ref)."""
     import oracle
-    L = ARM
     theta = synth.make_theta(L)
     obs = synth.make_obs(n, L[0])
     std = np.ones(L[-1])
     mean, action, adv = synth.make_rollout(L, "lttl", theta, obs, std)
     ctx = trpo_amd.Context(L, "lttl", theta, obs, std, DAMPING, device=device)
     ctx.set_rollout(mean, action, adv)
-    for _ in range(3):      # warm-up: eager first call, then the one-off capture of the update graph
+    for _ in range(3):      # warm-up: first-call allocations, CG graph capture
         r = ctx.update()
     t0 = time.perf_counter()
     for _ in range(reps):
@@ -196,7 +196,7 @@ def bench_update(device, n=N_TOTAL, reps=20):
     ctx.close()
     out = {"update_ms": 1e3 * wall, "accepted": r["accepted"], "cg_iters": int(r["cg_iters"]),
            "samples": n, "what": "policy gradient (fp32 tile kernel, fp64 sums) + CG(10, 1e-10) + FVP(x) + fp64 line search"}
-    if os.path.exists(oracle.REF_DRIVER_FAST):
+    if cpu_ref and os.path.exists(oracle.REF_DRIVER_FAST):
         with tempfile.TemporaryDirectory() as tmp:
             mf, df, of = (os.path.join(tmp, f) for f in ("m.txt", "d.txt", "o.txt"))
             synth.write_model_file(mf, theta)
@@ -352,6 +352,7 @@ def main():
                           "peak_fp64_mfma_tflops": PEAK_FP64_TFLOPS}
             cf.close()
         extra["C5_update_armDOF_0_N50000"] = bench_update(device)
+        extra["C5_update_2x64_N50000"] = bench_update(device, L=[15, 64, 64, 3], cpu_ref=False)
         extra["C5_baseline_evaluate_N3000"] = bench_baseline(device)
         result["extra"] = extra
 

@@ -16,7 +16,7 @@ std = np.ones(3)
 mean, action, adv = synth.make_rollout(L, "lttl", th, obs, std)
 with trpo_amd.Context(L, "lttl", th, obs, std) as ctx:
     ctx.set_rollout(mean, action, adv)
-    for _ in range(3):            # warm: the first call runs eagerly, the second captures the update graph
+    for _ in range(3):            # warm: first-call allocations, CG graph capture
         ctx.update()
     t0 = time.perf_counter()
     for _ in range(reps):
