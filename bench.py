@@ -6,51 +6,65 @@ BASELINE.json metric "FVP samples/sec + 10-iter CG wall time, armDOF_0 policy,
 so exactly 10 Fisher-vector products + the fp64 CG vector updates) over a
 synthetic armDOF_0 batch of 50 000 samples resident in HBM (SURVEY.md §8d,
 configs C3/C4).  With --gpus N the 50 000 samples are split into contiguous
-shards, one per rank, and every FVP all-reduces the P-sized partial sum over
-RCCL (strong scaling, config C4).
+shards, one per rank (one process per GPU), and every FVP all-reduces the
+P-sized partial sum over RCCL (strong scaling, config C4).
 
     python bench.py                      # N=1
+    python bench.py --gpus 8             # launches 8 rank processes itself
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
 Rank 0 prints ONE JSON line.  value = 10 * 50 000 / (seconds per solve), the
-whole-job FVP throughput; ms_per_step = the CG wall time.
+whole-job FVP throughput; ms_per_step = the CG wall time (max over ranks).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
 import subprocess
 import sys
 import tempfile
 import time
 
-import numpy as np
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
-sys.path[:0] = [os.path.join(ROOT, "trpo-robot-control_amd"), os.path.join(ROOT, "oracle")]
-
-import trpo_amd  # noqa: E402
-from trpo_amd import synth  # noqa: E402
 
 ARM = [15, 16, 16, 3]
 N_TOTAL = 50_000
-PEAK_FP64_TFLOPS = 78.6       # MI355X dense fp64 matrix (AMD spec sheet; the guide lists fp32/bf16 only)
 CG_ITERS = 10
 DAMPING = 0.1
 PEAK_FP32_TFLOPS = 157.3     # MI355X dense FP32 (vector = matrix), MI355X_MICROARCH.md
+PEAK_FP64_TFLOPS = 78.6      # MI355X dense fp64 matrix (AMD spec sheet; the guide lists fp32/bf16 only)
 PEAK_HBM_GBS = 8000.0
+SWEEP_N = (500_000, 4_000_000)   # SURVEY §8d C4: the latency crossover of the sharded solve
+
+
+def parse_args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the secondary configs (C2, C3 2x64, fp64, C5, baseline, N sweep)")
+    return ap.parse_args()
+
+
+def relaunch(args) -> int:
+    """--gpus N without a torch.distributed environment: start N rank processes (one per GPU) with
+    torch.distributed.run and exit with its code.  Nothing in this process has touched HIP."""
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
 
 
 def flops_per_sample(L):
     """2(5S - 2 L0 L1) + 7(L1 + L2) + 2 L3, S = sum L_i L_{i+1}."""
     S = sum(L[i] * L[i + 1] for i in range(len(L) - 1))
     return 2 * (5 * S - 2 * L[0] * L[1]) + 7 * sum(L[1:-1]) + 2 * L[-1]
-
-
-def bytes_per_fvp(L, n):
-    """observations read once + v in, Fv out, theta read once (fp32)."""
-    return 4 * n * L[0] + 12 * synth.num_params(L)
 
 
 def flops_per_sample_cached(L):
@@ -61,33 +75,39 @@ def flops_per_sample_cached(L):
     return 2 * (4 * S - 2 * L[0] * L[1]) + 7 * sum(L[1:-1]) + 2 * L[-1]
 
 
+def num_params(L):
+    return sum(L[i] * L[i + 1] + L[i + 1] for i in range(len(L) - 1)) + L[-1]
+
+
 def bytes_per_fvp_cached(L, n):
     """observations + the cached y1, y2 (fp32) read once, v in, Fv out, theta (188 B/sample armDOF_0)."""
-    return 4 * n * (L[0] + sum(L[1:-1])) + 12 * synth.num_params(L)
+    return 4 * n * (L[0] + sum(L[1:-1])) + 12 * num_params(L)
 
 
-from trpo_amd.dist import shard_range as shard  # noqa: E402
+def bytes_cg_step(L):
+    """The fp64 CG step fused into the CG-iteration kernel, each P-vector touched once: z, p, r, x in,
+    p, r, x and the new basis vector out."""
+    return 8 * 8 * num_params(L)
 
 
 class Dist:
-    """torch.distributed (gloo) only for bootstrap, barriers and the max-over-ranks
-    timing; the data path all-reduce is RCCL inside libtrpo_mi355x.so."""
+    """torch.distributed (gloo) only for bootstrap, barriers and the max-over-ranks timing; the
+    data-path all-reduce is RCCL inside libtrpo_mi355x.so."""
 
     def __init__(self):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-        self.pg = None
         if self.world > 1:
             import torch.distributed as dist
             dist.init_process_group("gloo")
             self.dist = dist
 
     def barrier(self):
-        if self.pg is None and self.world > 1:
+        if self.world > 1:
             self.dist.barrier()
 
-    def bcast_bytes(self, b: bytes | None) -> bytes:
+    def bcast_bytes(self, b):
         if self.world == 1:
             return b
         obj = [b]
@@ -108,15 +128,22 @@ class Dist:
 
 
 def make_ctx(L, n_total, dist, device, precision=None):
+    """This rank's context: all weights, its contiguous shard of the seeded observation stream."""
+    import numpy as np
+    import trpo_amd
+    from trpo_amd import synth
+    from trpo_amd.dist import shard_range
     theta = synth.make_theta(L)
-    obs_all = synth.make_obs(n_total, L[0])
-    lo, hi = shard(n_total, dist.rank, dist.world)
-    ctx = trpo_amd.Context(L, "lttl", theta, obs_all[lo:hi], np.ones(L[-1]), DAMPING, device=device,
-                           precision=precision)
+    lo, hi = shard_range(n_total, dist.rank, dist.world)
+    obs = synth.make_obs(hi - lo, L[0], start=lo)
+    ctx = trpo_amd.Context(L, "lttl", theta, obs, np.ones(L[-1]), DAMPING, device=device, precision=precision)
     if dist.world > 1:
         uid = dist.bcast_bytes(trpo_amd.unique_id() if dist.rank == 0 else None)
         ctx.attach_comm(dist.rank, dist.world, uid)
-    return ctx, theta, obs_all
+        info = ctx.comm_info()
+        if info["world"] != dist.world:
+            raise SystemExit("RCCL communicator has %d ranks, expected %d" % (info["world"], dist.world))
+    return ctx, theta, obs
 
 
 def time_steps(ctx, dist, steps, warmup, b):
@@ -134,53 +161,82 @@ def time_steps(ctx, dist, steps, warmup, b):
     return dist.max(t1 - t0)
 
 
-def cpu_baseline(theta, obs_all, b, gpu_x):
-    """The reference's own CG (oracle/_ref, compiled from src/TRPO_FVP.c + TRPO_CG.c with
-    the Makefile.cpuonly flags) on 1 host core, full 10-iteration solve at N=50k; falls back
-    to the clean-room port (oracle/liboracle.so) when oracle/_ref was not built."""
+def cpu_rows(theta, obs_all, b, threads_all):
+    """The reference itself (oracle/_ref/ref_driver_fast: src/TRPO_FVP.c + TRPO_CG.c compiled with the
+    Makefile.cpuonly flags, -march=x86-64-v3) on this host: returns (headline, rows, x_ref)."""
+    import numpy as np
     import oracle
+    from trpo_amd import synth
     n = obs_all.shape[0]
-    res = dict(unit="FVP samples/s", cores=1,
-               sample="one full 10-iteration CG solve, armDOF_0, N=50000, ResidualTh=0, 1 thread")
-    x_ref = None
-    if os.path.exists(oracle.REF_DRIVER_FAST):
-        with tempfile.TemporaryDirectory() as tmp:
-            mf, df, bf, xf = (os.path.join(tmp, f) for f in ("m.txt", "d.txt", "b.txt", "x.txt"))
-            synth.write_model_file(mf, theta)
-            synth.write_data_file(df, obs_all, np.ones(ARM[-1]))
-            synth.write_vector_file(bf, b)
-            cmd = [oracle.REF_DRIVER_FAST, "cg", mf, df, str(n), ",".join(map(str, ARM)), "lttl", str(DAMPING), bf,
-                   str(CG_ITERS), "0", xf, "1"]
-            w0 = time.perf_counter()
-            out = subprocess.run(cmd, capture_output=True, text=True)
-            wall = time.perf_counter() - w0
-            if out.returncode == 0:
-                x_ref = np.loadtxt(xf)
-                # compute seconds exclude the reference's per-call file parsing: time it separately
-                tcmd = [oracle.REF_DRIVER_FAST, "time", mf, df, str(n), ",".join(map(str, ARM)), "lttl",
-                        str(DAMPING), bf, str(CG_ITERS), "0", "1"]
-                tout = subprocess.run(tcmd, capture_output=True, text=True)
-                tj = json.loads(tout.stderr.strip().splitlines()[-1])
-                res.update(kind="reference", value=CG_ITERS * n / tj["compute_s"], compute_s=tj["compute_s"],
-                           wall_s_incl_file_parse=tj["wall_s"])
-    if x_ref is None:
-        r = oracle.cg(ARM, "lttl", theta, obs_all, np.ones(ARM[-1]), b, CG_ITERS, 0.0, DAMPING, threads=1)
-        x_ref = r["x"]
-        res.update(kind="port", value=CG_ITERS * n / r["seconds"], compute_s=r["seconds"])
+    flags = "gcc -O3 -march=x86-64-v3 -fopenmp (Makefile.cpuonly flags, portable -march)"
     try:
-        res["cpu_model"] = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if "model name" in l][0]
+        cpu_model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if "model name" in l][0]
     except Exception:
-        pass
-    rel = float(np.linalg.norm(gpu_x - x_ref) / np.linalg.norm(x_ref))
-    return res, rel
+        cpu_model = None
+    rows = []
+    if not os.path.exists(oracle.REF_DRIVER_FAST):
+        r = oracle.cg(ARM, "lttl", theta, obs_all, np.ones(ARM[-1]), b, CG_ITERS, 0.0, DAMPING, threads=1)
+        head = dict(value=CG_ITERS * n / r["seconds"], unit="FVP samples/s", cores=1, kind="port",
+                    sample="one 10-iteration CG solve, armDOF_0, N=%d, ResidualTh=0, clean-room port, 1 thread" % n,
+                    compute_s=r["seconds"], cpu_model=cpu_model)
+        return head, rows, r["x"]
+
+    def run(mode, mf, df, nn, vec, extra, threads):
+        cmd = [oracle.REF_DRIVER_FAST, mode, mf, df, str(nn), ",".join(map(str, ARM)), "lttl", str(DAMPING), vec]
+        cmd += extra + [str(threads)]
+        p = subprocess.run(cmd, capture_output=True, text=True)
+        if p.returncode != 0:
+            raise RuntimeError("%s failed: %s" % (mode, p.stderr[-400:]))
+        return json.loads(p.stderr.strip().splitlines()[-1])
+
+    with tempfile.TemporaryDirectory() as tmp:
+        mf, df, bf, xf = (os.path.join(tmp, f) for f in ("m.txt", "d.txt", "b.txt", "x.txt"))
+        synth.write_model_file(mf, theta)
+        synth.write_data_file(df, obs_all, np.ones(ARM[-1]))
+        synth.write_vector_file(bf, b)
+        t1 = run("cg", mf, df, n, bf, [str(CG_ITERS), "0", xf], 1)
+        x_ref = np.loadtxt(xf)
+        head = dict(value=CG_ITERS * n / t1["compute_s"], unit="FVP samples/s", cores=1, kind="reference",
+                    sample="one 10-iteration CG solve (the reference's CG, src/TRPO_CG.c), armDOF_0, N=%d, "
+                           "ResidualTh=0, NumThreads=1; compute seconds as CG returns them (file parsing excluded)"
+                           % n,
+                    compute_s=t1["compute_s"], wall_s_incl_file_parse=t1["wall_s"], build=flags, cpu_model=cpu_model)
+        rows.append(dict(config="C3 CG10 armDOF_0 N=%d" % n, threads=1, compute_s=t1["compute_s"],
+                         fvp_samples_per_s=CG_ITERS * n / t1["compute_s"]))
+        # all host cores: the reference's per-neuron OpenMP fork/join anti-scales (SURVEY §3.3), so a
+        # bounded sample -- the first 5 000 samples, one 10-iteration solve -- keeps this row to seconds
+        ns = min(n, 5000)
+        df5 = os.path.join(tmp, "d5.txt")
+        synth.write_data_file(df5, obs_all[:ns], np.ones(ARM[-1]))
+        ta = run("time", mf, df5, ns, bf, [str(CG_ITERS), "0"], threads_all)
+        rows.append(dict(config="C3 CG10 armDOF_0 N=%d (bounded sample of the N=%d workload)" % (ns, n),
+                         threads=threads_all, compute_s=ta["compute_s"],
+                         fvp_samples_per_s=CG_ITERS * ns / ta["compute_s"]))
+    # C1: the reference's own fixtures (ArmTest{Model,Data,FVP,CG}.txt, N=3150), 1 thread and all cores
+    g = os.path.join(ROOT, "tests", "golden")
+    mfix, dfix = os.path.join(g, "ArmTestModel.txt"), os.path.join(g, "ArmTestData.txt")
+    with tempfile.TemporaryDirectory() as tmp:
+        vf, bf2, of = (os.path.join(tmp, f) for f in ("v.txt", "b.txt", "o.txt"))
+        synth.write_vector_file(vf, np.loadtxt(os.path.join(g, "ArmTestFVP.txt"))[:, 0])
+        synth.write_vector_file(bf2, np.loadtxt(os.path.join(g, "ArmTestCG.txt"))[:, 0])
+        for th in (1, threads_all):
+            tf = run("fvp", mfix, dfix, 3150, vf, [of], th)
+            tc = run("time", mfix, dfix, 3150, bf2, ["10", "1e-10"], th)
+            rows.append(dict(config="C1 fixture FVPFast N=3150", threads=th, compute_s=tf["compute_s"],
+                             fvp_samples_per_s=3150 / tf["compute_s"]))
+            rows.append(dict(config="C1 fixture CG(10, 1e-10) N=3150 (8 FVPs)", threads=th,
+                             compute_s=tc["compute_s"], fvp_samples_per_s=8 * 3150 / tc["compute_s"]))
+    return head, rows, x_ref
 
 
 def bench_update(device, L=ARM, n=N_TOTAL, reps=20, cpu_ref=True):
     """One full TRPO policy update (src/TRPO_Update.c: policy gradient, 10-iteration CG, FVP(x),
     line search) on a synthetic rollout of policy L, host-visible wall time per update (includes the
-    host round trips of x / z / the line-search scalars); CPU reference TRPO_Update timed beside it
-    (cpu_ref)."""
+    host round trips of x / z / the line-search scalars); CPU reference TRPO_Update timed beside it."""
+    import numpy as np
     import oracle
+    import trpo_amd
+    from trpo_amd import synth
     theta = synth.make_theta(L)
     obs = synth.make_obs(n, L[0])
     std = np.ones(L[-1])
@@ -194,8 +250,8 @@ def bench_update(device, L=ARM, n=N_TOTAL, reps=20, cpu_ref=True):
         r = ctx.update()
     wall = (time.perf_counter() - t0) / reps
     ctx.close()
-    out = {"update_ms": 1e3 * wall, "accepted": r["accepted"], "cg_iters": int(r["cg_iters"]),
-           "samples": n, "what": "policy gradient (fp32 tile kernel, fp64 sums) + CG(10, 1e-10) + FVP(x) + fp64 line search"}
+    out = {"update_ms": 1e3 * wall, "accepted": r["accepted"], "cg_iters": int(r["cg_iters"]), "samples": n,
+           "what": "policy gradient (fp32 tile kernel, fp64 sums) + CG(10, 1e-10) + FVP(x) + fp64 line search"}
     if cpu_ref and os.path.exists(oracle.REF_DRIVER_FAST):
         with tempfile.TemporaryDirectory() as tmp:
             mf, df, of = (os.path.join(tmp, f) for f in ("m.txt", "d.txt", "o.txt"))
@@ -219,7 +275,10 @@ def bench_baseline(device, num_ep=20, ep_len=150, reps=50):
     """One value-baseline objective + gradient evaluation (src/TRPO_Baseline.c evaluate(), the
     L-BFGS callback) on the reference's own batch shape (20 episodes x 150 steps, [16,16,16,1]),
     device-resident data; the clean-room CPU port timed beside it (1 core)."""
+    import numpy as np
     import oracle
+    import trpo_amd
+    from trpo_amd import synth
     L = [16, 16, 16, 1]
     x, obs, tgt = synth.make_baseline_problem(L, num_ep, ep_len)
     with trpo_amd.Baseline(L, "lttl", device=device) as b:
@@ -237,22 +296,74 @@ def bench_baseline(device, num_ep=20, ep_len=150, reps=50):
             "what": "host-visible wall per L-BFGS callback incl. x upload and g/f download"}
 
 
+def extras_single(device, dist, reps):
+    """Secondary configs at N=1 (SURVEY §8d C2, C3 for the 2x64 MLP, the fp64 mode, C5)."""
+    from trpo_amd import synth
+    extra = {}
+    L2 = [15, 64, 64, 3]
+    c2res = {}
+    for tag, env in (("", None), ("_recompute", "0")):
+        # C2: repeated FVP calls on one context reuse the forward-activation cache (theta unchanged);
+        # a first call after set_theta recomputes the forward pass -- timed too (TRPO_YCACHE=0)
+        if env is not None:
+            os.environ["TRPO_YCACHE"] = env
+        c2, _, _ = make_ctx(L2, 4096, dist, device)
+        os.environ.pop("TRPO_YCACHE", None)
+        c2.upload_v(synth.make_v(num_params(L2)))
+        k2 = c2.time_ms(0, reps)
+        f2 = c2.time_ms(1, reps)
+        fl = flops_per_sample_cached(L2) if env is None else flops_per_sample(L2)
+        c2res.update({"fvp_ms" + tag: f2, "kernel_ms" + tag: k2, "fvp_samples_per_s" + tag: 4096 / (f2 * 1e-3),
+                      "kernel_tflops" + tag: fl * 4096 / (k2 * 1e-3) / 1e12})
+        c2.close()
+    extra["C2_fvp_2x64_N4096"] = c2res
+    for key, L, prec in (("C3_cg10_2x64_N50000", L2, None),
+                         ("C3_cg10_armDOF_0_N50000_fp64", ARM, "fp64"), ("C3_cg10_2x64_N50000_fp64", L2, "fp64")):
+        c3, _, _ = make_ctx(L, N_TOTAL, dist, device, precision=prec)
+        t3 = time_steps(c3, dist, 20, 3, synth.make_b(num_params(L)))
+        k3 = c3.time_ms(3, 10, CG_ITERS)
+        extra[key] = {"cg_wall_ms": 1e3 * t3 / 20, "fvp_samples_per_s": CG_ITERS * N_TOTAL / (t3 / 20),
+                      "cg_iter_kernel_ms": k3, "kernel": c3.kernel_name + " (CG-iteration kernel, cached forward)",
+                      "kernel_tflops": flops_per_sample_cached(L) * N_TOTAL / (k3 * 1e-3) / 1e12,
+                      "kernel_tflops_recompute_equiv": flops_per_sample(L) * N_TOTAL / (k3 * 1e-3) / 1e12,
+                      "peak_tflops": PEAK_FP64_TFLOPS if prec == "fp64" else PEAK_FP32_TFLOPS}
+        c3.close()
+    extra["C5_update_armDOF_0_N50000"] = bench_update(device)
+    extra["C5_update_2x64_N50000"] = bench_update(device, L=L2, cpu_ref=False)
+    extra["C5_baseline_evaluate_N3000"] = bench_baseline(device)
+    return extra
+
+
+def sweep(device, dist, steps=10):
+    """C4's N sweep: the same sharded 10-iteration solve at larger batches (whole-job rates)."""
+    from trpo_amd import synth
+    out = {}
+    for n in SWEEP_N:
+        ctx, _, _ = make_ctx(ARM, n, dist, device)
+        t = time_steps(ctx, dist, steps, 2, synth.make_b(num_params(ARM)))
+        out["cg10_armDOF_0_N%d" % n] = {"ms_per_step": 1e3 * t / steps,
+                                        "fvp_samples_per_s": CG_ITERS * n / (t / steps), "n_gpus": dist.world}
+        ctx.close()
+    return out
+
+
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--extra", action="store_true", help="also time the 2x64 configs (C2/C3)")
-    args = ap.parse_args()
+    args = parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(relaunch(args))
+    sys.path[:0] = [os.path.join(ROOT, "trpo-robot-control_amd"), os.path.join(ROOT, "oracle")]
+    import numpy as np
+    from trpo_amd import synth
 
     dist = Dist()
-    if dist.world != args.gpus and dist.rank == 0:
-        print("warning: --gpus %d but WORLD_SIZE=%d" % (args.gpus, dist.world), file=sys.stderr)
+    if dist.world != args.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, dist.world), file=sys.stderr)
+        sys.exit(2)
     device = int(os.environ.get("TRPO_BENCH_DEVICE", dist.local_rank))   # override: testing only
 
-    ctx, theta, obs_all = make_ctx(ARM, N_TOTAL, dist, device)
-    P = synth.num_params(ARM)
+    ctx, theta, obs_local = make_ctx(ARM, N_TOTAL, dist, device)
+    comm = ctx.comm_info()
+    P = num_params(ARM)
     b = synth.make_b(P)
 
     t = time_steps(ctx, dist, args.steps, args.warmup, b)
@@ -260,22 +371,21 @@ def main():
     value = CG_ITERS * N_TOTAL / (t / args.steps)
     x = ctx.download_x()
 
-    # dominant kernel: the fused FVP kernel, timed with HIP events on the context's stream
+    # the dominant kernel: the fused CG-iteration kernel (9 of the 10 launches of a solve), timed alone
+    # with HIP events on the context's stream, averaged over the iterations K_1..K_9 of a solve
+    reps = 20
+    k3 = ctx.time_ms(3, reps, CG_ITERS)
     ctx.upload_v(synth.make_v(P))
-    reps = 200
-    k_ms = ctx.time_ms(0, reps)
-    fvp_ms = ctx.time_ms(1, reps)
+    k2 = ctx.time_ms(0, 200)                     # the standalone FVP kernel (no CG step), secondary
     n_local = ctx.n
-    # the kernel timed is the one 9 of the 10 FVPs of a solve run: the cached-forward variant
-    # (MODE 2); its algorithmic work is its own (fewer flops, the cache's bytes counted)
     flops = flops_per_sample_cached(ARM) * n_local
-    bytes_alg = bytes_per_fvp_cached(ARM, n_local)
-    achieved_tflops = flops / (k_ms * 1e-3) / 1e12
-    achieved_gbs = bytes_alg / (k_ms * 1e-3) / 1e9
+    bytes_alg = bytes_per_fvp_cached(ARM, n_local) + bytes_cg_step(ARM)
+    achieved_gbs = bytes_alg / (k3 * 1e-3) / 1e9
+    achieved_tflops = flops / (k3 * 1e-3) / 1e12
     hbm_bound = bytes_alg / (PEAK_HBM_GBS * 1e9) >= flops / (PEAK_FP32_TFLOPS * 1e12)
 
     traffic = None
-    tpath = os.environ.get("TRPO_TRAFFIC_JSON", os.path.join(ROOT, "profiles", "r01_fvp_traffic.json"))
+    tpath = os.environ.get("TRPO_TRAFFIC_JSON", os.path.join(ROOT, "profiles", "r02_cgiter_traffic.json"))
     if os.path.exists(tpath) and dist.world == 1:
         # HBM bytes per launch of this kernel at this workload, from the committed rocprofv3 PMC passes
         traffic = json.load(open(tpath))["traffic_bytes"]
@@ -294,71 +404,38 @@ def main():
         "dtype": "fp32",
         "data": "synthetic (seeded splitmix64, SURVEY §8d)",
         "config": {"workload": "cg10_armDOF_0_N50000", "policy": "armDOF_0 [15,16,16,3] lttl",
-                   "samples": N_TOTAL, "cg_iters": CG_ITERS, "residual_th": 0.0, "damping": DAMPING,
+                   "samples": N_TOTAL, "samples_per_rank": n_local, "cg_iters": CG_ITERS, "residual_th": 0.0,
+                   "damping": DAMPING,
                    "parallelism": "dp%d (contiguous sample shards, RCCL all-reduce per FVP)" % dist.world,
                    "cg_scalars": "fp64", "fvp_kernel": ctx.kernel_name, "geometry": ctx.geometry},
+        "comm": {"backend": "rccl" if dist.world > 1 else "none", "ranks": comm["world"],
+                 "replicas_per_fvp": comm["replicas"]},
         "cg_wall_ms": ms_per_step,
-        "fvp_ms": fvp_ms,
         "roofline": {"bound": "hbm" if hbm_bound else "mfma",
                      "achieved": achieved_gbs if hbm_bound else achieved_tflops,
                      "peak": PEAK_HBM_GBS if hbm_bound else PEAK_FP32_TFLOPS,
                      "unit": "GB/s" if hbm_bound else "TFLOP/s",
                      "frac": achieved_gbs / PEAK_HBM_GBS if hbm_bound else achieved_tflops / PEAK_FP32_TFLOPS,
                      "traffic": traffic,
-                     "kernel": "fvp_mlp3_kernel (MODE 2: cached forward)", "kernel_ms": k_ms,
-                     "flops_per_launch": flops, "alg_bytes_per_launch": bytes_alg,
+                     "kernel": "fvp_mlp3_kernel MODE 3 (CG-iteration kernel: fp64 CG step + cached-forward FVP)",
+                     "kernel_ms": k3, "flops_per_launch": flops, "alg_bytes_per_launch": bytes_alg,
                      "fp32_tflops": achieved_tflops, "fp32_frac": achieved_tflops / PEAK_FP32_TFLOPS,
                      "hbm_gbs_algorithmic": achieved_gbs, "hbm_frac_algorithmic": achieved_gbs / PEAK_HBM_GBS,
-                     "full_recompute_equiv_tflops": flops_per_sample(ARM) * n_local / (k_ms * 1e-3) / 1e12},
+                     "full_recompute_equiv_tflops": flops_per_sample(ARM) * n_local / (k3 * 1e-3) / 1e12,
+                     "secondary_fvp_kernel_mode2_ms": k2},
     }
 
-    if args.extra and dist.world == 1:
-        extra = {}
-        L2 = [15, 64, 64, 3]
-        # C2: repeated FVP calls on one context reuse the forward-activation cache (theta unchanged);
-        # a first call after set_theta recomputes the forward pass -- timed too (TRPO_YCACHE=0)
-        c2res = {}
-        for tag, env in (("", None), ("_recompute", "0")):
-            if env is not None:
-                os.environ["TRPO_YCACHE"] = env
-            c2, th2, obs2 = make_ctx(L2, 4096, dist, device)
-            os.environ.pop("TRPO_YCACHE", None)
-            c2.upload_v(synth.make_v(synth.num_params(L2)))
-            k2 = c2.time_ms(0, reps)
-            f2 = c2.time_ms(1, reps)
-            fl = flops_per_sample_cached(L2) if env is None else flops_per_sample(L2)
-            c2res.update({"fvp_ms" + tag: f2, "kernel_ms" + tag: k2, "fvp_samples_per_s" + tag: 4096 / (f2 * 1e-3),
-                          "kernel_tflops" + tag: fl * 4096 / (k2 * 1e-3) / 1e12})
-            c2.close()
-        extra["C2_fvp_2x64_N4096"] = c2res
-        c3, th3, obs3 = make_ctx(L2, N_TOTAL, dist, device)
-        t3 = time_steps(c3, dist, 20, 3, synth.make_b(synth.num_params(L2)))
-        k3 = c3.time_ms(0, reps)
-        extra["C3_cg10_2x64_N50000"] = {"cg_wall_ms": 1e3 * t3 / 20, "fvp_samples_per_s": CG_ITERS * N_TOTAL / (t3 / 20),
-                                        "kernel_ms": k3, "kernel": c3.kernel_name + " (cached forward)",
-                                        "kernel_tflops": flops_per_sample_cached(L2) * N_TOTAL / (k3 * 1e-3) / 1e12,
-                                        "kernel_tflops_recompute_equiv":
-                                            flops_per_sample(L2) * N_TOTAL / (k3 * 1e-3) / 1e12}
-        c3.close()
-        # fp64 precision mode (the reference's arithmetic, fp64 MFMA): same CG(10) workloads
-        for key, L in (("C1_cg10_armDOF_0_N50000_fp64", [15, 16, 16, 3]), ("C3_cg10_2x64_N50000_fp64", L2)):
-            cf, _, _ = make_ctx(L, N_TOTAL, dist, device, precision="fp64")
-            tf = time_steps(cf, dist, 20, 3, synth.make_b(synth.num_params(L)))
-            kf = cf.time_ms(0, reps)
-            extra[key] = {"cg_wall_ms": 1e3 * tf / 20, "fvp_samples_per_s": CG_ITERS * N_TOTAL / (tf / 20),
-                          "kernel": cf.kernel_name + " (cached forward)", "kernel_ms": kf,
-                          "kernel_tflops": flops_per_sample_cached(L) * N_TOTAL / (kf * 1e-3) / 1e12,
-                          "kernel_tflops_recompute_equiv": flops_per_sample(L) * N_TOTAL / (kf * 1e-3) / 1e12,
-                          "peak_fp64_mfma_tflops": PEAK_FP64_TFLOPS}
-            cf.close()
-        extra["C5_update_armDOF_0_N50000"] = bench_update(device)
-        extra["C5_update_2x64_N50000"] = bench_update(device, L=[15, 64, 64, 3], cpu_ref=False)
-        extra["C5_baseline_evaluate_N3000"] = bench_baseline(device)
-        result["extra"] = extra
+    if not args.no_extra:
+        if dist.world == 1:
+            result["extra"] = extras_single(device, dist, 200)
+        result.setdefault("extra", {})["C4_sweep"] = sweep(device, dist)
 
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
-        cb, rel = cpu_baseline(theta, obs_all, b, x)
-        result["cpu_baseline"] = cb
+        threads_all = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+        head, rows, x_ref = cpu_rows(theta, obs_local, b, threads_all)
+        head["rows"] = rows
+        result["cpu_baseline"] = head
+        rel = float(np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref))
         result["parity"] = {"cg_step_relL2_vs_cpu": rel, "tolerance": 1e-4}
     ctx.close()
     dist.close()

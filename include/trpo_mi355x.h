@@ -130,6 +130,21 @@ size_t trpo_ctx_num_params(const trpo_ctx *ctx);
 int trpo_comm_unique_id(void *unique_id_128);
 int trpo_ctx_attach_comm(trpo_ctx *ctx, int rank, int world, const void *unique_id_128);
 
+/* In-process sharding without RCCL: `world` contexts of ONE process, each driven by its own
+ * thread (any devices, the same one included), attach to a host group and run the sharded code
+ * path with a host-staged all-reduce (rank-order sums: identical bits on every rank).  Meant for
+ * tests and debugging of the multi-rank logic on one GPU; CG runs eagerly under a group.
+ * trpo_ctx_attach_group must be called by all ranks concurrently (it all-reduces N). */
+typedef struct trpo_group trpo_group;
+trpo_group *trpo_group_create(int world);
+void trpo_group_destroy(trpo_group *g);
+int trpo_ctx_attach_group(trpo_ctx *ctx, trpo_group *g, int rank);
+
+/* The attached communicator as the collective library reports it: this context's rank, the rank
+ * count (RCCL's ncclCommCount; 1 without a communicator) and the fp64 atomic replica sets each FVP
+ * all-reduces (0 when the block-slab reduction is in use). */
+int trpo_ctx_comm_info(const trpo_ctx *ctx, int *rank, int *world, int *replicas);
+
 /* Host-pointer convenience entry points (copy in / compute / copy out).
  * Return elapsed seconds (>= 0) or a negative error code. */
 double trpo_ctx_fvp(trpo_ctx *ctx, const double *v, double *out);

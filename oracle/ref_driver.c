@@ -157,8 +157,11 @@ int main(int argc, char **argv) {
     }
     if (!strcmp(mode, "fvp")) {
         size_t th = argc > 10 ? (size_t)atoi(argv[10]) : 1;
+        double w0 = wall();
         double t = FVPFast(prm, out, in, th);
+        double w1 = wall();
         if (t < 0) return 1;
+        fprintf(stderr, "{\"compute_s\": %.9f, \"wall_s\": %.9f, \"threads\": %zu}\n", t, w1 - w0, th);
         return write_vec(argv[9], out, P) ? 1 : 0;
     }
     if (!strcmp(mode, "cg") || !strcmp(mode, "time")) {

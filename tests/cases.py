@@ -93,7 +93,17 @@ def update_inputs(c):
 
 
 def baseline_inputs(c):
-    """(x, observ, target) of a baseline case; the expected file holds g [padded] then predict [N]."""
+    """(x, observ, target) of a baseline case; the expected file holds g [padded] then predict [N].
+    Fixture case: x = the reference's ArmTestBaseline.txt (561 values) zero-padded to a multiple of 16,
+    observations and targets (the advantage column) from the first num_ep * ep_len lines of
+    ArmTestData.txt."""
+    if c.get("src") == "fixture":
+        th = _read_table("ArmTestBaseline.txt")
+        x = np.zeros((th.size + 15) // 16 * 16)
+        x[:th.size] = th
+        n = c["num_ep"] * c["ep_len"]
+        t = _read_table("ArmTestData.txt")[:n]
+        return x, np.ascontiguousarray(t[:, 6:21]), t[:, 24].copy()
     return synth.make_baseline_problem(c["layers"], c["num_ep"], c["ep_len"], scale=c["scale"], pad_value=c["pad"])
 
 

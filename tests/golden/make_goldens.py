@@ -28,7 +28,7 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, os.path.join(ROOT, "trpo-robot-control_amd"))
 sys.path.insert(0, os.path.dirname(HERE))
 from trpo_amd import synth  # noqa: E402
-from cases import synth_update_inputs  # noqa: E402
+from cases import baseline_inputs, synth_update_inputs  # noqa: E402
 
 DRIVER = os.path.join(ROOT, "oracle", "_ref", "ref_driver")
 ARM = [15, 16, 16, 3]
@@ -79,6 +79,11 @@ CASES = [
          scale=1.7, pad=0.25),
     dict(name="syn_baseline_lin_n1000", kind="baseline", layers=[16, 32, 16, 1], acfunc="lltl", num_ep=10,
          ep_len=100, scale=0.8, pad=0.0),
+    # the reference's own baseline parameters (build/ArmTestBaseline.txt: the [16,16,16,1] theta that
+    # src/TRPOCpuCode.c:381 hands to the trainers), zero-padded to 576 as the L-BFGS vector; the
+    # fixture's observations, 20 episodes x 150 steps, and its advantage column as regression targets
+    dict(name="fix_baseline_armtest", kind="baseline", src="fixture", layers=[16, 16, 16, 1], acfunc="lttl",
+         num_ep=20, ep_len=150),
 ]
 
 
@@ -138,8 +143,7 @@ def run_update_case(case, tmp):
 
 
 def run_baseline_case(case, tmp):
-    x, obs, target = synth.make_baseline_problem(case["layers"], case["num_ep"], case["ep_len"],
-                                                 scale=case["scale"], pad_value=case["pad"])
+    x, obs, target = baseline_inputs(case)
     files = {}
     for key, arr in (("obs", obs.ravel()), ("tgt", target), ("x", x)):
         files[key] = os.path.join(tmp, case["name"] + "." + key)
@@ -187,10 +191,16 @@ def run_case(case, tmp):
 
 
 def main():
+    """python tests/golden/make_goldens.py [NAME ...]: all cases, or only the named ones (the other
+    records of manifest.json are kept)."""
     if not os.path.exists(DRIVER):
         sys.exit("build the reference first: make -C oracle ref")
+    only = set(sys.argv[1:])
+    old = {}
+    if only and os.path.exists(os.path.join(HERE, "manifest.json")):
+        old = {c["name"]: c for c in json.load(open(os.path.join(HERE, "manifest.json")))["cases"]}
     with tempfile.TemporaryDirectory() as tmp:
-        recs = [run_case(c, tmp) for c in CASES]
+        recs = [run_case(c, tmp) if (not only or c["name"] in only) else old[c["name"]] for c in CASES]
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump({"generator": "tests/golden/make_goldens.py", "driver": "oracle/_ref/ref_driver",
                    "seed": synth.SEED, "cases": recs}, f, indent=1)

@@ -3,6 +3,7 @@ public header declares, TRPOparam has the reference layout, host-side error
 paths follow the reference (src/TRPO_FVP.c:671-674,732-735)."""
 import ctypes as C
 import os
+import re
 import subprocess
 import textwrap
 
@@ -75,3 +76,19 @@ def test_no_gpu_fails_loudly():
     with pytest.raises(trpo_amd.TRPOError):
         trpo_amd.Context([15, 16, 16, 3], "lttl", synth.make_theta([15, 16, 16, 3]), synth.make_obs(8, 15),
                          np.ones(3))
+
+
+@pytest.mark.parametrize("compiler", [["gcc", "-std=gnu99"], ["g++", "-x", "c++", "-std=c++11"]])
+def test_compiled_caller_builds_and_links(compiler, tmp_path):
+    """The drop-in caller (tests/c_caller/drop_in_caller.c, the TRPOCpuCode.c pattern) compiles as C and
+    as C++ against include/trpo_mi355x.h alone and links with -ltrpo_mi355x; the reference's entry
+    points are imported UNMANGLED in the C++ build (extern "C" linkage, build/Makefile.cpuonly:5)."""
+    import subprocess
+    libdir = os.path.dirname(trpo_amd.LIB_PATH)
+    exe = str(tmp_path / "caller")
+    src = os.path.join(os.path.dirname(__file__), "c_caller", "drop_in_caller.c")
+    subprocess.run(compiler + ["-O1", "-Wall", "-Werror", "-I", os.path.dirname(trpo_amd.HEADER), "-o", exe, src,
+                               "-L", libdir, "-ltrpo_mi355x"], check=True)
+    syms = subprocess.run(["nm", "-D", "--undefined-only", exe], capture_output=True, text=True, check=True).stdout
+    for name in ("NumParamsCalc", "FVPFast", "CG", "TRPO_Update"):
+        assert re.search(r"\bU %s$" % name, syms, re.M), name

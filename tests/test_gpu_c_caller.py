@@ -1,0 +1,42 @@
+"""MI355X: the drop-in from a COMPILED caller.
+
+tests/c_caller/drop_in_caller.c calls NumParamsCalc / FVPFast / CG / TRPO_Update the way the
+reference's src/TRPOCpuCode.c:15-135,314-372 calls them -- built as C with gcc and as C++ with g++
+(build/Makefile.cpuonly:5 compiles callers with g++) against include/trpo_mi355x.h and linked with
+-ltrpo_mi355x (built by __graft_entry__.build(), make -C tests/c_caller).  Run on the reference's
+fixture files; its output vectors are checked against the goldens the reference produced, with the
+same tolerances as the ctypes parity tests, and its stdout must carry the reference's lines.
+"""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import cases
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.mark.parametrize("binary", ["drop_in_caller_c", "drop_in_caller_cxx"])
+def test_compiled_caller_on_fixtures(binary, tmp_path):
+    exe = os.path.join(HERE, "c_caller", binary)
+    assert os.path.exists(exe), "build the callers first: make -C tests/c_caller (__graft_entry__.build)"
+    p = subprocess.run([exe, cases.GOLDEN, str(tmp_path), "3150", "6"], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    fvp = np.loadtxt(tmp_path / "fvp.txt")
+    cg = np.loadtxt(tmp_path / "cg.txt")
+    upd = np.loadtxt(tmp_path / "update.txt")
+    assert cases.rel_l2(fvp, cases.expected(cases.case("fix_fvp_n3150"))) <= 1e-5
+    assert cases.rel_l2(cg, cases.expected(cases.case("fix_cg_n3150_th1e-10"))) <= 1e-4
+    th = cases.fixture_model()
+    assert cases.rel_l2(upd - th, cases.expected(cases.case("fix_update_n3150")) - th) <= 1e-4
+    out = p.stdout
+    iters = re.findall(r"CG Iter\[(\d+)\] Residual Norm=(\S+), Soln Norm=(\S+)", out)
+    assert iters and iters[0][0] == "0" and iters[0][1].startswith("9.05595253")
+    assert re.search(r"shs: \S+", out) and re.search(r"lagrange multiplier: \S+, gnorm: \S+", out)
+    assert re.search(r"a/e/r \S+ / \S+ / \S+", out)
+    assert "[ERROR] Cannot open Model File" in p.stderr          # the bad-path call, reference message

@@ -154,7 +154,8 @@ def test_update_requires_rollout():
 @pytest.mark.parametrize("layers", [[15, 16, 16, 3], [15, 64, 64, 3]])
 def test_repeated_updates_deterministic(layers, monkeypatch):
     """A trainer-like sequence on one context -- several updates, set_theta / set_rollout between them,
-    a rejected full step, each update repeated -- is deterministic: two runs agree bit for bit (the
+    a rejected full step, each update repeated -- is deterministic: a run with every CG launched
+    eagerly (TRPO_NO_GRAPH=1) and a run on the captured, replayed CG graphs agree bit for bit (the
     device state the update reuses across calls: forward cache, replica sets, rollout rows, graphs)."""
     from trpo_amd import synth
     n = 3000
@@ -177,7 +178,9 @@ def test_repeated_updates_deterministic(layers, monkeypatch):
                 ctx.set_theta(th)
         return out
 
+    monkeypatch.setenv("TRPO_NO_GRAPH", "1")         # read by the library at every CG enqueue
     eager = run()
+    monkeypatch.delenv("TRPO_NO_GRAPH")
     graph = run()
     for a, e in zip(graph, eager):
         for x, y in zip(a, e):

@@ -126,6 +126,31 @@ def test_cache_invalidated_by_theta_and_obs():
     assert cases.rel_l2(z3, zr) <= FVP_TOL
 
 
+@pytest.mark.parametrize("layers,fused", [([15, 16, 16, 3], "1"), ([15, 64, 64, 3], "1"), ([15, 64, 64, 3], "0")])
+def test_update_without_cache_writing_cg_leaves_cache_invalid(layers, fused, monkeypatch):
+    """set_theta -> update: FVP(x) and every later FVP may read the forward cache only if the
+    update's CG actually rewrote it (its fused K_0).  update(max_iter=0) enqueues no FVP in the CG,
+    and the unfused cooperative path (TRPO_COOP_FUSED=0) never writes the cache: in both cases the
+    next FVP must recompute the forward pass of the NEW theta."""
+    monkeypatch.setenv("TRPO_COOP_FUSED", fused)
+    P = synth.num_params(layers)
+    th1, obs = synth.make_theta(layers), synth.make_obs(2000, layers[0])
+    th2 = th1 + 0.05 * np.random.default_rng(11).standard_normal(P)
+    th2[-layers[-1]:] = th1[-layers[-1]:]
+    std = np.ones(layers[-1])
+    v = synth.make_v(P)
+    mean, action, adv = synth.make_rollout(layers, "lttl", th2, obs, std)
+    zr, _ = oracle.fvp(layers, "lttl", th2, obs, std, v)
+    for max_iter in ((0, 10) if fused == "1" else (10,)):
+        with trpo_amd.Context(layers, "lttl", th1, obs, std, 0.1) as ctx:
+            ctx.fvp(v)                                  # cache now holds th1's activations
+            ctx.set_theta(th2)
+            ctx.set_rollout(mean, action, adv)
+            r = ctx.update(max_iter=max_iter)
+            assert r["cg_iters"] == max_iter
+            assert cases.rel_l2(ctx.fvp(v), zr) <= FVP_TOL, max_iter
+
+
 @pytest.mark.parametrize("layers,acf,n", [([15, 64, 64, 3], "lttl", 4096), ([15, 32, 32, 3], "lttl", 3000),
                                           ([15, 64, 64, 3], "lsso", 2000), ([15, 64, 64, 3], "lttt", 2000),
                                           ([20, 64, 64, 3], "lttl", 1000)])

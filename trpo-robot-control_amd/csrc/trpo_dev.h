@@ -30,6 +30,13 @@ int trpo_dev_set_damping(trpo_dev *d, double damping);
 
 int trpo_dev_comm_unique_id(void *id128);
 int trpo_dev_set_comm(trpo_dev *d, int rank, int world, const void *id128);
+/* in-process host-staged group of `world` contexts (one thread each): the sharded code path
+ * without RCCL, for tests (trpo_kernels.hip) */
+typedef struct trpo_hgroup trpo_hgroup;
+trpo_hgroup *trpo_hgroup_create(int world);
+void trpo_hgroup_destroy(trpo_hgroup *g);
+int trpo_dev_set_group(trpo_dev *d, trpo_hgroup *g, int rank);
+int trpo_dev_comm_info(const trpo_dev *d, int *rank, int *world, int *replicas);
 
 int trpo_dev_upload(trpo_dev *d, int slot, const double *host);
 int trpo_dev_download(trpo_dev *d, int slot, double *host);

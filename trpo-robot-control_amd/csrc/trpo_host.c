@@ -158,6 +158,18 @@ int trpo_ctx_attach_comm(trpo_ctx *c, int rank, int world, const void *id) {
     return trpo_dev_set_comm(c->dev, rank, world, id);
 }
 
+trpo_group *trpo_group_create(int world) { return (trpo_group *)trpo_hgroup_create(world); }
+void trpo_group_destroy(trpo_group *g) { trpo_hgroup_destroy((trpo_hgroup *)g); }
+int trpo_ctx_attach_group(trpo_ctx *c, trpo_group *g, int rank) {
+    if (!c || !g) return TRPO_E_INVALID;
+    const int rc = trpo_dev_set_group(c->dev, (trpo_hgroup *)g, rank);
+    if (rc) set_err("attach_group(rank %d) failed (code %d)", rank, rc);
+    return rc;
+}
+int trpo_ctx_comm_info(const trpo_ctx *c, int *rank, int *world, int *replicas) {
+    return c ? trpo_dev_comm_info(c->dev, rank, world, replicas) : TRPO_E_INVALID;
+}
+
 double trpo_ctx_fvp(trpo_ctx *c, const double *v, double *out) {
     if (!c || !v || !out) return TRPO_E_INVALID;
     const double t0 = now_s();

@@ -27,6 +27,7 @@
 #include <rccl/rccl.h>
 
 #include <math.h>
+#include <pthread.h>
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -2390,12 +2391,15 @@ struct trpo_dev {
     size_t n;                   // local samples
     size_t npad_cap;
     double n_total;
+    double n_max;               // largest shard over the ranks (replica sizing)
     double damping;
     // CG graph cache
     hipGraphExec_t cg_exec;
     int no_graph;
     size_t cg_graph_iters;
     double cg_graph_resth;
+    size_t cg_last_iters;       // maxiter of the last enqueued CG (trpo_dev_ycache_written)
+    void *tscr;                 // scratch of the kernel-only timing of the CG-iteration kernel
     hipEvent_t ev0, ev1;
     // pinned, device-mapped host staging for the host <-> device vector moves (kernel copies)
     double *hst, *hst_dev;
@@ -2403,9 +2407,97 @@ struct trpo_dev {
     int hst_pending;        // an upload's copy kernel may still read hst: sync before the host rewrites it
     // RCCL
     ncclComm_t comm;
+    // in-process host-staged group (trpo_dev_set_group): the same sharded code path without RCCL
+    trpo_hgroup *group;
+    double *gbuf;               // pinned host staging for the group exchange
+    size_t gbuf_cap;
     int rank, world;
     char name[64];
 };
+
+// ---------------------------------------------------------------------------
+// In-process host-staged all-reduce (trpo_dev_set_group).  The contexts of one process -- one
+// thread per context, on any devices -- exchange their partial sums through host memory: every rank
+// copies its buffer in, waits for all ranks, sums the slots in rank order (so every rank gets the
+// same bits, as RCCL's all-reduce guarantees) and copies the sum back.  It exists to run the
+// library's sharded code path (global N, replica sizing from the largest shard, lockstep CG) on a
+// single GPU in tests; the collective is a host round trip, so CG runs eagerly under it.
+// ---------------------------------------------------------------------------
+struct trpo_hgroup {
+    int world;
+    pthread_barrier_t bar;
+    pthread_mutex_t mu;
+    double **slot;              // per-rank host views of the buffers being reduced
+    size_t *count;
+    int *attached;
+};
+
+extern "C" trpo_hgroup *trpo_hgroup_create(int world) {
+    if (world < 1 || world > 1024) return NULL;
+    trpo_hgroup *g = (trpo_hgroup *)calloc(1, sizeof(trpo_hgroup));
+    if (!g) return NULL;
+    g->world = world;
+    g->slot = (double **)calloc(world, sizeof(double *));
+    g->count = (size_t *)calloc(world, sizeof(size_t));
+    g->attached = (int *)calloc(world, sizeof(int));
+    if (!g->slot || !g->count || !g->attached || pthread_barrier_init(&g->bar, NULL, (unsigned)world) ||
+        pthread_mutex_init(&g->mu, NULL)) {
+        free(g->slot);
+        free(g->count);
+        free(g->attached);
+        free(g);
+        return NULL;
+    }
+    return g;
+}
+
+extern "C" void trpo_hgroup_destroy(trpo_hgroup *g) {
+    if (!g) return;
+    pthread_barrier_destroy(&g->bar);
+    pthread_mutex_destroy(&g->mu);
+    free(g->slot);
+    free(g->count);
+    free(g->attached);
+    free(g);
+}
+
+// in-place sum of buf[count] (device, on d's stream) over the group; every rank must call it with
+// the same count, in the same order as the others (the library's fixed launch sequences do)
+static int hgroup_allreduce(trpo_dev *d, double *buf, size_t count) {
+    trpo_hgroup *g = d->group;
+    if (count > d->gbuf_cap) {
+        if (d->gbuf) hipHostFree(d->gbuf);
+        d->gbuf = NULL;
+        d->gbuf_cap = 0;
+        HCHK(hipHostMalloc((void **)&d->gbuf, sizeof(double) * count, hipHostMallocDefault));
+        d->gbuf_cap = count;
+    }
+    HCHK(hipMemcpyAsync(d->gbuf, buf, sizeof(double) * count, hipMemcpyDeviceToHost, d->stream));
+    HCHK(hipStreamSynchronize(d->stream));
+    g->slot[d->rank] = d->gbuf;
+    g->count[d->rank] = count;
+    pthread_barrier_wait(&g->bar);                 // every rank's partial is in host memory
+    int bad = 0;
+    for (int r = 0; r < g->world; ++r) bad |= g->count[r] != count;
+    double *sum = (double *)malloc(sizeof(double) * (count ? count : 1));
+    if (sum && !bad) {
+        for (size_t i = 0; i < count; ++i) {
+            double s = g->slot[0][i];
+            for (int r = 1; r < g->world; ++r) s += g->slot[r][i];   // rank order: identical bits everywhere
+            sum[i] = s;
+        }
+    }
+    pthread_barrier_wait(&g->bar);                 // every rank has read every slot
+    if (!sum || bad) {
+        free(sum);
+        return -4;
+    }
+    memcpy(d->gbuf, sum, sizeof(double) * count);
+    free(sum);
+    HCHK(hipMemcpyAsync(buf, d->gbuf, sizeof(double) * count, hipMemcpyHostToDevice, d->stream));
+    HCHK(hipStreamSynchronize(d->stream));
+    return 0;
+}
 
 static int act_code(char a) {
     switch (a) {
@@ -2649,12 +2741,13 @@ extern "C" void trpo_dev_destroy(trpo_dev *d) {
     if (d->comm) ncclCommDestroy(d->comm);
     trpo_update_state_free(d->upd);
     void *ptrs[] = {d->obs64, d->pg_d, d->pg_adv, d->pg_iv, d->st, d->pbuf[0], d->pbuf[1], d->rbuf[0], d->rbuf[1], d->accbuf, d->pacc, d->imap, d->tpack, d->vpack, d->tmap, d->vmap, d->pslot, d->obs4, d->yc, d->th32, d->v32, d->iv32, d->obs32, d->scratch,
-                    d->theta64, d->std64, d->r, d->zacc, d->slabs, d->ctl, d->hist};
+                    d->theta64, d->std64, d->r, d->zacc, d->slabs, d->ctl, d->hist, d->tscr};
     for (void *p : ptrs)
         if (p) hipFree(p);
     for (int i = 0; i < 5; ++i)
         if (d->vec[i]) hipFree(d->vec[i]);
     if (d->hst) hipHostFree(d->hst);
+    if (d->gbuf) hipHostFree(d->gbuf);
     if (d->ev0) hipEventDestroy(d->ev0);
     if (d->ev1) hipEventDestroy(d->ev1);
     if (d->stream) hipStreamDestroy(d->stream);
@@ -2742,6 +2835,7 @@ static int choose_grid(trpo_dev *d) {
 }
 
 static int refresh_n_total(trpo_dev *d);
+static int allreduce(trpo_dev *d, double *buf, size_t count);
 
 extern "C" int trpo_dev_set_obs(trpo_dev *d, const double *obs, size_t n) {
     if (!d || (!obs && n) || n > (size_t)1 << 30) return -1;
@@ -2820,7 +2914,7 @@ static int choose_replicas(trpo_dev *d) {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, d->device) == hipSuccess && prop.multiProcessorCount > 0)
             cus = prop.multiProcessorCount;
-        const long nmax = (long)ceil(d->n_total / d->world);
+        const long nmax = (long)d->n_max;                 // the largest shard over all ranks
         long g = cdiv(cdiv(nmax, 16), d->k_tiles);
         if (g > cus) g = cus;
         rc = (int)cdiv(g, 32);
@@ -2846,17 +2940,36 @@ static int choose_replicas(trpo_dev *d) {
 // N is the global sample count: local n, or the all-reduced n under RCCL
 static int refresh_n_total(trpo_dev *d) {
     const size_t n = d->n;
-    if (d->comm) {
-        double nl = (double)n, *dn = NULL;
-        HCHK(hipMalloc((void **)&dn, sizeof(double)));
-        HCHK(hipMemcpyAsync(dn, &nl, sizeof(double), hipMemcpyHostToDevice, d->stream));
-        if (ncclAllReduce(dn, dn, 1, ncclFloat64, ncclSum, d->comm, d->stream) != ncclSuccess) return -4;
-        HCHK(hipStreamSynchronize(d->stream));
-        HCHK(hipMemcpyAsync(&d->n_total, dn, sizeof(double), hipMemcpyDeviceToHost, d->stream));
-        HCHK(hipStreamSynchronize(d->stream));
+    if (d->comm || d->group) {
+        // every rank's shard size in one sum-all-reduce (rank r contributes n at slot r): N is the
+        // total, and the replica sizing below reads the LARGEST shard -- both identical on all ranks
+        const int W = d->world;
+        double *hn = (double *)calloc(W, sizeof(double)), *dn = NULL;
+        if (!hn) return -3;
+        hn[d->rank] = (double)n;
+        if (hipMalloc((void **)&dn, sizeof(double) * W) != hipSuccess) {
+            free(hn);
+            return -2;
+        }
+        int rc = hipMemcpyAsync(dn, hn, sizeof(double) * W, hipMemcpyHostToDevice, d->stream) ? -2 : 0;
+        if (!rc) rc = allreduce(d, dn, (size_t)W);
+        if (!rc && hipMemcpyAsync(hn, dn, sizeof(double) * W, hipMemcpyDeviceToHost, d->stream)) rc = -2;
+        if (!rc && hipStreamSynchronize(d->stream)) rc = -2;
         hipFree(dn);
+        if (!rc) {
+            double tot = 0.0, mx = 0.0;
+            for (int r = 0; r < W; ++r) {
+                tot += hn[r];
+                mx = hn[r] > mx ? hn[r] : mx;
+            }
+            d->n_total = tot;
+            d->n_max = mx;
+        }
+        free(hn);
+        if (rc) return rc;
     } else {
         d->n_total = (double)n;
+        d->n_max = (double)n;
     }
     if (choose_replicas(d)) return -2;
     return sync_ctl_scalars(d);
@@ -2869,9 +2982,48 @@ extern "C" int trpo_dev_comm_unique_id(void *id128) {
     return 0;
 }
 
+extern "C" int trpo_dev_set_group(trpo_dev *d, trpo_hgroup *g, int rank) {
+    if (!d || !g || rank < 0 || rank >= g->world) return -1;
+    HCHK(hipSetDevice(d->device));
+    if (d->comm) {
+        ncclCommDestroy(d->comm);
+        d->comm = NULL;
+    }
+    pthread_mutex_lock(&g->mu);
+    const int taken = g->attached[rank];
+    g->attached[rank] = 1;
+    pthread_mutex_unlock(&g->mu);
+    if (taken) return -1;
+    d->group = g;
+    d->rank = rank;
+    d->world = g->world;
+    if (d->cg_exec) {               // the host exchange cannot live in a graph: CG runs eagerly
+        hipGraphExecDestroy(d->cg_exec);
+        d->cg_exec = NULL;
+    }
+    return refresh_n_total(d);
+}
+
+// ranks of the attached communicator as the collective library itself reports them (RCCL's
+// ncclCommCount), the context's rank, and the atomic replica sets in use
+extern "C" int trpo_dev_comm_info(const trpo_dev *d, int *rank, int *world, int *replicas) {
+    if (!d) return -1;
+    int w = d->world;
+    if (d->comm) {
+        int c = 0;
+        if (ncclCommCount(d->comm, &c) != ncclSuccess) return -4;
+        w = c;
+    }
+    if (rank) *rank = d->rank;
+    if (world) *world = w;
+    if (replicas) *replicas = d->atomic ? d->Rc : 0;
+    return 0;
+}
+
 extern "C" int trpo_dev_set_comm(trpo_dev *d, int rank, int world, const void *id128) {
     if (!d || world < 1 || rank < 0 || rank >= world) return -1;
     HCHK(hipSetDevice(d->device));
+    d->group = NULL;
     if (d->comm) {
         ncclCommDestroy(d->comm);
         d->comm = NULL;
@@ -3021,10 +3173,7 @@ static int enqueue_fvp_core(trpo_dev *d, const double *src, const int *skip) {
     }
     launch_reduce(d, skip);
     HCHK(hipGetLastError());
-    if (d->comm) {
-        if (ncclAllReduce(d->zacc, d->zacc, d->nw, ncclFloat64, ncclSum, d->comm, d->stream) != ncclSuccess) return -4;
-    }
-    return 0;
+    return allreduce(d, d->zacc, d->nw);
 }
 
 // z = F src into slot Z (src: any device P-vector, e.g. slot X for the update's FVP(x)); with
@@ -3036,7 +3185,7 @@ static int fvp_src(trpo_dev *d, const double *src, double **zh) {
     HCHK(hipSetDevice(d->device));
     double *zhost = *zh;
     *zh = NULL;
-    if (d->fast && (d->atomic || !d->comm)) {
+    if (d->fast && (d->atomic || !(d->comm || d->group))) {
         // two launches: the tile kernel gathers its direction fragments from v itself, then the
         // atomic-replica or slab reduce applies the epilogue (under RCCL after the all-reduce)
         IterArgs a = plain_args(d, &d->ctl->zero);
@@ -3118,9 +3267,19 @@ static int ensure_hist(trpo_dev *d, size_t maxiter) {
 
 static double *acc_slot(trpo_dev *d, long j) { return d->accbuf + (j % 3) * (long)d->R * d->P; }
 
+// the one place every collective of the library goes through: RCCL, the in-process host group, or
+// nothing (one rank)
 static int allreduce(trpo_dev *d, double *buf, size_t count) {
+    if (d->group) return hgroup_allreduce(d, buf, count);
     if (!d->comm) return 0;
     return ncclAllReduce(buf, buf, count, ncclFloat64, ncclSum, d->comm, d->stream) == ncclSuccess ? 0 : -4;
+}
+
+// per-iteration arguments of the fused CG-iteration kernel K_j beyond the CG state
+static void cg_iter_args_extra(trpo_dev *d, IterArgs &a, long j) {
+    (void)d;
+    (void)a;
+    (void)j;
 }
 
 // CG(maxiter) as a straight-line launch sequence (captured into a hipGraph by trpo_dev_cg).
@@ -3248,10 +3407,20 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
     return 0;
 }
 
-// after a CG solve the forward-activation cache holds the current theta's activations (its first FVP
-// writes them unconditionally), so the FVP(x) that follows may read it
+// Does the CG launch sequence of enqueue_cg_body(maxiter) write the forward-activation cache?  Only
+// the fused paths do, in their first FVP K_0 (launched with a.yc and never skipped); maxiter = 0
+// enqueues no FVP at all, and the unfused cooperative path (TRPO_COOP_FUSED=0) runs its FVPs
+// through enqueue_fvp_core without the cache.
+static bool cg_writes_ycache(const trpo_dev *d, size_t maxiter) {
+    if (!d->yc_on || maxiter == 0 || !d->fast) return false;
+    return !d->coop || d->coop_fused;
+}
+
+// after a CG solve whose K_0 wrote the forward-activation cache it holds the current theta's
+// activations, so the FVP(x) that follows may read it; otherwise the cache state is left alone (a
+// stale cache stays invalid and the next standalone FVP recomputes and rewrites it)
 void trpo_dev_ycache_written(trpo_dev *d) {
-    if (d->yc_on) d->yc_valid = 1;
+    if (cg_writes_ycache(d, d->cg_last_iters)) d->yc_valid = 1;
 }
 
 extern "C" int trpo_dev_cg(trpo_dev *d, size_t maxiter, double resth) {
@@ -3260,8 +3429,9 @@ extern "C" int trpo_dev_cg(trpo_dev *d, size_t maxiter, double resth) {
     if (maxiter > 100000) return -1;
     int rc = ensure_hist(d, maxiter);
     if (rc) return rc;
+    d->cg_last_iters = maxiter;
     const char *ng = getenv("TRPO_NO_GRAPH");
-    if ((ng && atoi(ng)) || d->no_graph) return enqueue_cg_body(d, maxiter, resth);
+    if ((ng && atoi(ng)) || d->no_graph || d->group) return enqueue_cg_body(d, maxiter, resth);
     // the graph bakes (maxiter, resth) into cg_init's arguments: key on both
     if (!d->cg_exec || d->cg_graph_iters != maxiter || d->cg_graph_resth != resth) {
         if (d->cg_exec) {
@@ -3331,10 +3501,89 @@ extern "C" int trpo_dev_sync(trpo_dev *d) {
     return 0;
 }
 
+// Kernel-only timing of the fused CG-iteration kernel K_j (j >= 1: CG step j-1 -> j in the prologue,
+// then FVP j) exactly as the CG graph launches it, except that everything it writes goes to private
+// scratch (p, r, x, the scalar state, the history, a sink replica set) so that repeated launches
+// leave the context's solve untouched and never reach the convergence exit.  Inputs are the state
+// of the last solve.  Returns 1 when this context has no fused CG-iteration kernel.
+static int cg_iter_kernel_only(trpo_dev *d, long j) {
+    const bool fused = d->fast && (!d->coop || d->coop_fused);
+    if (!fused) return 1;
+    if (!d->tscr) {
+        const size_t bytes = sizeof(double) * (3 * (size_t)d->P + 2 * 65) + 2 * sizeof(CgSt) + sizeof(Ctl);
+        HCHK(hipMalloc(&d->tscr, bytes));
+        HCHK(hipMemsetAsync(d->tscr, 0, bytes, d->stream));
+    }
+    double *sp = (double *)d->tscr, *sr = sp + d->P, *sx = sr + d->P, *sh = sx + d->P;
+    CgSt *sst = (CgSt *)(sh + 2 * 65);
+    Ctl *sctl = (Ctl *)(sst + 2);
+    {   // the scratch control block never reports convergence; the scratch state is at iteration 0
+        Ctl c;
+        CgSt st;
+        HCHK(hipMemcpyAsync(&c, d->ctl, sizeof c, hipMemcpyDeviceToHost, d->stream));
+        HCHK(hipMemcpyAsync(&st, d->st, sizeof st, hipMemcpyDeviceToHost, d->stream));
+        HCHK(hipStreamSynchronize(d->stream));
+        c.maxiter = 1 << 30;
+        c.resth = -1.0;
+        c.done = 0;
+        c.zero = 0;
+        st.iter = 0;
+        HCHK(hipMemcpyAsync(sctl, &c, sizeof c, hipMemcpyHostToDevice, d->stream));
+        HCHK(hipMemcpyAsync(sst, &st, sizeof st, hipMemcpyHostToDevice, d->stream));
+        HCHK(hipStreamSynchronize(d->stream));
+    }
+    IterArgs a = plain_args(d, &sctl->zero);
+    a.update = 1;
+    a.p_in = d->pbuf[0];
+    a.r_in = d->rbuf[0];
+    a.p_out = sp;
+    a.r_out = sr;
+    a.x = sx;
+    a.st_in = sst;
+    a.st_out = sst + 1;
+    a.ctl = sctl;
+    a.hist = sh;
+    a.vmap = d->vmap;
+    if (d->atomic) {
+        a.acc_in = acc_slot(d, 0);
+        a.R_in = d->Rc;
+        a.acc_out = d->pacc + (long)d->R * d->P;      // the sink set: accumulates, never consumed
+        a.R_out = d->Rc;
+    } else {
+        a.acc_in = d->zacc;
+        a.R_in = 1;
+    }
+    cg_iter_args_extra(d, a, j);
+    if (d->yc_on) a.yc = reinterpret_cast<float4 *>(d->yc);
+    fast_launch_fn k = d->coop ? (d->yc_on ? d->k_cg_yc : d->coop_e->launch_cg) : (d->yc_on ? d->k_cg_yc : d->k_fvp);
+    k(dim3(d->grid), d->k_lds, d->stream, a, d->net);
+    HCHK(hipGetLastError());
+    return 0;
+}
+
 extern "C" double trpo_dev_time(trpo_dev *d, int what, int reps, size_t maxiter, double resth) {
     if (!d || reps < 1) return -1;
     if (hipSetDevice(d->device) != hipSuccess) return -2;
     int rc = 0;
+    if (what == 3) {
+        // the CG-iteration kernel alone, averaged over the iterations K_1 .. K_{maxiter-1} of a solve
+        // (reps launches of each); needs a solve first (its state and forward cache)
+        if (maxiter < 2) return -1;
+        rc = trpo_dev_cg(d, maxiter, resth);
+        if (rc) return rc;
+        rc = cg_iter_kernel_only(d, 1);
+        if (rc) return rc > 0 ? -1 : rc;
+        if (hipStreamSynchronize(d->stream) != hipSuccess) return -2;
+        hipEventRecord(d->ev0, d->stream);
+        for (long j = 1; j < (long)maxiter && !rc; ++j)
+            for (int i = 0; i < reps && !rc; ++i) rc = cg_iter_kernel_only(d, j);
+        hipEventRecord(d->ev1, d->stream);
+        if (rc) return rc;
+        if (hipEventSynchronize(d->ev1) != hipSuccess) return -2;
+        float ms = 0;
+        hipEventElapsedTime(&ms, d->ev0, d->ev1);
+        return (double)ms / (reps * (double)(maxiter - 1));
+    }
     // warm once (also captures the CG graph)
     if (what == 0) rc = trpo_dev_fvp_kernel(d);
     else if (what == 1) rc = trpo_dev_fvp(d);

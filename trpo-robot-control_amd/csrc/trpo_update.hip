@@ -9,13 +9,19 @@
 //       surr_k = sum_n Adv_n exp(0.5 sum_i [tx^2 - tn^2 + log Std_i - LogStd'_i])
 //       for candidates theta_k = theta + 2^-k fullstep, several k per launch.
 //
-// Both run once per update (not per CG iteration), so they are written for
-// fidelity first: fp64 throughout, one sample per lane, 64-sample passes per
-// one-wave workgroup, the pass's activations staged in LDS ([row][64], up to
-// 160 KB; a global scratch beyond that), weights read with wave-uniform scalar
-// loads.  Cross-sample sums are fixed-order (lane order within a pass, block
-// order across blocks), so results are deterministic; multi-GPU ranks add their
-// shard sums with one RCCL all-reduce.
+// Precision of the policy gradient.  DEFAULT (shapes with an MFMA tile kernel): the weight / bias
+// part runs on the fp32 tile kernel in its policy-gradient mode (trpo_dev_pg_sums_fast;
+// (Action - Mean) and Adv are rounded to fp32 by pg_prep_kernel, per-sample products in fp32,
+// cross-tile sums in fp64) and only the LogStd part and sum(Adv) are fp64 (pg_logstd_kernel);
+// measured 1.2e-7 relative to the reference's fp64 gradient (tests allow 2e-6).
+// TRPO_UPDATE_GENERIC=1, shapes without a tile kernel, and the fp64 precision mode take the
+// generic pg_kernel below: fp64 throughout, reference-exact to ~1e-15.
+// The generic kernels (pg_kernel, the line-search surrogate) are written for fidelity first:
+// fp64, one sample per lane, 64-sample passes per one-wave workgroup, the pass's activations
+// staged in LDS ([row][64], up to 160 KB; a global scratch beyond that), weights read with
+// wave-uniform scalar loads.  Cross-sample sums are fixed-order (lane order within a pass, block
+// order across blocks), so results are deterministic; multi-GPU ranks add their shard sums with
+// one RCCL all-reduce.
 #include <hip/hip_runtime.h>
 
 #include <math.h>

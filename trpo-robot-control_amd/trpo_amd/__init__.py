@@ -91,6 +91,14 @@ def lib():
     L.trpo_comm_unique_id.argtypes = [C.c_char_p]
     L.trpo_ctx_attach_comm.restype = C.c_int
     L.trpo_ctx_attach_comm.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_char_p]
+    L.trpo_group_create.restype = C.c_void_p
+    L.trpo_group_create.argtypes = [C.c_int]
+    L.trpo_group_destroy.restype = None
+    L.trpo_group_destroy.argtypes = [C.c_void_p]
+    L.trpo_ctx_attach_group.restype = C.c_int
+    L.trpo_ctx_attach_group.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+    L.trpo_ctx_comm_info.restype = C.c_int
+    L.trpo_ctx_comm_info.argtypes = [C.c_void_p, P(C.c_int), P(C.c_int), P(C.c_int)]
     L.trpo_ctx_fvp.restype = C.c_double
     L.trpo_ctx_fvp.argtypes = [C.c_void_p, _dp, _dp]
     L.trpo_ctx_cg.restype = C.c_double
@@ -367,6 +375,16 @@ class Context:
     def attach_comm(self, rank: int, world: int, unique_id: bytes):
         self._chk(lib().trpo_ctx_attach_comm(self._h, rank, world, unique_id), "attach_comm")
 
+    def attach_group(self, group: "Group", rank: int):
+        """Join an in-process host group as `rank` (call concurrently from one thread per rank)."""
+        self._chk(lib().trpo_ctx_attach_group(self._h, group._h, rank), "attach_group")
+
+    def comm_info(self):
+        """dict(rank, world, replicas): the communicator as the collective library reports it."""
+        r, w, rep = C.c_int(0), C.c_int(0), C.c_int(0)
+        self._chk(lib().trpo_ctx_comm_info(self._h, C.byref(r), C.byref(w), C.byref(rep)), "comm_info")
+        return dict(rank=r.value, world=w.value, replicas=rep.value)
+
     def fvp(self, v):
         out = np.zeros(self.P)
         self._chk(lib().trpo_ctx_fvp(self._h, np.ascontiguousarray(v, np.float64), out), "fvp")
@@ -449,6 +467,27 @@ class Context:
         b, t, l = C.c_int(0), C.c_int(0), C.c_int(0)
         lib().trpo_ctx_launch_geometry(self._h, C.byref(b), C.byref(t), C.byref(l))
         return dict(blocks=b.value, threads=t.value, lds_bytes=l.value)
+
+
+class Group:
+    """In-process host-staged sharding group (include/trpo_mi355x.h trpo_group_*)."""
+
+    def __init__(self, world: int):
+        self._h = lib().trpo_group_create(world)
+        if not self._h:
+            raise TRPOError("trpo_group_create(%d) failed" % world)
+        self.world = world
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().trpo_group_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
 
 
 def unique_id() -> bytes:

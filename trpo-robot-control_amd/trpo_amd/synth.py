@@ -72,8 +72,9 @@ def make_theta(layers, seed: int = SEED, logstd: float = 0.0) -> np.ndarray:
     return np.concatenate(parts)
 
 
-def make_obs(n: int, obs_dim: int, seed: int = SEED) -> np.ndarray:
-    return uniform(seed, STREAM_OBS, n * obs_dim, -0.17, 0.19).reshape(n, obs_dim)
+def make_obs(n: int, obs_dim: int, seed: int = SEED, start: int = 0) -> np.ndarray:
+    """Rows [start, start + n) of the seeded observation stream (a rank generates only its shard)."""
+    return uniform(seed, STREAM_OBS, n * obs_dim, -0.17, 0.19, offset=start * obs_dim).reshape(n, obs_dim)
 
 
 def make_v(P: int, seed: int = SEED) -> np.ndarray:
