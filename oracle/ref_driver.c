@@ -175,10 +175,8 @@ int main(int argc, char **argv) {
         double t = CG(prm, out, in, maxiter, resth, th);
         double w1 = wall();
         if (t < 0) return 1;
-        if (is_time) {
-            fprintf(stderr, "{\"compute_s\": %.9f, \"wall_s\": %.9f, \"threads\": %zu}\n", t, w1 - w0, th);
-            return 0;
-        }
+        fprintf(stderr, "{\"compute_s\": %.9f, \"wall_s\": %.9f, \"threads\": %zu}\n", t, w1 - w0, th);
+        if (is_time) return 0;
         return write_vec(argv[11], out, P) ? 1 : 0;
     }
     fprintf(stderr, "unknown mode %s\n", mode);

@@ -18,10 +18,9 @@ import trpo_amd
 pytestmark = pytest.mark.gpu
 
 FVP_TOL = 1e-5
-CG_TOL = 1e-4
-# syn_sigma_cg (N=1000, sigma != 1, 10 iterations, ResidualTh=0) is ill-conditioned: the fp32
-# FVP is within 6e-8 of the reference, CG amplifies that ~2000x by iteration 10 (measured 1.35e-4).
-CG_TOL_CASE = {"syn_sigma_cg": 3e-4}
+CG_TOL = 1e-4          # every CG golden, the ill-conditioned sigma != 1 case included: the device CG
+                       # reorthogonalises its residuals, which removes the amplification of
+                       # the fp32 FVP's p-dependent rounding (1.35e-4 on syn_sigma_cg without it)
 
 
 def _ctx(x, **kw):
@@ -38,7 +37,7 @@ def test_context_matches_reference_golden(name):
             assert cases.rel_l2(out, cases.expected(c)) <= FVP_TOL, ctx.kernel_name
         else:
             out = ctx.cg(x["vin"], c["maxiter"], c["resth"])
-            assert cases.rel_l2(out, cases.expected(c)) <= CG_TOL_CASE.get(name, CG_TOL), ctx.kernel_name
+            assert cases.rel_l2(out, cases.expected(c)) <= CG_TOL, ctx.kernel_name
             rr, xn, iters = ctx.cg_history()
             if c["resth"] == 0.0:
                 assert iters == c["iters"]
@@ -200,7 +199,7 @@ def test_cooperative_kernel_shapes_against_oracle(layers, mode, monkeypatch):
         assert cases.rel_l2(ctx.fvp(v), ref) <= FVP_TOL
         x = ctx.cg(b, 10, 0.0)
         xr = oracle.cg(layers, "lttl", th, obs, std, b, 10, 0.0)["x"]
-        assert cases.rel_l2(x, xr) <= 2e-3          # fp32 FVP in an ill-conditioned 10-step CG
+        assert cases.rel_l2(x, xr) <= 1e-4          # fp32 FVP + reorthogonalised CG
         mean, action, adv = synth.make_rollout(layers, "lttl", th, obs, std)
         ctx.set_rollout(mean, action, adv)
         r = ctx.update()

@@ -5,16 +5,13 @@ Tolerances (stated):
     LogStd part and sum(Adv) in fp64 -> relL2 <= 2e-6 (numpy emulation of fp32 per-sample math:
     1.2e-7, which moves the CG step by 4e-7); the generic fp64 kernel (TRPO_UPDATE_GENERIC=1,
     used for shapes without a tile kernel) -> relL2 <= 1e-12
-  * CG step x: fp32 FVP inside the solve -> relL2 <= 1e-4 (as the CG tests) for armDOF_0;
-    2e-3 for the 2x64 policy.  Why: the fp32 rounding of each CG direction p (and the
-    p-proportional rounding of the R-chain) is noise that CG amplifies by the condition
-    number; a numpy emulation (fp32 per-sample math, fp64 sums) of this exact case gives
-    8.1e-4, and rounding ONLY p to fp32 with fp64 math elsewhere gives 9.4e-4 -- it is the
-    fp32 contract, not the kernel.  The reference's 2x64 solve runs all 10 iterations down to
-    |r|/|b| = 1.4e-4, below what an fp32 matrix-vector product can resolve.
-  * step size shs / lagrange: derived from x -> rel <= 1e-4 (2e-3 for 2x64)
-  * parameter update theta' - theta: relL2 <= 1e-4 (2e-3 for 2x64) against the reference's own
-    TRPO_Update
+  * CG step x: fp32 FVP inside the solve -> relL2 <= 1e-4 (as the CG tests) for every case, the
+    2x64 policy included.  Without the device CG's residual reorthogonalisation the
+    fp32 rounding of each CG direction p (and the p-proportional rounding of the R chains) is noise
+    that CG amplifies by the condition number: 7.7e-4 on the 2x64 case (numpy emulation of fp32
+    per-sample math: 7.6e-4; with reorthogonalisation 8e-8, tools/cg_noise_variants.py).
+  * step size shs / lagrange: derived from x -> rel <= 1e-4
+  * parameter update theta' - theta: relL2 <= 1e-4 against the reference's own TRPO_Update
   * line search: same accepted backtrack as the reference, ratios within rtol 1e-3
 """
 import os
@@ -28,7 +25,7 @@ import trpo_amd
 pytestmark = pytest.mark.gpu
 
 UPDATE = [c["name"] for c in cases.manifest() if c["kind"] == "update"]
-TOL = {"syn_update_2x64_n8192": 2e-3}
+TOL = {}
 B_TOL = 2e-6            # fp32 tile-kernel policy gradient
 B_TOL_GENERIC = 1e-12   # fp64 generic kernel
 

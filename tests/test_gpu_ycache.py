@@ -147,7 +147,7 @@ def test_update_without_cache_writing_cg_leaves_cache_invalid(layers, fused, mon
             ctx.set_theta(th2)
             ctx.set_rollout(mean, action, adv)
             r = ctx.update(max_iter=max_iter)
-            assert r["cg_iters"] == max_iter
+            assert r["cg_iters"] <= max_iter and (max_iter > 0 or r["cg_iters"] == 0)
             assert cases.rel_l2(ctx.fvp(v), zr) <= FVP_TOL, max_iter
 
 

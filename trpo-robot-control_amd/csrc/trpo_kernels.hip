@@ -106,6 +106,12 @@ struct IterArgs {
     double init_resth;
     const double *b_init;
     const int *pslot;             // natural parameter -> v-pack slot (pslot_at), -1 for LogStd
+    // residual reorthogonalisation (update / init): the basis q_0 .. q_{QCAP-1} (fp64 [QCAP][P]), the
+    // number of stored vectors this step uses (nq = min(iteration before the step, QCAP)), a zero line,
+    // and whether reorthogonalisation is on (TRPO_CG_REORTH, default 1)
+    double *q;
+    const double *qz;
+    int nq, reorth;
 };
 
 // fixed-order block-wide fp64 sum (every thread gets the result)
@@ -185,6 +191,131 @@ __device__ void block_sum2(double a, double b, double *sh, double &sa, double &s
     }
     sa = ta;
     sb = tb;
+}
+
+// ---------------------------------------------------------------------------
+// Residual reorthogonalisation of the CG step.  The fp32 FVP returns F p + delta(p) with
+// |delta| ~ 1e-7 |F p| and delta a NON-linear function of p, so CG's residuals lose their mutual
+// orthogonality and the 10-step iterate drifts from the fp64 reference's by up to ~1e-3
+// (tools/cg_noise_variants.py).  Each step therefore removes from the new residual
+// r' = r - alpha z its components along the normalised earlier residuals q_i = r_i / |r_i| (classical
+// Gram-Schmidt, fp64): c_i = q_i . r' = -alpha q_i . z for the stored basis (r is orthogonal to it
+// after the previous step) and c = |r| - alpha (r . z) / |r| along the current residual itself, so
+// only the dots q_i . z join the step's block reduction.  In exact arithmetic every c is zero, so the
+// iterates are the reference's (src/TRPO_CG.c:65-103); with the fp32 FVP the step lands within 1e-7 of
+// the fp64 reference instead of 1e-3.  |r''|^2 = |r'|^2 - sum c^2.  The basis q_0 .. q_{QCAP-1} lives in
+// HBM (fp64, natural order); longer solves are reorthogonalised against the first QCAP residuals.
+// ---------------------------------------------------------------------------
+constexpr int QCAP = 16;
+
+// the thread's E elements (q = tid + e * nthreads) of basis vector i, or zeros for i >= nq / q >= P:
+// the load is unconditional (a select on the address: qz is a small zero line every lane may read)
+template <int E>
+__device__ __forceinline__ void qload(double (&dst)[E], const double *Q, const double *qz, int P, int i, int nq,
+                                      int nthreads) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int q = tid + e * nthreads;
+        const bool ok = i < nq && q < P;
+        const double *src = ok ? Q + (long)i * P + q : qz + (tid & 7);
+        const double v = *src;
+        dst[e] = ok ? v : 0.0;
+    }
+}
+
+// stage 1 of the dots e_i = q_i . z, i < nq (runtime): per wave the 16-lane row sums, written to
+// shq[i * 4W + 4w + row] -- block_sums_dpp's layout; a later barrier (the caller's block reduction)
+// makes them visible.  Loads of the next vector are issued before the current one is reduced.
+template <int E>
+__device__ void qdots_stage1(const double *Q, const double *qz, int P, int nq, const double (&zv)[E], int nthreads,
+                             double *shq) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nr = (blockDim.x >> 6) * 4;
+    if constexpr (E > 4) {          // many elements per thread: one vector at a time (register budget)
+        for (int i = 0; i < nq; ++i) {
+            double qa[E];
+            qload(qa, Q, qz, P, i, nq, nthreads);
+            double t = 0.0;
+#pragma unroll
+            for (int e = 0; e < E; ++e) t += qa[e] * zv[e];
+            t = rowsum16_f64(t);
+            if ((lane & 15) == 0) shq[i * nr + w * 4 + (lane >> 4)] = t;
+        }
+        return;
+    }
+    double qa[E], qb[E];
+    qload(qa, Q, qz, P, 0, nq, nthreads);
+    for (int i = 0; i < nq; i += 2) {
+        qload(qb, Q, qz, P, i + 1, nq, nthreads);
+        double t = 0.0;
+#pragma unroll
+        for (int e = 0; e < E; ++e) t += qa[e] * zv[e];
+        t = rowsum16_f64(t);
+        if ((lane & 15) == 0) shq[i * nr + w * 4 + (lane >> 4)] = t;
+        qload(qa, Q, qz, P, i + 2, nq, nthreads);
+        if (i + 1 < nq) {
+            t = 0.0;
+#pragma unroll
+            for (int e = 0; e < E; ++e) t += qb[e] * zv[e];
+            t = rowsum16_f64(t);
+            if ((lane & 15) == 0) shq[(i + 1) * nr + w * 4 + (lane >> 4)] = t;
+        }
+    }
+}
+
+// stage 2: e_i from the row sums, the same fixed order in every wave and block (after a barrier)
+__device__ __forceinline__ double qdot_final(const double *shq, int i) {
+    const int lane = threadIdx.x & 63, nr = (blockDim.x >> 6) * 4;
+    const double t = shq[i * nr + min(lane, nr - 1)];
+    const double u = rowsum16_f64(lane < nr ? t : 0.0);
+    return (readlane64(u, 0) + readlane64(u, 16)) + (readlane64(u, 32) + readlane64(u, 48));
+}
+
+// stage 3: rv -= sum_i c_i q_i with c_i = -alpha e_i (i < nq); returns sum_i c_i^2
+template <int E>
+__device__ double qcorrect(const double *Q, const double *qz, int P, int nq, int nthreads, const double *shq,
+                           double alpha, double (&rv)[E]) {
+    if constexpr (E > 4) {          // register budget, as qdots_stage1
+        double cs = 0.0;
+        for (int i = 0; i < nq; ++i) {
+            double qa[E];
+            qload(qa, Q, qz, P, i, nq, nthreads);
+            const double c = -alpha * qdot_final(shq, i);
+            cs += c * c;
+#pragma unroll
+            for (int e = 0; e < E; ++e) rv[e] -= c * qa[e];
+        }
+        return cs;
+    }
+    double qa[E], qb[E], cs = 0.0;
+    qload(qa, Q, qz, P, 0, nq, nthreads);
+    for (int i = 0; i < nq; i += 2) {
+        qload(qb, Q, qz, P, i + 1, nq, nthreads);
+        double c = -alpha * qdot_final(shq, i);
+        cs += c * c;
+#pragma unroll
+        for (int e = 0; e < E; ++e) rv[e] -= c * qa[e];
+        qload(qa, Q, qz, P, i + 2, nq, nthreads);
+        if (i + 1 < nq) {
+            c = -alpha * qdot_final(shq, i + 1);
+            cs += c * c;
+#pragma unroll
+            for (int e = 0; e < E; ++e) rv[e] -= c * qb[e];
+        }
+    }
+    return cs;
+}
+
+// block 0 stores the new basis vector q_it = r'' / |r''| (it < QCAP)
+template <int E>
+__device__ __forceinline__ void qstore(double *Q, int P, int it, double nr, const double (&rv)[E], int nthreads) {
+    if (!Q || it >= QCAP) return;
+    const double inv = nr > 0.0 ? 1.0 / sqrt(nr) : 0.0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int q = threadIdx.x + e * nthreads;
+        if (q < P) Q[(long)it * P + q] = rv[e] * inv;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -574,7 +705,9 @@ __device__ __forceinline__ f4 scr_get(const float *scr, int row0, int c, int g) 
 // only the R chains (linear in v) are recomputed -- 40 instead of 48 MFMAs and no tanh per tile.
 // MODE 3: MODE 2 as launched inside the CG graph (K_1 ..): identical code under its own name, so a
 // kernel trace separates the standalone FVP kernel from the fused CG-iteration kernels.
-template <int T0, int T1, int T2, int T3, int ACT, int MODE>
+// QB (MODE 3 only): basis vectors of the residual reorthogonalisation loaded in the prologue's single
+// load round (slots >= A.nq read zeros); QB = 0 with an update: the streaming form (qdots_stage1).
+template <int T0, int T1, int T2, int T3, int ACT, int MODE, int QB = 0>
 __global__ void __launch_bounds__((64 * FastCfg<T0, T1, T2, T3>::WAVES))
 fvp_mlp3_kernel(IterArgs A, Net net) {
     constexpr bool FV = MODE != 1;
@@ -586,7 +719,10 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
     // push the kernel into scratch spills (and those runs were not bitwise reproducible)
     static_assert(!YC || C::REGW, "forward cache only for the small-net kernels");
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    __shared__ double sh64[20 * C::WAVES];      // 5 DPP block sums, 4 rows per wave
+    __shared__ double sh64[(5 + QB) * 4 * C::WAVES];      // 5 + QB DPP block sums, 4 rows per wave
+    // streaming basis dots of a MODE 0 update: the tile scratch, unused until the tile loop's barrier
+    double *shq = reinterpret_cast<double *>(lds + C::TLEN + C::VLEN);
+    static_assert(C::SCRATCH >= 2 * QCAP * 4 * C::WAVES, "basis-dot scratch");
     float *tw = lds;                                   // theta pack
     float *vw = lds + C::TLEN;                         // v pack (fragment order, fp32)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -696,6 +832,12 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
             ps[e] = q < A.P ? m : -1;
         }
     }
+    // the reorthogonalisation basis, in the same load round (MODE 3 kernels launched with QB > 0)
+    [[maybe_unused]] double qv[QB > 0 ? QB : 1][C::EMAX];
+    if constexpr (QB > 0) {
+#pragma unroll
+        for (int i = 0; i < QB; ++i) qload<C::EMAX>(qv[i], A.q, A.qz, A.P, i, upd ? A.nq : 0, C::THREADS);
+    }
     // plain FVP: the direction fragments gathered from v in the same load round
     float vg[C::VEMAX];
     if (vnat) {
@@ -747,6 +889,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
                     A.x[q] = 0.0;
                 }
             }
+            if (A.reorth) qstore<C::EMAX>(A.q, A.P, 0, rr, pv, C::THREADS);     // q_0 = b / |b|
             if (tid == 0) {
                 A.st_out->rdotr = rr;
                 A.st_out->xx = 0.0;
@@ -766,7 +909,11 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
         // results in all blocks); block 0 publishes the new state
         // ONE block reduction per step: p.z, r.z, z.z, x.p, p.p; then |r'|^2 = |r|^2 - 2a r.z + a^2 z.z
         // and |x'|^2 = |x|^2 + 2a x.p + a^2 p.p in fp64 (algebraically the reference's r.r / x.x)
-        double red[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+        // + the basis dots q_i . z of the residual reorthogonalisation (QB of them in registers, or the
+        // streaming stage 1 into shq), in the same single barrier
+        double red[5 + QB];
+#pragma unroll
+        for (int k = 0; k < 5 + QB; ++k) red[k] = 0.0;
 #pragma unroll
         for (int e = 0; e < C::EMAX; ++e) {
             const int q = tid + e * C::THREADS;
@@ -776,17 +923,42 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
             red[2] += zv[e] * zv[e];
             red[3] += xv[e] * pv[e];
             red[4] += pv[e] * pv[e];
+#pragma unroll
+            for (int i = 0; i < QB; ++i) red[5 + i] += qv[i][e] * zv[e];
+        }
+        if constexpr (QB == 0) {
+            if (A.reorth && A.nq > 0) qdots_stage1<C::EMAX>(A.q, A.qz, A.P, A.nq, zv, C::THREADS, shq);
         }
         STAMP(8);
-        block_sums_dpp<5>(red, sh64);
+        block_sums_dpp<5 + QB>(red, sh64);
         STAMP(9);
         const double alpha = sin.rdotr / red[0];
+        // coefficient along the current residual r (unit vector r / |r|): |r| - alpha (r . z) / |r|
+        double cs = 0.0, cr = 0.0;
+        if (A.reorth && sin.rdotr > 0.0) {
+            const double nrm = sqrt(sin.rdotr), cl = nrm - alpha * (red[1] / nrm);
+            cs = cl * cl;
+            cr = cl / nrm;
+        }
 #pragma unroll
         for (int e = 0; e < C::EMAX; ++e) {
+            const double r0 = rv[e];
             rv[e] -= alpha * zv[e];
+            rv[e] -= cr * r0;
             xv[e] += alpha * pv[e];
         }
-        const double nr = sin.rdotr - 2.0 * alpha * red[1] + alpha * alpha * red[2];
+        if constexpr (QB > 0) {
+#pragma unroll
+            for (int i = 0; i < QB; ++i) {
+                const double c = -alpha * red[5 + i];       // zero for the slots >= nq
+                cs += c * c;
+#pragma unroll
+                for (int e = 0; e < C::EMAX; ++e) rv[e] -= c * qv[i][e];
+            }
+        } else {
+            if (A.reorth && A.nq > 0) cs += qcorrect<C::EMAX>(A.q, A.qz, A.P, A.nq, C::THREADS, shq, alpha, rv);
+        }
+        const double nr = sin.rdotr - 2.0 * alpha * red[1] + alpha * alpha * red[2] - cs;
         const double xn2 = sin.xx + 2.0 * alpha * red[3] + alpha * alpha * red[4];
         STAMP(10);
         const double beta = nr / sin.rdotr;
@@ -802,6 +974,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
         }
         const int it = sin.iter + 1;
         const int done = (nr < cth || it >= cmax) ? 1 : 0;
+        if (blockIdx.x == 0 && A.reorth) qstore<C::EMAX>(A.q, A.P, it, nr, rv, C::THREADS);
         if (blockIdx.x == 0 && tid == 0) {
             A.st_out->rdotr = nr;
             A.st_out->xx = xn2;
@@ -1523,8 +1696,11 @@ fvp_coop_kernel(IterArgs A, Net net) {
     if constexpr (UPD) {
         // ---- CG step j-1 -> j; z = F p_{j-1} arrives reduced (un-normalised) in acc_in ----
         constexpr int EP = (Q::PMAX + Q::THREADS - 1) / Q::THREADS;
-        __shared__ double shc[96];                         // block_sums_dpp<1> | <2>, <= 8 waves
-        double *sp = reinterpret_cast<double *>(lds);      // p_j (aliases the tile exchange buffers)
+        // p_j, then the block-sum and basis-dot scratch, alias the tile exchange buffers (the fused
+        // path requires MAIN_BYTES >= 8 (P + 2 + COOP_SH_EXTRA), see trpo_dev_create)
+        double *sp = reinterpret_cast<double *>(lds);
+        double *shc = sp + ((A.P + 1) & ~1);               // block_sums_dpp<2> | <2>, <= 8 waves
+        double *shq = shc + 128;                           // streaming basis dots (reorthogonalisation)
         const CgSt sin = *A.st_in;
         const double cn = A.ctl->n_total, clam = A.ctl->damping, cth = A.ctl->resth;
         const int cmax = A.ctl->maxiter;
@@ -1540,24 +1716,35 @@ fvp_coop_kernel(IterArgs A, Net net) {
             xv[e] = (in && b0) ? x0 : 0.0;
             zv[e] = q < A.nw ? z0 : 0.0;
         }
-        double s1[1] = {0.0};
+        double s1[2] = {0.0, 0.0};
 #pragma unroll
         for (int e = 0; e < EP; ++e) {                     // z = sum/N + lambda p; log-std block 2p + lambda p
             const int q = tid + e * Q::THREADS;
             zv[e] = (q < A.nw ? zv[e] / cn : 2.0 * pv[e]) + clam * pv[e];
             s1[0] += pv[e] * zv[e];
+            s1[1] += rv[e] * zv[e];
         }
-        block_sums_dpp<1>(s1, shc);
+        const bool ro = A.reorth && sin.rdotr > 0.0;
+        if (ro && A.nq > 0) qdots_stage1<EP>(A.q, A.qz, A.P, A.nq, zv, Q::THREADS, shq);
+        block_sums_dpp<2>(s1, shc);
         const double alpha = sin.rdotr / s1[0];
+        // residual reorthogonalisation (see QCAP): along r itself, then along the stored basis
+        const double cr = ro ? (sqrt(sin.rdotr) - alpha * (s1[1] / sqrt(sin.rdotr))) / sqrt(sin.rdotr) : 0.0;
+#pragma unroll
+        for (int e = 0; e < EP; ++e) {
+            const double r0 = rv[e];
+            xv[e] += alpha * pv[e];
+            rv[e] -= alpha * zv[e];
+            rv[e] -= cr * r0;
+        }
+        if (ro && A.nq > 0) qcorrect<EP>(A.q, A.qz, A.P, A.nq, Q::THREADS, shq, alpha, rv);
         double s2[2] = {0.0, 0.0};
 #pragma unroll
         for (int e = 0; e < EP; ++e) {
-            xv[e] += alpha * pv[e];
-            rv[e] -= alpha * zv[e];
             s2[0] += rv[e] * rv[e];
             s2[1] += xv[e] * xv[e];
         }
-        block_sums_dpp<2>(s2, shc + 32);
+        block_sums_dpp<2>(s2, shc + 64);
         const double nr = s2[0], beta = nr / sin.rdotr;
 #pragma unroll
         for (int e = 0; e < EP; ++e) {
@@ -1574,6 +1761,7 @@ fvp_coop_kernel(IterArgs A, Net net) {
         }
         const int it = sin.iter + 1;
         const int done = (nr < cth || it >= cmax) ? 1 : 0;
+        if (b0 && A.reorth) qstore<EP>(A.q, A.P, it, nr, rv, Q::THREADS);
         if (b0 && tid == 0) {
             A.st_out->rdotr = nr;
             A.st_out->xx = s2[1];
@@ -2075,7 +2263,7 @@ template <int E>
 __global__ void __launch_bounds__(1024)
 cg_init_kernel(const double *__restrict__ b, double *x, double *r, double *p, int P, Ctl *ctl, CgSt *st,
                double *hist, int maxiter, double resth, const int *__restrict__ vmap, void *vpack,
-               int vlen, int f64, double *acc_zero, int zero_len) {
+               int vlen, int f64, double *acc_zero, int zero_len, double *qbuf) {
     __shared__ double sh[16];
     extern __shared__ double sp[];
     double bv[E];
@@ -2100,6 +2288,7 @@ cg_init_kernel(const double *__restrict__ b, double *x, double *r, double *p, in
         }
     }
     const double rr = block_sum(s, sh);
+    qstore<E>(qbuf, P, 0, rr, bv, 1024);              // q_0 = b / |b| (reorthogonalisation basis; NULL: off)
     if (threadIdx.x == 0) {
         ctl->maxiter = maxiter;
         ctl->resth = resth;
@@ -2124,10 +2313,16 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
                  const double *__restrict__ r_in, double *p_out, double *r_out, double *x, int P, int nw, Ctl *ctl,
                  const CgSt *st_in, CgSt *st_out, double *hist,
                  const int *__restrict__ vmap, void *vpack, int vlen, int f64,
+                 double *qbuf, const double *__restrict__ qz, int nq,
                  double *acc_zero = nullptr, int zero_len = 0) {
     // acc_zero: the atomic target of the NEXT solve's first FVP (which also runs the CG start),
     // zeroed here once this step has consumed its input
-    __shared__ double sh[64 + 128];                  // block_sums_dpp<1> and <2> regions (16 waves)
+    // few elements per thread (small P): the reorthogonalisation basis joins the single load round and
+    // the first block reduction (QREG); otherwise the streaming form
+    constexpr bool QREG = E <= 2;
+    constexpr int NS1 = 2 + (QREG ? QCAP : 0);
+    __shared__ double sh[NS1 * 64 + 128];            // block_sums_dpp<NS1> | <2> regions (16 waves)
+    __shared__ double shq[QREG ? 1 : QCAP * 4 * 16]; // streaming basis dots
     const int done = ctl->done;
     const double n = ctl->n_total, lam = ctl->damping, th = ctl->resth;
     const int maxiter = ctl->maxiter;
@@ -2148,30 +2343,63 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
             if (k < R_in && q < nw) z += acc[(long)k * P + q];
         zv[e] = z;
     }
+    [[maybe_unused]] double qv[QREG ? QCAP : 1][E];
+    if constexpr (QREG) {
+#pragma unroll
+        for (int i = 0; i < QCAP; ++i) qload<E>(qv[i], qbuf, qz, P, i, qbuf ? nq : 0, 1024);
+    }
     if (done) {
         for (int e = threadIdx.x; e < zero_len; e += 1024) acc_zero[e] = 0.0;   // inputs unused
         return;
     }
-    double pz = 0.0;
+    double s1[NS1];
+#pragma unroll
+    for (int k = 0; k < NS1; ++k) s1[k] = 0.0;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const int q = threadIdx.x + e * 1024;
         zv[e] = (q < nw ? zv[e] / n : 2.0 * pv[e]) + lam * pv[e];
-        pz += pv[e] * zv[e];
+        s1[0] += pv[e] * zv[e];
+        s1[1] += rv[e] * zv[e];
+        if constexpr (QREG) {
+#pragma unroll
+            for (int i = 0; i < QCAP; ++i) s1[2 + i] += qv[i][e] * zv[e];
+        }
     }
-    double s1[1] = {pz};
-    block_sums_dpp<1>(s1, sh);
+    const bool ro = qbuf != nullptr && sin.rdotr > 0.0;     // residual reorthogonalisation (QCAP)
+    if constexpr (!QREG) {
+        if (ro && nq > 0) qdots_stage1<E>(qbuf, qz, P, nq, zv, 1024, shq);
+    }
+    block_sums_dpp<NS1>(s1, sh);
     const double alpha = sin.rdotr / s1[0];
+    const double cr = ro ? (sqrt(sin.rdotr) - alpha * (s1[1] / sqrt(sin.rdotr))) / sqrt(sin.rdotr) : 0.0;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const double r0 = rv[e];
+        xv[e] += alpha * pv[e];
+        rv[e] -= alpha * zv[e];
+        rv[e] -= cr * r0;
+    }
+    if constexpr (QREG) {
+        if (ro) {
+#pragma unroll
+            for (int i = 0; i < QCAP; ++i) {
+                const double c = -alpha * s1[2 + i];         // zero for the slots >= nq
+#pragma unroll
+                for (int e = 0; e < E; ++e) rv[e] -= c * qv[i][e];
+            }
+        }
+    } else {
+        if (ro && nq > 0) qcorrect<E>(qbuf, qz, P, nq, 1024, shq, alpha, rv);
+    }
     double rr = 0.0, xx = 0.0;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-        xv[e] += alpha * pv[e];
-        rv[e] -= alpha * zv[e];
         rr += rv[e] * rv[e];
         xx += xv[e] * xv[e];
     }
     double s2[2] = {rr, xx};
-    block_sums_dpp<2>(s2, sh + 64);
+    block_sums_dpp<2>(s2, sh + NS1 * 64);
     const double nr = s2[0], xn = s2[1];
     const double beta = nr / sin.rdotr;
     extern __shared__ double sp[];
@@ -2190,6 +2418,7 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
         __syncthreads();
         write_vpack(sp, vm, vpack, vlen, f64);
     }
+    qstore<E>(qbuf, P, sin.iter + 1, nr, rv, 1024);
     if (threadIdx.x == 0) {
         const int it = sin.iter + 1;
         st_out->rdotr = nr;
@@ -2210,11 +2439,14 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
 // ===========================================================================
 typedef void (*fast_launch_fn)(dim3, int, hipStream_t, const IterArgs &, const Net &);
 
-template <int T0, int T1, int T2, int T3, int ACT, int MODE>
+template <int T0, int T1, int T2, int T3, int ACT, int MODE, int QB = 0>
 static void fast_launch(dim3 g, int lds, hipStream_t st, const IterArgs &a, const Net &net) {
-    hipLaunchKernelGGL((fvp_mlp3_kernel<T0, T1, T2, T3, ACT, MODE>), g, dim3(64 * FastCfg<T0, T1, T2, T3>::WAVES), lds,
-                       st, a, net);
+    hipLaunchKernelGGL((fvp_mlp3_kernel<T0, T1, T2, T3, ACT, MODE, QB>), g, dim3(64 * FastCfg<T0, T1, T2, T3>::WAVES),
+                       lds, st, a, net);
 }
+// MODE 3 kernels by the reorthogonalisation basis they load in their prologue (QB slots)
+constexpr int kQB[4] = {0, 4, 8, QCAP};
+static int qb_index(int nq) { return nq <= 0 ? 0 : nq <= 4 ? 1 : nq <= 8 ? 2 : 3; }
 
 // CG kernels are templated on the per-thread element count E = ceil(P / 1024)
 static int cg_E(int P) {
@@ -2239,18 +2471,23 @@ static hipError_t fast_attr(int lds) {
         e = hipFuncSetAttribute((const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 2>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return e;
-        e = hipFuncSetAttribute((const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 3>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        if (e != hipSuccess) return e;
+        const void *k3[4] = {(const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 3, kQB[0]>,
+                             (const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 3, kQB[1]>,
+                             (const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 3, kQB[2]>,
+                             (const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 3, kQB[3]>};
+        for (const void *k : k3) {
+            e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+            if (e != hipSuccess) return e;
+        }
     }
     return hipFuncSetAttribute((const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 1>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 }
 
 // MODE 2 (forward cache) exists for the register-resident small-net shapes only
-template <int T0, int T1, int T2, int T3, int ACT, int MODE>
+template <int T0, int T1, int T2, int T3, int ACT, int MODE, int QB = 0>
 static constexpr fast_launch_fn yc_launch() {
-    if constexpr (FastCfg<T0, T1, T2, T3>::REGW) return fast_launch<T0, T1, T2, T3, ACT, MODE>;
+    if constexpr (FastCfg<T0, T1, T2, T3>::REGW) return fast_launch<T0, T1, T2, T3, ACT, MODE, QB>;
     else return nullptr;
 }
 
@@ -2260,7 +2497,7 @@ struct FastEntry {
     fast_launch_fn launch;
     fast_launch_fn launch_pg;    // MODE 1: policy gradient
     fast_launch_fn launch_yc;    // MODE 2: FVP on the cached forward activations
-    fast_launch_fn launch_yc_cg; // MODE 3: the same inside the CG graph
+    fast_launch_fn launch_yc_cg[4]; // MODE 3: the same inside the CG graph, by reorthogonalisation slots kQB
     hipError_t (*attr)(int);
     int lds, tlen, vlen, slab, emax, waves;
 };
@@ -2268,7 +2505,9 @@ struct FastEntry {
 #define ACT_TTL (ACT_T | (ACT_T << 2) | (ACT_L << 4))
 #define FAST_ENTRY(a, b, c, d, act)                                                                               \
     {{a, b, c, d}, act, fast_launch<a, b, c, d, act, 0>, fast_launch<a, b, c, d, act, 1>,                         \
-     yc_launch<a, b, c, d, act, 2>(), yc_launch<a, b, c, d, act, 3>(), fast_attr<a, b, c, d, act>,                \
+     yc_launch<a, b, c, d, act, 2>(),                                                                             \
+     {yc_launch<a, b, c, d, act, 3, kQB[0]>(), yc_launch<a, b, c, d, act, 3, kQB[1]>(),                           \
+      yc_launch<a, b, c, d, act, 3, kQB[2]>(), yc_launch<a, b, c, d, act, 3, kQB[3]>()}, fast_attr<a, b, c, d, act>, \
      FastCfg<a, b, c, d>::lds_bytes(), FastCfg<a, b, c, d>::TLEN, FastCfg<a, b, c, d>::VLEN,                      \
      FastCfg<a, b, c, d>::SLAB, FastCfg<a, b, c, d>::EMAX, FastCfg<a, b, c, d>::WAVES}
 #define FAST_SHAPE(a, b, c, d) FAST_ENTRY(a, b, c, d, ACT_TTL), FAST_ENTRY(a, b, c, d, -1)
@@ -2344,6 +2583,9 @@ struct trpo_dev {
     int coop_fused;             // CG step fused into the cooperative FVP kernel (MODE 2)
     fast_launch_fn k_fvp, k_pg; // the tile kernel serving this shape, FVP and policy-gradient modes
     fast_launch_fn k_fvp_yc, k_cg_yc;   // the same kernel on the forward cache: standalone FVP, CG iteration
+    fast_launch_fn k_cg_yc_q[4];        // one-wave-per-tile CG iteration by reorthogonalisation slots (kQB)
+    double *qbuf, *qzero;               // reorthogonalisation basis [QCAP][P] and a zero line
+    int reorth;                         // TRPO_CG_REORTH (default 1)
     int k_lds, k_tiles;         // its dynamic LDS bytes and tiles per block per step
     Pack pack;
     int f64;                    // fp64 precision mode: fp64 packs/observations/slabs, fp64 MFMA kernel
@@ -2622,6 +2864,12 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
         if (d->R > 8) d->R = 8;
     }
     DMALLOC(d->accbuf, sizeof(double) * 3 * d->R * d->P);
+    DMALLOC(d->qbuf, sizeof(double) * QCAP * d->P);
+    DMALLOC(d->qzero, sizeof(double) * 64);
+    {
+        const char *eo = getenv("TRPO_CG_REORTH");
+        d->reorth = !(eo && atoi(eo) == 0);
+    }
     DMALLOC(d->pacc, sizeof(double) * 2 * d->R * d->P);
     d->Rc = d->R;
     if (d->fast) {
@@ -2682,7 +2930,9 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
             d->k_tiles = d->coop_e->ng;
             d->slab = d->coop_e->slab;
             const char *ef = getenv("TRPO_COOP_FUSED");
-            d->coop_fused = !(ef && atoi(ef) == 0) && (size_t)d->coop_e->main_bytes >= sizeof(double) * d->P;
+            d->coop_fused = !(ef && atoi(ef) == 0) &&
+                            (size_t)d->coop_e->main_bytes >=
+                                sizeof(double) * (d->P + 2 + 128 + QCAP * 4 * (d->coop_e->threads / 64));
             DMALLOC(d->imap, sizeof(int) * d->slab);
             hipLaunchKernelGGL(build_imap_coop_kernel, dim3(cdiv(d->slab, 256)), dim3(256), 0, d->stream, n, T[0],
                                T[1], d->f64, d->imap, d->slab);
@@ -2701,7 +2951,8 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
                 if (n.act[3] == ACT_T || n.act[3] == ACT_S) d->k_fvp_yc = d->k_cg_yc = NULL;
             } else {
                 d->k_fvp_yc = d->fast->launch_yc;
-                d->k_cg_yc = d->fast->launch_yc_cg;
+                d->k_cg_yc = d->fast->launch_yc_cg[0];
+                for (int i = 0; i < 4; ++i) d->k_cg_yc_q[i] = d->fast->launch_yc_cg[i];
             }
             d->yc_on = d->k_fvp_yc && d->k_cg_yc && !(ey && atoi(ey) == 0);
         }
@@ -2741,7 +2992,7 @@ extern "C" void trpo_dev_destroy(trpo_dev *d) {
     if (d->comm) ncclCommDestroy(d->comm);
     trpo_update_state_free(d->upd);
     void *ptrs[] = {d->obs64, d->pg_d, d->pg_adv, d->pg_iv, d->st, d->pbuf[0], d->pbuf[1], d->rbuf[0], d->rbuf[1], d->accbuf, d->pacc, d->imap, d->tpack, d->vpack, d->tmap, d->vmap, d->pslot, d->obs4, d->yc, d->th32, d->v32, d->iv32, d->obs32, d->scratch,
-                    d->theta64, d->std64, d->r, d->zacc, d->slabs, d->ctl, d->hist, d->tscr};
+                    d->theta64, d->std64, d->r, d->zacc, d->slabs, d->ctl, d->hist, d->tscr, d->qbuf, d->qzero};
     for (void *p : ptrs)
         if (p) hipFree(p);
     for (int i = 0; i < 5; ++i)
@@ -3276,10 +3527,22 @@ static int allreduce(trpo_dev *d, double *buf, size_t count) {
 }
 
 // per-iteration arguments of the fused CG-iteration kernel K_j beyond the CG state
+// (reorthogonalisation: step j-1 -> j uses the stored basis q_0 .. q_{j-2}, capped at QCAP)
 static void cg_iter_args_extra(trpo_dev *d, IterArgs &a, long j) {
-    (void)d;
-    (void)a;
-    (void)j;
+    a.reorth = d->reorth;
+    a.q = d->reorth ? d->qbuf : nullptr;
+    a.qz = d->qzero;
+    a.nq = d->reorth ? (int)(j - 1 < QCAP ? j - 1 : QCAP) : 0;
+}
+// the CG-iteration kernel K_j (j >= 1) of the fused paths
+static fast_launch_fn cg_iter_kernel(trpo_dev *d, const IterArgs &a) {
+    if (d->coop) return d->yc_on ? d->k_cg_yc : d->coop_e->launch_cg;
+    if (!d->yc_on) return d->k_fvp;                       // MODE 0 with the streaming reorthogonalisation
+    return d->k_cg_yc_q[qb_index(a.nq)];
+}
+// arguments of the last CG step (after FVP M-1) and of every step of the unfused paths
+static int cg_step_nq(const trpo_dev *d, long sin_iter) {
+    return d->reorth ? (int)(sin_iter < QCAP ? sin_iter : QCAP) : 0;
 }
 
 // CG(maxiter) as a straight-line launch sequence (captured into a hipGraph by trpo_dev_cg).
@@ -3299,7 +3562,7 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
     if (!fused_init)
         CG_DISPATCH(E, cg_init_kernel, dim3(1), dim3(1024), shm, d->stream, b, x, d->rbuf[0], d->pbuf[0], d->P,
                     d->ctl, d->st, d->hist, (int)maxiter, resth, d->vmap, d->vpack, vlen, d->f64,
-                    d->atomic ? acc_slot(d, 0) : nullptr, d->atomic ? RP : 0);
+                    d->atomic ? acc_slot(d, 0) : nullptr, d->atomic ? RP : 0, d->reorth ? d->qbuf : nullptr);
     if (d->fast && !d->coop) {
         for (long j = 0; j < M; ++j) {
             IterArgs a = plain_args(d, j == 0 ? &d->ctl->zero : done);
@@ -3314,6 +3577,8 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
                 a.st_out = d->st;
                 a.ctl = d->ctl;
                 a.hist = d->hist;
+                a.reorth = d->reorth;
+                a.q = d->reorth ? d->qbuf : nullptr;
             }
             if (d->atomic) {
                 a.acc_out = acc_slot(d, j);
@@ -3336,10 +3601,11 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
                 a.ctl = d->ctl;
                 a.hist = d->hist;
                 a.vmap = d->vmap;
+                cg_iter_args_extra(d, a, j);
             }
             // K_0 refreshes the forward-activation cache, K_1.. read it (theta is fixed in a solve)
             if (d->yc_on) a.yc = reinterpret_cast<float4 *>(d->yc);
-            (j > 0 && d->yc_on ? d->k_cg_yc : d->k_fvp)(dim3(d->grid), d->k_lds, d->stream, a, d->net);
+            (j > 0 ? cg_iter_kernel(d, a) : d->k_fvp)(dim3(d->grid), d->k_lds, d->stream, a, d->net);
             int rc;
             if (d->atomic) {
                 rc = allreduce(d, acc_slot(d, j), (size_t)RP);
@@ -3354,7 +3620,8 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
             CG_DISPATCH(E, cg_update_kernel, dim3(1), dim3(1024), 0, d->stream,
                         d->atomic ? acc_slot(d, M - 1) : d->zacc, d->atomic ? d->Rc : 1, d->pbuf[in], d->rbuf[in],
                         d->pbuf[out], d->rbuf[out], x, d->P, d->nw, d->ctl, d->st + in, d->st + out, d->hist,
-                        (const int *)nullptr, (void *)nullptr, 0, 0, d->atomic ? acc_slot(d, 0) : nullptr,
+                        (const int *)nullptr, (void *)nullptr, 0, 0, d->reorth ? d->qbuf : nullptr,
+                        (const double *)d->qzero, cg_step_nq(d, M - 1), d->atomic ? acc_slot(d, 0) : nullptr,
                         d->atomic ? RP : 0);
         }
     } else if (d->coop_fused) {
@@ -3376,11 +3643,11 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
                 a.st_out = d->st + out;
                 a.ctl = d->ctl;
                 a.hist = d->hist;
+                cg_iter_args_extra(d, a, j);
             }
             // K_0 refreshes the forward-activation cache (fp32), K_1.. read it
             if (d->yc_on) a.yc = reinterpret_cast<float4 *>(d->yc);
-            (j > 0 ? (d->yc_on ? d->k_cg_yc : d->coop_e->launch_cg) : d->k_fvp)(dim3(d->grid), d->k_lds, d->stream, a,
-                                                                             d->net);
+            (j > 0 ? cg_iter_kernel(d, a) : d->k_fvp)(dim3(d->grid), d->k_lds, d->stream, a, d->net);
             launch_reduce(d, done);
             int rc = allreduce(d, d->zacc, d->nw);
             if (rc) return rc;
@@ -3389,7 +3656,8 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
             const int in = (int)((M - 1) & 1), out = (int)(M & 1);
             CG_DISPATCH(E, cg_update_kernel, dim3(1), dim3(1024), 0, d->stream, d->zacc, 1, d->pbuf[in], d->rbuf[in],
                         d->pbuf[out], d->rbuf[out], x, d->P, d->nw, d->ctl, d->st + in, d->st + out, d->hist,
-                        (const int *)nullptr, (void *)nullptr, 0, 0);
+                        (const int *)nullptr, (void *)nullptr, 0, 0, d->reorth ? d->qbuf : nullptr,
+                        (const double *)d->qzero, cg_step_nq(d, M - 1));
         }
     } else {
         // generic or cooperative kernel: FVP, reduce, [all-reduce], CG step per iteration
@@ -3400,7 +3668,8 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
             // cooperative kernel: the update also packs p' for the next FVP (fp32 fragment order)
             CG_DISPATCH(E, cg_update_kernel, dim3(1), dim3(1024), d->coop ? shm : 0, d->stream, d->zacc, 1,
                         d->pbuf[cur], d->rbuf[cur], d->pbuf[nxt], d->rbuf[nxt], x, d->P, d->nw, d->ctl, d->st + cur,
-                        d->st + nxt, d->hist, d->vmap, d->vpack, d->coop ? vlen : 0, d->f64);
+                        d->st + nxt, d->hist, d->vmap, d->vpack, d->coop ? vlen : 0, d->f64,
+                        d->reorth ? d->qbuf : nullptr, (const double *)d->qzero, cg_step_nq(d, j));
         }
     }
     HCHK(hipGetLastError());
@@ -3506,7 +3775,7 @@ extern "C" int trpo_dev_sync(trpo_dev *d) {
 // scratch (p, r, x, the scalar state, the history, a sink replica set) so that repeated launches
 // leave the context's solve untouched and never reach the convergence exit.  Inputs are the state
 // of the last solve.  Returns 1 when this context has no fused CG-iteration kernel.
-static int cg_iter_kernel_only(trpo_dev *d, long j) {
+static int cg_iter_kernel_only(trpo_dev *d, long j, bool init) {
     const bool fused = d->fast && (!d->coop || d->coop_fused);
     if (!fused) return 1;
     if (!d->tscr) {
@@ -3517,7 +3786,7 @@ static int cg_iter_kernel_only(trpo_dev *d, long j) {
     double *sp = (double *)d->tscr, *sr = sp + d->P, *sx = sr + d->P, *sh = sx + d->P;
     CgSt *sst = (CgSt *)(sh + 2 * 65);
     Ctl *sctl = (Ctl *)(sst + 2);
-    {   // the scratch control block never reports convergence; the scratch state is at iteration 0
+    if (init) {   // the scratch control block never reports convergence; the scratch state is at iteration 0
         Ctl c;
         CgSt st;
         HCHK(hipMemcpyAsync(&c, d->ctl, sizeof c, hipMemcpyDeviceToHost, d->stream));
@@ -3555,8 +3824,7 @@ static int cg_iter_kernel_only(trpo_dev *d, long j) {
     }
     cg_iter_args_extra(d, a, j);
     if (d->yc_on) a.yc = reinterpret_cast<float4 *>(d->yc);
-    fast_launch_fn k = d->coop ? (d->yc_on ? d->k_cg_yc : d->coop_e->launch_cg) : (d->yc_on ? d->k_cg_yc : d->k_fvp);
-    k(dim3(d->grid), d->k_lds, d->stream, a, d->net);
+    cg_iter_kernel(d, a)(dim3(d->grid), d->k_lds, d->stream, a, d->net);
     HCHK(hipGetLastError());
     return 0;
 }
@@ -3571,12 +3839,12 @@ extern "C" double trpo_dev_time(trpo_dev *d, int what, int reps, size_t maxiter,
         if (maxiter < 2) return -1;
         rc = trpo_dev_cg(d, maxiter, resth);
         if (rc) return rc;
-        rc = cg_iter_kernel_only(d, 1);
+        rc = cg_iter_kernel_only(d, 1, true);
         if (rc) return rc > 0 ? -1 : rc;
         if (hipStreamSynchronize(d->stream) != hipSuccess) return -2;
         hipEventRecord(d->ev0, d->stream);
         for (long j = 1; j < (long)maxiter && !rc; ++j)
-            for (int i = 0; i < reps && !rc; ++i) rc = cg_iter_kernel_only(d, j);
+            for (int i = 0; i < reps && !rc; ++i) rc = cg_iter_kernel_only(d, j, false);
         hipEventRecord(d->ev1, d->stream);
         if (rc) return rc;
         if (hipEventSynchronize(d->ev1) != hipSuccess) return -2;
