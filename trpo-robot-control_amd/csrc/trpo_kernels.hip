@@ -146,28 +146,81 @@ __device__ __forceinline__ double readlane64(double v, int l) {
     const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
-// block-wide fp64 sums of K values with ONE barrier: DPP row sums, the (waves x 4 rows) partials
-// through LDS, then every wave sums them again with DPP rows + 4 lane reads -- the same fixed
-// order in every wave and block.  Blocks of <= 16 waves.  sh must hold K * 4 * waves doubles and
-// must not be reused by another call before the block passes another barrier.
-template <int K>
+// fp64 half exchanges across a wave (gfx950 v_permlane32_swap / v_permlane16_swap, one per dword):
+// swap32: lanes 32-63 of a <-> lanes 0-31 of b;  swap16: odd 16-lane rows of a <-> even rows of b
+__device__ __forceinline__ void swap32_f64(double &a, double &b) {
+    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)__double2loint(a), (unsigned)__double2loint(b), false,
+                                                     false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)__double2hiint(a), (unsigned)__double2hiint(b), false,
+                                                     false);
+    a = __hiloint2double((int)hi[0], (int)lo[0]);
+    b = __hiloint2double((int)hi[1], (int)lo[1]);
+}
+__device__ __forceinline__ void swap16_f64(double &a, double &b) {
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)__double2loint(a), (unsigned)__double2loint(b), false,
+                                                     false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)__double2hiint(a), (unsigned)__double2hiint(b), false,
+                                                     false);
+    a = __hiloint2double((int)hi[0], (int)lo[0]);
+    b = __hiloint2double((int)hi[1], (int)lo[1]);
+}
+// block-wide fp64 sums of K values (blocks of W waves, W <= 16) with ONE barrier; every thread gets
+// the K totals (wave-uniform).  Per wave a transpose-reduce: the K values (padded to KP = 4, 8, 16
+// or 32) are halved twice across the half-waves and the 16-lane rows by permlane swaps -- each step
+// adds lane l and its partner in a fixed order and leaves half the values per lane -- then each of
+// the KP/4 registers is summed over its rows with DPP; row r of register k then holds the wave's
+// total of value k + (r & 1) KP/4 + (r >> 1) KP/2.  Those go to LDS ([wave][value]); after the
+// barrier lane v sums value v over the waves in wave order and the totals are read out of lanes.
+// Fixed order throughout, so every wave and block gets bit-identical totals.  ~2K + 8 VALU
+// cross-lane steps per wave instead of 12K for K separate DPP+readlane reductions.
+// sh must hold W * KP doubles and must not be reused by another call before the block passes
+// another barrier.
+template <int K, int W>
 __device__ __forceinline__ void block_sums_dpp(double (&v)[K], double *sh) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nr = (blockDim.x >> 6) * 4;
+    static_assert(K >= 1 && K <= 32 && W >= 1 && W <= 16, "block_sums_dpp");
+    constexpr int KP = K <= 4 ? 4 : K <= 8 ? 8 : K <= 16 ? 16 : 32;
+    constexpr int H = KP / 2, Q = KP / 4;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, row = lane >> 4;
+    double t[KP];
 #pragma unroll
-    for (int k = 0; k < K; ++k) v[k] = rowsum16_f64(v[k]);
+    for (int k = 0; k < KP; ++k) t[k] = k < K ? v[k] : 0.0;
+#pragma unroll
+    for (int k = 0; k < H; ++k) {               // lanes 0-31: value k, lanes 32-63: value k + H
+        swap32_f64(t[k], t[k + H]);
+        t[k] = t[k] + t[k + H];
+    }
+#pragma unroll
+    for (int k = 0; k < Q; ++k) {               // rows 0..3: values k, k + Q, k + H, k + Q + H
+        swap16_f64(t[k], t[k + Q]);
+        t[k] = t[k] + t[k + Q];
+    }
+#pragma unroll
+    for (int k = 0; k < Q; ++k) t[k] = rowsum16_f64(t[k]);
     if ((lane & 15) == 0) {
+        const int off = w * KP + (row & 1) * Q + (row >> 1) * H;
 #pragma unroll
-        for (int k = 0; k < K; ++k) sh[k * nr + w * 4 + (lane >> 4)] = v[k];
+        for (int k = 0; k < Q; ++k) sh[off + k] = t[k];
     }
     __syncthreads();
-    double t[K];
+    const int vv = lane & (KP - 1);
+    double s = sh[vv];
 #pragma unroll
-    for (int k = 0; k < K; ++k) t[k] = sh[k * nr + min(lane, nr - 1)];
+    for (int ww = 1; ww < W; ++ww) s += sh[ww * KP + vv];
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const double u = rowsum16_f64(lane < nr ? t[k] : 0.0);
-        v[k] = (readlane64(u, 0) + readlane64(u, 16)) + (readlane64(u, 32) + readlane64(u, 48));
-    }
+    for (int k = 0; k < K; ++k) v[k] = readlane64(s, k);
+}
+
+// one value through block_sums_dpp's per-wave tree (lane l + lane l+32, then + the next row, then the
+// DPP row sum): the result in lane 0 equals the wave total block_sums_dpp forms for any value, so
+// the streaming basis dots below reproduce its bits
+__device__ __forceinline__ double wave_tree_sum(double v) {
+    double a = v, b = v;
+    swap32_f64(a, b);
+    a = a + b;
+    b = a;
+    swap16_f64(a, b);
+    a = a + b;
+    return rowsum16_f64(a);
 }
 
 // two fixed-order block-wide fp64 sums at once (sh: 2 x 16 doubles)
@@ -224,13 +277,13 @@ __device__ __forceinline__ void qload(double (&dst)[E], const double *Q, const d
     }
 }
 
-// stage 1 of the dots e_i = q_i . z, i < nq (runtime): per wave the 16-lane row sums, written to
-// shq[i * 4W + 4w + row] -- block_sums_dpp's layout; a later barrier (the caller's block reduction)
-// makes them visible.  Loads of the next vector are issued before the current one is reduced.
+// stage 1 of the dots e_i = q_i . z, i < nq (runtime): per wave the total by block_sums_dpp's tree,
+// written to shq[i * W + w]; a later barrier (the caller's block reduction) makes them visible.
+// Loads of the next vector are issued before the current one is reduced.
 template <int E>
 __device__ void qdots_stage1(const double *Q, const double *qz, int P, int nq, const double (&zv)[E], int nthreads,
                              double *shq) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nr = (blockDim.x >> 6) * 4;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nwv = blockDim.x >> 6;
     if constexpr (E > 4) {          // many elements per thread: one vector at a time (register budget)
         for (int i = 0; i < nq; ++i) {
             double qa[E];
@@ -238,8 +291,8 @@ __device__ void qdots_stage1(const double *Q, const double *qz, int P, int nq, c
             double t = 0.0;
 #pragma unroll
             for (int e = 0; e < E; ++e) t += qa[e] * zv[e];
-            t = rowsum16_f64(t);
-            if ((lane & 15) == 0) shq[i * nr + w * 4 + (lane >> 4)] = t;
+            t = wave_tree_sum(t);
+            if (lane == 0) shq[i * nwv + w] = t;
         }
         return;
     }
@@ -250,25 +303,25 @@ __device__ void qdots_stage1(const double *Q, const double *qz, int P, int nq, c
         double t = 0.0;
 #pragma unroll
         for (int e = 0; e < E; ++e) t += qa[e] * zv[e];
-        t = rowsum16_f64(t);
-        if ((lane & 15) == 0) shq[i * nr + w * 4 + (lane >> 4)] = t;
+        t = wave_tree_sum(t);
+        if (lane == 0) shq[i * nwv + w] = t;
         qload(qa, Q, qz, P, i + 2, nq, nthreads);
         if (i + 1 < nq) {
             t = 0.0;
 #pragma unroll
             for (int e = 0; e < E; ++e) t += qb[e] * zv[e];
-            t = rowsum16_f64(t);
-            if ((lane & 15) == 0) shq[(i + 1) * nr + w * 4 + (lane >> 4)] = t;
+            t = wave_tree_sum(t);
+            if (lane == 0) shq[(i + 1) * nwv + w] = t;
         }
     }
 }
 
-// stage 2: e_i from the row sums, the same fixed order in every wave and block (after a barrier)
+// stage 2: e_i from the wave totals in wave order -- block_sums_dpp's order (after a barrier)
 __device__ __forceinline__ double qdot_final(const double *shq, int i) {
-    const int lane = threadIdx.x & 63, nr = (blockDim.x >> 6) * 4;
-    const double t = shq[i * nr + min(lane, nr - 1)];
-    const double u = rowsum16_f64(lane < nr ? t : 0.0);
-    return (readlane64(u, 0) + readlane64(u, 16)) + (readlane64(u, 32) + readlane64(u, 48));
+    const int nwv = blockDim.x >> 6;
+    double s = shq[i * nwv];
+    for (int w = 1; w < nwv; ++w) s += shq[i * nwv + w];
+    return s;
 }
 
 // stage 3: rv -= sum_i c_i q_i with c_i = -alpha e_i (i < nq); returns sum_i c_i^2
@@ -800,8 +853,10 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
 #pragma unroll
                 for (int k = 0; k < 8; ++k) za[k] = A.acc_in[(long)min(k, A.R_in - 1) * A.P + qz];
                 z = za[0];                                // R_in >= 1: no select on the first term
+#ifndef TRPO_ABL_R1
 #pragma unroll
                 for (int k = 1; k < 8; ++k) z += k < A.R_in ? za[k] : 0.0;
+#endif
             } else {
                 z = A.acc_in[qz];                         // slab mode: one reduced vector
             }
@@ -878,7 +933,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
             double red[1] = {0.0};
 #pragma unroll
             for (int e = 0; e < C::EMAX; ++e) red[0] += pv[e] * pv[e];
-            block_sums_dpp<1>(red, sh64);
+            block_sums_dpp<1, C::WAVES>(red, sh64);
             const double rr = red[0];
 #pragma unroll
             for (int e = 0; e < C::EMAX; ++e) {
@@ -930,7 +985,9 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
             if (A.reorth && A.nq > 0) qdots_stage1<C::EMAX>(A.q, A.qz, A.P, A.nq, zv, C::THREADS, shq);
         }
         STAMP(8);
-        block_sums_dpp<5 + QB>(red, sh64);
+#ifndef TRPO_ABL_NORED
+        block_sums_dpp<5 + QB, C::WAVES>(red, sh64);
+#endif
         STAMP(9);
         const double alpha = sin.rdotr / red[0];
         // coefficient along the current residual r (unit vector r / |r|): |r| - alpha (r . z) / |r|
@@ -1726,7 +1783,7 @@ fvp_coop_kernel(IterArgs A, Net net) {
         }
         const bool ro = A.reorth && sin.rdotr > 0.0;
         if (ro && A.nq > 0) qdots_stage1<EP>(A.q, A.qz, A.P, A.nq, zv, Q::THREADS, shq);
-        block_sums_dpp<2>(s1, shc);
+        block_sums_dpp<2, Q::THREADS / 64>(s1, shc);
         const double alpha = sin.rdotr / s1[0];
         // residual reorthogonalisation (see QCAP): along r itself, then along the stored basis
         const double cr = ro ? (sqrt(sin.rdotr) - alpha * (s1[1] / sqrt(sin.rdotr))) / sqrt(sin.rdotr) : 0.0;
@@ -1744,7 +1801,7 @@ fvp_coop_kernel(IterArgs A, Net net) {
             s2[0] += rv[e] * rv[e];
             s2[1] += xv[e] * xv[e];
         }
-        block_sums_dpp<2>(s2, shc + 64);
+        block_sums_dpp<2, Q::THREADS / 64>(s2, shc + 64);
         const double nr = s2[0], beta = nr / sin.rdotr;
 #pragma unroll
         for (int e = 0; e < EP; ++e) {
@@ -2239,10 +2296,12 @@ __global__ void acc_epilogue_kernel(double *__restrict__ acc, int R, const doubl
 // vlen == 0 otherwise).  The map entries are loaded up front with the kernel's other loads.
 constexpr int VPACK_PER_THREAD = 8;                 // vlen <= 8 * 1024 (checked at context creation)
 __device__ __forceinline__ void load_vmap(const int *__restrict__ vmap, int vlen, int (&vm)[VPACK_PER_THREAD]) {
+    // unconditional (clamped) loads: a guarded load would drain vmcnt before the next one
 #pragma unroll
     for (int k = 0; k < VPACK_PER_THREAD; ++k) {
         const int e = threadIdx.x + k * 1024;
-        vm[k] = e < vlen ? vmap[e] : -1;
+        const int m = vmap[min(e, max(vlen - 1, 0))];
+        vm[k] = e < vlen ? m : -1;
     }
 }
 __device__ __forceinline__ void write_vpack(const double *sp, const int (&vm)[VPACK_PER_THREAD], void *vpack, int vlen,
@@ -2271,9 +2330,10 @@ cg_init_kernel(const double *__restrict__ b, double *x, double *r, double *p, in
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const int q = threadIdx.x + e * 1024;
-        bv[e] = q < P ? b[q] : 0.0;
+        const double b0 = b[min(q, P - 1)];
+        bv[e] = q < P ? b0 : 0.0;
     }
-    load_vmap(vmap, vlen, vm);
+    if (vlen) load_vmap(vmap, vlen, vm);
     for (int e = threadIdx.x; e < zero_len; e += 1024) acc_zero[e] = 0.0;
     double s = 0.0;
 #pragma unroll
@@ -2329,19 +2389,24 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
     const CgSt sin = *st_in;
     double pv[E], zv[E], xv[E], rv[E];
     int vm[VPACK_PER_THREAD];
-    load_vmap(vmap, vlen, vm);
+    if (vlen) load_vmap(vmap, vlen, vm);
+    // every load unconditional (clamped index, value selected after): a load guarded by a run-time
+    // condition makes hipcc branch around it and drain vmcnt, serialising the round trips
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-        const int q = threadIdx.x + e * 1024;
+        const int q = threadIdx.x + e * 1024, qc = min(q, P - 1), qw = min(q, nw - 1);
         const bool in = q < P;
-        pv[e] = in ? p_in[q] : 0.0;
-        xv[e] = in ? x[q] : 0.0;
-        rv[e] = in ? r_in[q] : 0.0;
-        double z = 0.0;
+        const double p0 = p_in[qc], x0 = x[qc], r0 = r_in[qc];
+        double za[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-            if (k < R_in && q < nw) z += acc[(long)k * P + q];
-        zv[e] = z;
+        for (int k = 0; k < 8; ++k) za[k] = acc[(long)min(k, R_in - 1) * P + qw];
+        double z = za[0];                              // the summation order of the guarded form
+#pragma unroll
+        for (int k = 1; k < 8; ++k) z += k < R_in ? za[k] : 0.0;
+        pv[e] = in ? p0 : 0.0;
+        xv[e] = in ? x0 : 0.0;
+        rv[e] = in ? r0 : 0.0;
+        zv[e] = q < nw ? z : 0.0;
     }
     [[maybe_unused]] double qv[QREG ? QCAP : 1][E];
     if constexpr (QREG) {
@@ -2370,7 +2435,7 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
     if constexpr (!QREG) {
         if (ro && nq > 0) qdots_stage1<E>(qbuf, qz, P, nq, zv, 1024, shq);
     }
-    block_sums_dpp<NS1>(s1, sh);
+    block_sums_dpp<NS1, 16>(s1, sh);
     const double alpha = sin.rdotr / s1[0];
     const double cr = ro ? (sqrt(sin.rdotr) - alpha * (s1[1] / sqrt(sin.rdotr))) / sqrt(sin.rdotr) : 0.0;
 #pragma unroll
@@ -2399,7 +2464,7 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
         xx += xv[e] * xv[e];
     }
     double s2[2] = {rr, xx};
-    block_sums_dpp<2>(s2, sh + NS1 * 64);
+    block_sums_dpp<2, 16>(s2, sh + NS1 * 64);
     const double nr = s2[0], xn = s2[1];
     const double beta = nr / sin.rdotr;
     extern __shared__ double sp[];
@@ -2513,8 +2578,12 @@ struct FastEntry {
 #define FAST_SHAPE(a, b, c, d) FAST_ENTRY(a, b, c, d, ACT_TTL), FAST_ENTRY(a, b, c, d, -1)
 
 static const FastEntry kFast[] = {
+#ifdef TRPO_ARM_ONLY    // experiment builds (make variant): armDOF_0-class shapes only, fast to compile
+    FAST_ENTRY(1, 1, 1, 1, ACT_TTL),
+#else
     FAST_SHAPE(1, 1, 1, 1), FAST_SHAPE(1, 2, 2, 1), FAST_SHAPE(1, 4, 4, 1),
     FAST_SHAPE(2, 1, 1, 1), FAST_SHAPE(2, 2, 2, 1), FAST_SHAPE(2, 4, 4, 1),
+#endif
 };
 
 // cooperative kernels (T1 == T2 == TH, T3 == 1); element type T: fp32 or the fp64 precision mode
@@ -2567,9 +2636,13 @@ struct CoopEntry {
      CoopCfg<T, t0, th>::SLAB, CoopCfg<T, t0, th>::NG, CoopCfg<T, t0, th>::THREADS, CoopCfg<T, t0, th>::MAIN_BYTES}
 #define COOP_SHAPE(T, t0, th) COOP_ENTRY(T, t0, th, ACT_TTL), COOP_ENTRY(T, t0, th, -1)
 static const CoopEntry kCoop[] = {
+#ifdef TRPO_ARM_ONLY
+    COOP_ENTRY(double, 1, 1, ACT_TTL)};
+#else
     COOP_SHAPE(float, 1, 2),  COOP_SHAPE(float, 1, 4),  COOP_SHAPE(float, 2, 2),  COOP_SHAPE(float, 2, 4),
     COOP_SHAPE(double, 1, 1), COOP_SHAPE(double, 1, 2), COOP_SHAPE(double, 1, 4), COOP_SHAPE(double, 2, 1),
     COOP_SHAPE(double, 2, 2), COOP_SHAPE(double, 2, 4)};
+#endif
 
 struct trpo_dev {
     int device;
