@@ -109,8 +109,8 @@ struct IterArgs {
     // residual reorthogonalisation (update / init): the basis q_0 .. q_{QCAP-1} (fp64 [QCAP][P]), the
     // number of stored vectors this step uses (nq = min(iteration before the step, QCAP)), a zero line,
     // and whether reorthogonalisation is on (TRPO_CG_REORTH, default 1)
-    double *q;
-    const double *qz;
+    void *q;                      // QT [QCAP][P]: float (fp32 kernels) or double (fp64 mode)
+    const void *qz;
     int nq, reorth;
 };
 
@@ -257,22 +257,29 @@ __device__ void block_sum2(double a, double b, double *sh, double &sa, double &s
 // only the dots q_i . z join the step's block reduction.  In exact arithmetic every c is zero, so the
 // iterates are the reference's (src/TRPO_CG.c:65-103); with the fp32 FVP the step lands within 1e-7 of
 // the fp64 reference instead of 1e-3.  |r''|^2 = |r'|^2 - sum c^2.  The basis q_0 .. q_{QCAP-1} lives in
-// HBM (fp64, natural order); longer solves are reorthogonalised against the first QCAP residuals.
+// HBM (natural order); longer solves are reorthogonalised against the first QCAP residuals.
+// Basis element type QT: fp32 in the fp32-FVP paths, fp64 in the fp64 precision mode.  An fp32
+// basis is enough where the FVP itself carries fp32 noise: the projection then removes the
+// components along fl32(q_i), which leaves r'' orthogonal to the true q_i to ~3e-9 |r''| (against
+// ~1e-7 without reorthogonalisation), and the numpy emulation (tools/cg_noise_variants.py) lands
+// on the fp64-basis step to 3 digits on every CG / update golden; it halves the basis bytes every
+// block of the CG-iteration kernel loads in its prologue.  In the fp64 mode the fp32 rounding of
+// the basis (6e-8) would itself exceed the FVP noise, so that mode keeps fp64.
 // ---------------------------------------------------------------------------
 constexpr int QCAP = 16;
 
 // the thread's E elements (q = tid + e * nthreads) of basis vector i, or zeros for i >= nq / q >= P:
 // the load is unconditional (a select on the address: qz is a small zero line every lane may read)
-template <int E>
-__device__ __forceinline__ void qload(double (&dst)[E], const double *Q, const double *qz, int P, int i, int nq,
+template <int E, typename QT>
+__device__ __forceinline__ void qload(double (&dst)[E], const QT *Q, const QT *qz, int P, int i, int nq,
                                       int nthreads) {
     const int tid = threadIdx.x;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const int q = tid + e * nthreads;
         const bool ok = i < nq && q < P;
-        const double *src = ok ? Q + (long)i * P + q : qz + (tid & 7);
-        const double v = *src;
+        const QT *src = ok ? Q + (long)i * P + q : qz + (tid & 7);
+        const double v = (double)*src;
         dst[e] = ok ? v : 0.0;
     }
 }
@@ -280,8 +287,8 @@ __device__ __forceinline__ void qload(double (&dst)[E], const double *Q, const d
 // stage 1 of the dots e_i = q_i . z, i < nq (runtime): per wave the total by block_sums_dpp's tree,
 // written to shq[i * W + w]; a later barrier (the caller's block reduction) makes them visible.
 // Loads of the next vector are issued before the current one is reduced.
-template <int E>
-__device__ void qdots_stage1(const double *Q, const double *qz, int P, int nq, const double (&zv)[E], int nthreads,
+template <int E, typename QT>
+__device__ void qdots_stage1(const QT *Q, const QT *qz, int P, int nq, const double (&zv)[E], int nthreads,
                              double *shq) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nwv = blockDim.x >> 6;
     if constexpr (E > 4) {          // many elements per thread: one vector at a time (register budget)
@@ -325,8 +332,8 @@ __device__ __forceinline__ double qdot_final(const double *shq, int i) {
 }
 
 // stage 3: rv -= sum_i c_i q_i with c_i = -alpha e_i (i < nq); returns sum_i c_i^2
-template <int E>
-__device__ double qcorrect(const double *Q, const double *qz, int P, int nq, int nthreads, const double *shq,
+template <int E, typename QT>
+__device__ double qcorrect(const QT *Q, const QT *qz, int P, int nq, int nthreads, const double *shq,
                            double alpha, double (&rv)[E]) {
     if constexpr (E > 4) {          // register budget, as qdots_stage1
         double cs = 0.0;
@@ -360,14 +367,14 @@ __device__ double qcorrect(const double *Q, const double *qz, int P, int nq, int
 }
 
 // block 0 stores the new basis vector q_it = r'' / |r''| (it < QCAP)
-template <int E>
-__device__ __forceinline__ void qstore(double *Q, int P, int it, double nr, const double (&rv)[E], int nthreads) {
+template <int E, typename QT>
+__device__ __forceinline__ void qstore(QT *Q, int P, int it, double nr, const double (&rv)[E], int nthreads) {
     if (!Q || it >= QCAP) return;
     const double inv = nr > 0.0 ? 1.0 / sqrt(nr) : 0.0;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const int q = threadIdx.x + e * nthreads;
-        if (q < P) Q[(long)it * P + q] = rv[e] * inv;
+        if (q < P) Q[(long)it * P + q] = (QT)(rv[e] * inv);
     }
 }
 
@@ -775,6 +782,8 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
     __shared__ double sh64[(5 + QB) * 4 * C::WAVES];      // 5 + QB DPP block sums, 4 rows per wave
     // streaming basis dots of a MODE 0 update: the tile scratch, unused until the tile loop's barrier
     double *shq = reinterpret_cast<double *>(lds + C::TLEN + C::VLEN);
+    float *qf = reinterpret_cast<float *>(A.q);                     // fp32 reorthogonalisation basis
+    const float *qfz = reinterpret_cast<const float *>(A.qz);
     static_assert(C::SCRATCH >= 2 * QCAP * 4 * C::WAVES, "basis-dot scratch");
     float *tw = lds;                                   // theta pack
     float *vw = lds + C::TLEN;                         // v pack (fragment order, fp32)
@@ -891,7 +900,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
     [[maybe_unused]] double qv[QB > 0 ? QB : 1][C::EMAX];
     if constexpr (QB > 0) {
 #pragma unroll
-        for (int i = 0; i < QB; ++i) qload<C::EMAX>(qv[i], A.q, A.qz, A.P, i, upd ? A.nq : 0, C::THREADS);
+        for (int i = 0; i < QB; ++i) qload<C::EMAX>(qv[i], qf, qfz, A.P, i, upd ? A.nq : 0, C::THREADS);
     }
     // plain FVP: the direction fragments gathered from v in the same load round
     float vg[C::VEMAX];
@@ -944,7 +953,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
                     A.x[q] = 0.0;
                 }
             }
-            if (A.reorth) qstore<C::EMAX>(A.q, A.P, 0, rr, pv, C::THREADS);     // q_0 = b / |b|
+            if (A.reorth) qstore<C::EMAX>(qf, A.P, 0, rr, pv, C::THREADS);     // q_0 = b / |b|
             if (tid == 0) {
                 A.st_out->rdotr = rr;
                 A.st_out->xx = 0.0;
@@ -982,7 +991,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
             for (int i = 0; i < QB; ++i) red[5 + i] += qv[i][e] * zv[e];
         }
         if constexpr (QB == 0) {
-            if (A.reorth && A.nq > 0) qdots_stage1<C::EMAX>(A.q, A.qz, A.P, A.nq, zv, C::THREADS, shq);
+            if (A.reorth && A.nq > 0) qdots_stage1<C::EMAX>(qf, qfz, A.P, A.nq, zv, C::THREADS, shq);
         }
         STAMP(8);
 #ifndef TRPO_ABL_NORED
@@ -1013,7 +1022,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
                 for (int e = 0; e < C::EMAX; ++e) rv[e] -= c * qv[i][e];
             }
         } else {
-            if (A.reorth && A.nq > 0) cs += qcorrect<C::EMAX>(A.q, A.qz, A.P, A.nq, C::THREADS, shq, alpha, rv);
+            if (A.reorth && A.nq > 0) cs += qcorrect<C::EMAX>(qf, qfz, A.P, A.nq, C::THREADS, shq, alpha, rv);
         }
         const double nr = sin.rdotr - 2.0 * alpha * red[1] + alpha * alpha * red[2] - cs;
         const double xn2 = sin.xx + 2.0 * alpha * red[3] + alpha * alpha * red[4];
@@ -1031,7 +1040,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
         }
         const int it = sin.iter + 1;
         const int done = (nr < cth || it >= cmax) ? 1 : 0;
-        if (blockIdx.x == 0 && A.reorth) qstore<C::EMAX>(A.q, A.P, it, nr, rv, C::THREADS);
+        if (blockIdx.x == 0 && A.reorth) qstore<C::EMAX>(qf, A.P, it, nr, rv, C::THREADS);
         if (blockIdx.x == 0 && tid == 0) {
             A.st_out->rdotr = nr;
             A.st_out->xx = xn2;
@@ -1782,7 +1791,7 @@ fvp_coop_kernel(IterArgs A, Net net) {
             s1[1] += rv[e] * zv[e];
         }
         const bool ro = A.reorth && sin.rdotr > 0.0;
-        if (ro && A.nq > 0) qdots_stage1<EP>(A.q, A.qz, A.P, A.nq, zv, Q::THREADS, shq);
+        if (ro && A.nq > 0) qdots_stage1<EP>((const T *)A.q, (const T *)A.qz, A.P, A.nq, zv, Q::THREADS, shq);
         block_sums_dpp<2, Q::THREADS / 64>(s1, shc);
         const double alpha = sin.rdotr / s1[0];
         // residual reorthogonalisation (see QCAP): along r itself, then along the stored basis
@@ -1794,7 +1803,7 @@ fvp_coop_kernel(IterArgs A, Net net) {
             rv[e] -= alpha * zv[e];
             rv[e] -= cr * r0;
         }
-        if (ro && A.nq > 0) qcorrect<EP>(A.q, A.qz, A.P, A.nq, Q::THREADS, shq, alpha, rv);
+        if (ro && A.nq > 0) qcorrect<EP>((const T *)A.q, (const T *)A.qz, A.P, A.nq, Q::THREADS, shq, alpha, rv);
         double s2[2] = {0.0, 0.0};
 #pragma unroll
         for (int e = 0; e < EP; ++e) {
@@ -1818,7 +1827,7 @@ fvp_coop_kernel(IterArgs A, Net net) {
         }
         const int it = sin.iter + 1;
         const int done = (nr < cth || it >= cmax) ? 1 : 0;
-        if (b0 && A.reorth) qstore<EP>(A.q, A.P, it, nr, rv, Q::THREADS);
+        if (b0 && A.reorth) qstore<EP>((T *)A.q, A.P, it, nr, rv, Q::THREADS);
         if (b0 && tid == 0) {
             A.st_out->rdotr = nr;
             A.st_out->xx = s2[1];
@@ -2318,11 +2327,12 @@ __device__ __forceinline__ void write_vpack(const double *sp, const int (&vm)[VP
 }
 
 // x = 0, r = p = b, state 0; packs p for the first FVP; zeroes the first atomic target.
-template <int E>
+template <int E, typename QT>
 __global__ void __launch_bounds__(1024)
 cg_init_kernel(const double *__restrict__ b, double *x, double *r, double *p, int P, Ctl *ctl, CgSt *st,
                double *hist, int maxiter, double resth, const int *__restrict__ vmap, void *vpack,
-               int vlen, int f64, double *acc_zero, int zero_len, double *qbuf) {
+               int vlen, int f64, double *acc_zero, int zero_len, void *qbuf_v) {
+    QT *qbuf = reinterpret_cast<QT *>(qbuf_v);
     __shared__ double sh[16];
     extern __shared__ double sp[];
     double bv[E];
@@ -2367,18 +2377,20 @@ cg_init_kernel(const double *__restrict__ b, double *x, double *r, double *p, in
 // One CG step after z = F p is available as R_in fp64 partial-sum replicas (src/TRPO_CG.c:65-103):
 // used after the last FVP of a solve, and for every step of the generic (non-fused) path.
 // All global loads are issued before the first reduction.
-template <int E>
+template <int E, typename QT>
 __global__ void __launch_bounds__(1024)
 cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restrict__ p_in,
                  const double *__restrict__ r_in, double *p_out, double *r_out, double *x, int P, int nw, Ctl *ctl,
                  const CgSt *st_in, CgSt *st_out, double *hist,
                  const int *__restrict__ vmap, void *vpack, int vlen, int f64,
-                 double *qbuf, const double *__restrict__ qz, int nq,
+                 void *qbuf_v, const void *qz_v, int nq,
                  double *acc_zero = nullptr, int zero_len = 0) {
     // acc_zero: the atomic target of the NEXT solve's first FVP (which also runs the CG start),
     // zeroed here once this step has consumed its input
     // few elements per thread (small P): the reorthogonalisation basis joins the single load round and
     // the first block reduction (QREG); otherwise the streaming form
+    QT *qbuf = reinterpret_cast<QT *>(qbuf_v);
+    const QT *qz = reinterpret_cast<const QT *>(qz_v);
     constexpr bool QREG = E <= 2;
     constexpr int NS1 = 2 + (QREG ? QCAP : 0);
     __shared__ double sh[NS1 * 64 + 128];            // block_sums_dpp<NS1> | <2> regions (16 waves)
@@ -2518,15 +2530,21 @@ static int cg_E(int P) {
     const int e = (P + 1023) / 1024;
     return e <= 1 ? 1 : e <= 2 ? 2 : e <= 4 ? 4 : e <= 8 ? 8 : e <= 16 ? 16 : 32;
 }
-#define CG_DISPATCH(E, KERNEL, ...)                                                   \
+// QT: the reorthogonalisation basis element type of the context (qbuf_t)
+#define CG_DISPATCH_T(E, QT, KERNEL, ...)                                             \
     switch (E) {                                                                      \
-    case 1: hipLaunchKernelGGL(KERNEL<1>, __VA_ARGS__); break;                        \
-    case 2: hipLaunchKernelGGL(KERNEL<2>, __VA_ARGS__); break;                        \
-    case 4: hipLaunchKernelGGL(KERNEL<4>, __VA_ARGS__); break;                        \
-    case 8: hipLaunchKernelGGL(KERNEL<8>, __VA_ARGS__); break;                        \
-    case 16: hipLaunchKernelGGL(KERNEL<16>, __VA_ARGS__); break;                      \
-    default: hipLaunchKernelGGL(KERNEL<32>, __VA_ARGS__); break;                      \
+    case 1: hipLaunchKernelGGL((KERNEL<1, QT>), __VA_ARGS__); break;                  \
+    case 2: hipLaunchKernelGGL((KERNEL<2, QT>), __VA_ARGS__); break;                  \
+    case 4: hipLaunchKernelGGL((KERNEL<4, QT>), __VA_ARGS__); break;                  \
+    case 8: hipLaunchKernelGGL((KERNEL<8, QT>), __VA_ARGS__); break;                  \
+    case 16: hipLaunchKernelGGL((KERNEL<16, QT>), __VA_ARGS__); break;                \
+    default: hipLaunchKernelGGL((KERNEL<32, QT>), __VA_ARGS__); break;                \
     }
+#define CG_DISPATCH(E, KERNEL, ...)                                                   \
+    do {                                                                              \
+        if (d->f64) CG_DISPATCH_T(E, double, KERNEL, __VA_ARGS__)                     \
+        else CG_DISPATCH_T(E, float, KERNEL, __VA_ARGS__)                             \
+    } while (0)
 template <int T0, int T1, int T2, int T3, int ACT>
 static hipError_t fast_attr(int lds) {
     hipError_t e = hipFuncSetAttribute((const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 0>,
@@ -2657,7 +2675,8 @@ struct trpo_dev {
     fast_launch_fn k_fvp, k_pg; // the tile kernel serving this shape, FVP and policy-gradient modes
     fast_launch_fn k_fvp_yc, k_cg_yc;   // the same kernel on the forward cache: standalone FVP, CG iteration
     fast_launch_fn k_cg_yc_q[4];        // one-wave-per-tile CG iteration by reorthogonalisation slots (kQB)
-    double *qbuf, *qzero;               // reorthogonalisation basis [QCAP][P] and a zero line
+    void *qbuf;                         // reorthogonalisation basis QT [QCAP][P] (QT: fp32, fp64 mode fp64)
+    double *qzero;                      // a zero line
     int reorth;                         // TRPO_CG_REORTH (default 1)
     int k_lds, k_tiles;         // its dynamic LDS bytes and tiles per block per step
     Pack pack;
@@ -3694,7 +3713,7 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
                         d->atomic ? acc_slot(d, M - 1) : d->zacc, d->atomic ? d->Rc : 1, d->pbuf[in], d->rbuf[in],
                         d->pbuf[out], d->rbuf[out], x, d->P, d->nw, d->ctl, d->st + in, d->st + out, d->hist,
                         (const int *)nullptr, (void *)nullptr, 0, 0, d->reorth ? d->qbuf : nullptr,
-                        (const double *)d->qzero, cg_step_nq(d, M - 1), d->atomic ? acc_slot(d, 0) : nullptr,
+                        (const void *)d->qzero, cg_step_nq(d, M - 1), d->atomic ? acc_slot(d, 0) : nullptr,
                         d->atomic ? RP : 0);
         }
     } else if (d->coop_fused) {
@@ -3730,7 +3749,7 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
             CG_DISPATCH(E, cg_update_kernel, dim3(1), dim3(1024), 0, d->stream, d->zacc, 1, d->pbuf[in], d->rbuf[in],
                         d->pbuf[out], d->rbuf[out], x, d->P, d->nw, d->ctl, d->st + in, d->st + out, d->hist,
                         (const int *)nullptr, (void *)nullptr, 0, 0, d->reorth ? d->qbuf : nullptr,
-                        (const double *)d->qzero, cg_step_nq(d, M - 1));
+                        (const void *)d->qzero, cg_step_nq(d, M - 1));
         }
     } else {
         // generic or cooperative kernel: FVP, reduce, [all-reduce], CG step per iteration
@@ -3742,7 +3761,7 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
             CG_DISPATCH(E, cg_update_kernel, dim3(1), dim3(1024), d->coop ? shm : 0, d->stream, d->zacc, 1,
                         d->pbuf[cur], d->rbuf[cur], d->pbuf[nxt], d->rbuf[nxt], x, d->P, d->nw, d->ctl, d->st + cur,
                         d->st + nxt, d->hist, d->vmap, d->vpack, d->coop ? vlen : 0, d->f64,
-                        d->reorth ? d->qbuf : nullptr, (const double *)d->qzero, cg_step_nq(d, j));
+                        d->reorth ? d->qbuf : nullptr, (const void *)d->qzero, cg_step_nq(d, j));
         }
     }
     HCHK(hipGetLastError());
