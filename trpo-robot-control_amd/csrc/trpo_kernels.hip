@@ -290,6 +290,7 @@ __device__ __forceinline__ void qload(double (&dst)[E], const QT *Q, const QT *q
 template <int E, typename QT>
 __device__ void qdots_stage1(const QT *Q, const QT *qz, int P, int nq, const double (&zv)[E], int nthreads,
                              double *shq) {
+#pragma clang fp contract(off)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nwv = blockDim.x >> 6;
     if constexpr (E > 4) {          // many elements per thread: one vector at a time (register budget)
         for (int i = 0; i < nq; ++i) {
@@ -297,7 +298,7 @@ __device__ void qdots_stage1(const QT *Q, const QT *qz, int P, int nq, const dou
             qload(qa, Q, qz, P, i, nq, nthreads);
             double t = 0.0;
 #pragma unroll
-            for (int e = 0; e < E; ++e) t += qa[e] * zv[e];
+            for (int e = 0; e < E; ++e) t = __builtin_fma(qa[e], zv[e], t);
             t = wave_tree_sum(t);
             if (lane == 0) shq[i * nwv + w] = t;
         }
@@ -309,14 +310,14 @@ __device__ void qdots_stage1(const QT *Q, const QT *qz, int P, int nq, const dou
         qload(qb, Q, qz, P, i + 1, nq, nthreads);
         double t = 0.0;
 #pragma unroll
-        for (int e = 0; e < E; ++e) t += qa[e] * zv[e];
+        for (int e = 0; e < E; ++e) t = __builtin_fma(qa[e], zv[e], t);
         t = wave_tree_sum(t);
         if (lane == 0) shq[i * nwv + w] = t;
         qload(qa, Q, qz, P, i + 2, nq, nthreads);
         if (i + 1 < nq) {
             t = 0.0;
 #pragma unroll
-            for (int e = 0; e < E; ++e) t += qb[e] * zv[e];
+            for (int e = 0; e < E; ++e) t = __builtin_fma(qb[e], zv[e], t);
             t = wave_tree_sum(t);
             if (lane == 0) shq[(i + 1) * nwv + w] = t;
         }
@@ -335,6 +336,7 @@ __device__ __forceinline__ double qdot_final(const double *shq, int i) {
 template <int E, typename QT>
 __device__ double qcorrect(const QT *Q, const QT *qz, int P, int nq, int nthreads, const double *shq,
                            double alpha, double (&rv)[E]) {
+#pragma clang fp contract(off)
     if constexpr (E > 4) {          // register budget, as qdots_stage1
         double cs = 0.0;
         for (int i = 0; i < nq; ++i) {
@@ -343,7 +345,7 @@ __device__ double qcorrect(const QT *Q, const QT *qz, int P, int nq, int nthread
             const double c = -alpha * qdot_final(shq, i);
             cs += c * c;
 #pragma unroll
-            for (int e = 0; e < E; ++e) rv[e] -= c * qa[e];
+            for (int e = 0; e < E; ++e) rv[e] = __builtin_fma(-c, qa[e], rv[e]);
         }
         return cs;
     }
@@ -354,13 +356,13 @@ __device__ double qcorrect(const QT *Q, const QT *qz, int P, int nq, int nthread
         double c = -alpha * qdot_final(shq, i);
         cs += c * c;
 #pragma unroll
-        for (int e = 0; e < E; ++e) rv[e] -= c * qa[e];
+        for (int e = 0; e < E; ++e) rv[e] = __builtin_fma(-c, qa[e], rv[e]);
         qload(qa, Q, qz, P, i + 2, nq, nthreads);
         if (i + 1 < nq) {
             c = -alpha * qdot_final(shq, i + 1);
             cs += c * c;
 #pragma unroll
-            for (int e = 0; e < E; ++e) rv[e] -= c * qb[e];
+            for (int e = 0; e < E; ++e) rv[e] = __builtin_fma(-c, qb[e], rv[e]);
         }
     }
     return cs;
@@ -796,25 +798,18 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
     STAMP(0);
 
     // ---- prologue: ONE round of global loads (flags, theta pack, [v pack | CG state], first tile) ----
-    const bool upd = A.update != 0;
-    const bool ini = !upd && A.init != 0;
-    const bool vnat = !upd && !ini && A.v_nat != nullptr;   // plain FVP of a natural-order direction
-    constexpr int NT4 = C::TLEN / 4, NALL = (C::TLEN + C::VLEN) / 4;
+    // MODE 3 is always a CG update (compile time: no run-time mode branches around its loads)
+    constexpr bool CGK = MODE == 3;
+    const bool upd = CGK || (MODE == 0 && A.update != 0);
+    const bool ini = !CGK && MODE == 0 && !upd && A.init != 0;
+    const bool vnat = !CGK && !upd && !ini && A.v_nat != nullptr;   // plain FVP of a natural-order direction
+    constexpr int NT4 = C::TLEN / 4, NALL = CGK ? NT4 : (C::TLEN + C::VLEN) / 4;   // MODE 3: no v pack
     constexpr int PER = (NALL + C::THREADS - 1) / C::THREADS;
     const int skipv = *A.skip;
     // NOTE: every prologue load is unconditional (indices clamped, values selected after):
     // a load guarded by a run-time condition makes hipcc branch around it and drain vmcnt,
     // which serialises the round trips (cdna_hip_programming.md §5 trap (c)).
     f4 st[PER];
-    {
-        const f4 *tp4 = reinterpret_cast<const f4 *>(A.tpack);
-        const f4 *vp4 = reinterpret_cast<const f4 *>(A.vpack);
-#pragma unroll
-        for (int k = 0; k < PER; ++k) {
-            const int e = min(tid + k * C::THREADS, NALL - 1);
-            st[k] = e < NT4 ? tp4[e] : vp4[e - NT4];
-        }
-    }
 #if TRPO_TILE_ILV
     int tile = wave * gridDim.x + blockIdx.x;
 #else
@@ -824,7 +819,17 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
     [[maybe_unused]] f4 yn[YC ? NYC : 1];
     const f4 *yc4 = reinterpret_cast<const f4 *>(A.yc);
     const int a3c = ACT >= 0 ? ((ACT >> 4) & 3) : net.act[3];
-    {
+    // the loads that do not depend on the previous kernel: theta [+ v] pack and the first tile.
+    // MODE 3 issues them after the CG state, so the CG step's operands arrive first (loads return
+    // in issue order) and these land while the step computes.
+    auto load_static = [&]() {
+        const f4 *tp4 = reinterpret_cast<const f4 *>(A.tpack);
+        const f4 *vp4 = reinterpret_cast<const f4 *>(A.vpack);
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int e = min(tid + k * C::THREADS, NALL - 1);
+            st[k] = e < NT4 ? tp4[e] : vp4[e - NT4];
+        }
         const int tl = max(0, min(tile, ntiles - 1));
 #pragma unroll
         for (int kt = 0; kt < T0; ++kt) xn[kt] = obs4[(long)(tl * 16 + c) * (4 * T0) + kt * 4 + g];
@@ -835,7 +840,8 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
 #pragma unroll
                 for (int k = T1 + T2; k < NYC; ++k) yn[k] = yc4[((long)tl * NYC + k) * 64 + lane];
         }
-    }
+    };
+    if constexpr (!CGK) load_static();
     constexpr int Tc[4] = {T0, T1, T2, T3};
     // CG state for the fused update (src/TRPO_CG.c:77-103), loaded in the same round
     double pv[C::EMAX], rv[C::EMAX], zv[C::EMAX], xv[C::EMAX];
@@ -844,6 +850,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
     double cn = 1.0, clam = 0.0, cth = 0.0;
     int cmax = 0;
     if (upd) {
+        #pragma clang fp contract(off)   // explicit rounding: MODE 0 and MODE 3 give the same bits
         sin = *A.st_in;
         cn = A.ctl->n_total;
         clam = A.ctl->damping;
@@ -902,6 +909,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
 #pragma unroll
         for (int i = 0; i < QB; ++i) qload<C::EMAX>(qv[i], qf, qfz, A.P, i, upd ? A.nq : 0, C::THREADS);
     }
+    if constexpr (CGK) load_static();
     // plain FVP: the direction fragments gathered from v in the same load round
     float vg[C::VEMAX];
     if (vnat) {
@@ -913,14 +921,15 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
         }
     }
     if (skipv) return;                                 // grid-uniform
-    {
+    auto stage_static = [&]() {
         f4 *dst = reinterpret_cast<f4 *>(lds);
 #pragma unroll
         for (int k = 0; k < PER; ++k) {
             const int e = tid + k * C::THREADS;
             if (e < NT4 || (e < NALL && !upd && !ini && !vnat)) dst[e] = st[k];
         }
-    }
+    };
+    if constexpr (!CGK) stage_static();               // MODE 3: after the CG step (its loads came last)
     if (vnat) {
 #pragma unroll
         for (int e = 0; e < C::VEMAX; ++e) {
@@ -930,6 +939,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
     }
     STAMP(7);
     if (ini) {
+        #pragma clang fp contract(off)   // explicit rounding: MODE 0 and MODE 3 give the same bits
 #pragma unroll
         for (int e = 0; e < C::EMAX; ++e)
             if (ps[e] >= 0) vw[ps[e]] = (float)pv[e];
@@ -969,6 +979,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
         }
     }
     if (upd) {
+        #pragma clang fp contract(off)   // explicit rounding: MODE 0 and MODE 3 give the same bits
         // every block runs the identical fp64 CG step (fixed-order sums => bitwise-equal
         // results in all blocks); block 0 publishes the new state
         // ONE block reduction per step: p.z, r.z, z.z, x.p, p.p; then |r'|^2 = |r|^2 - 2a r.z + a^2 z.z
@@ -981,14 +992,15 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
 #pragma unroll
         for (int e = 0; e < C::EMAX; ++e) {
             const int q = tid + e * C::THREADS;
-            zv[e] = (q < A.nw ? zv[e] / cn : 2.0 * pv[e]) + clam * pv[e];
-            red[0] += pv[e] * zv[e];
-            red[1] += rv[e] * zv[e];
-            red[2] += zv[e] * zv[e];
-            red[3] += xv[e] * pv[e];
-            red[4] += pv[e] * pv[e];
+            // contraction is off in this block: the fused multiply-adds are spelled out
+            zv[e] = __builtin_fma(clam, pv[e], q < A.nw ? zv[e] / cn : 2.0 * pv[e]);
+            red[0] = __builtin_fma(pv[e], zv[e], red[0]);
+            red[1] = __builtin_fma(rv[e], zv[e], red[1]);
+            red[2] = __builtin_fma(zv[e], zv[e], red[2]);
+            red[3] = __builtin_fma(xv[e], pv[e], red[3]);
+            red[4] = __builtin_fma(pv[e], pv[e], red[4]);
 #pragma unroll
-            for (int i = 0; i < QB; ++i) red[5 + i] += qv[i][e] * zv[e];
+            for (int i = 0; i < QB; ++i) red[5 + i] = __builtin_fma(qv[i][e], zv[e], red[5 + i]);
         }
         if constexpr (QB == 0) {
             if (A.reorth && A.nq > 0) qdots_stage1<C::EMAX>(qf, qfz, A.P, A.nq, zv, C::THREADS, shq);
@@ -1009,9 +1021,9 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
 #pragma unroll
         for (int e = 0; e < C::EMAX; ++e) {
             const double r0 = rv[e];
-            rv[e] -= alpha * zv[e];
-            rv[e] -= cr * r0;
-            xv[e] += alpha * pv[e];
+            rv[e] = __builtin_fma(-alpha, zv[e], rv[e]);
+            rv[e] = __builtin_fma(-cr, r0, rv[e]);
+            xv[e] = __builtin_fma(alpha, pv[e], xv[e]);
         }
         if constexpr (QB > 0) {
 #pragma unroll
@@ -1019,7 +1031,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
                 const double c = -alpha * red[5 + i];       // zero for the slots >= nq
                 cs += c * c;
 #pragma unroll
-                for (int e = 0; e < C::EMAX; ++e) rv[e] -= c * qv[i][e];
+                for (int e = 0; e < C::EMAX; ++e) rv[e] = __builtin_fma(-c, qv[i][e], rv[e]);
             }
         } else {
             if (A.reorth && A.nq > 0) cs += qcorrect<C::EMAX>(qf, qfz, A.P, A.nq, C::THREADS, shq, alpha, rv);
@@ -1031,7 +1043,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
 #pragma unroll
         for (int e = 0; e < C::EMAX; ++e) {
             const int q = tid + e * C::THREADS;
-            pv[e] = rv[e] + beta * pv[e];
+            pv[e] = __builtin_fma(beta, pv[e], rv[e]);
             if (q < A.P && blockIdx.x == 0) {
                 A.p_out[q] = pv[e];
                 A.r_out[q] = rv[e];
@@ -1065,6 +1077,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
         }
         STAMP(12);
     }
+    if constexpr (CGK) stage_static();
     __syncthreads();
     STAMP(1);
     [[maybe_unused]] bool first_tile = true;
