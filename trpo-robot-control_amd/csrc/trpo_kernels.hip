@@ -70,6 +70,7 @@ struct CgSt {                  // ping-ponged CG scalars (state k = before FVP k
 struct IterArgs {
     const float4 *obs4;
     int n, ntiles, P, nw;
+    int Ps;                       // even row stride of the replica sets and the basis (P rounded up)
     const float *tpack;
     const float *vpack;           // plain FVP: the packed direction
     const double *v_nat;          // plain FVP: gather the direction from this natural-order vector instead
@@ -270,15 +271,46 @@ constexpr int QCAP = 16;
 
 // the thread's E elements (q = tid + e * nthreads) of basis vector i, or zeros for i >= nq / q >= P:
 // the load is unconditional (a select on the address: qz is a small zero line every lane may read)
-template <int E, typename QT>
-__device__ __forceinline__ void qload(double (&dst)[E], const QT *Q, const QT *qz, int P, int i, int nq,
+// Element layouts of the P-vectors in the CG steps: thread t holds elements t + e * nthreads, or with
+// PAIR (two elements per thread, P <= 2 * nthreads) the adjacent pair 2t, 2t + 1, loaded by one
+// 16-byte (8-byte for fp32) instruction -- narrow loads issue at about half the byte rate.
+// Replica and basis rows have the even stride Ps, so every pair is aligned.
+template <bool PAIR>
+__device__ __forceinline__ int elem_of(int e, int nthreads) {
+    return PAIR ? 2 * (int)threadIdx.x + e : (int)threadIdx.x + e * nthreads;
+}
+template <typename T> struct V2T;
+template <> struct V2T<float> { typedef float2 type; };
+template <> struct V2T<double> { typedef double2 type; };
+template <> struct V2T<int> { typedef int2 type; };
+// the pair (2t, 2t + 1) of row `row` (stride Ps) of base, clamped to a valid pair (values selected by
+// the caller); one vector load
+template <typename T>
+__device__ __forceinline__ typename V2T<T>::type pair_at(const T *base, long row, int Ps) {
+    const int t = min((int)threadIdx.x, (Ps >> 1) - 1);
+    return reinterpret_cast<const typename V2T<T>::type *>(base + row * Ps)[t];
+}
+
+template <int E, typename QT, bool PAIR = false>
+__device__ __forceinline__ void qload(double (&dst)[E], const QT *Q, const QT *qz, int P, int Ps, int i, int nq,
                                       int nthreads) {
     const int tid = threadIdx.x;
+    if constexpr (PAIR) {
+        static_assert(E == 2, "pair layout");
+        const bool ok = i < nq;
+        typedef typename V2T<QT>::type V2;
+        const V2 *src = ok ? reinterpret_cast<const V2 *>(Q + (long)i * Ps) + min(tid, (Ps >> 1) - 1)
+                           : reinterpret_cast<const V2 *>(qz) + (tid & 7);
+        const V2 v = *src;
+        dst[0] = (ok && 2 * tid < P) ? (double)v.x : 0.0;
+        dst[1] = (ok && 2 * tid + 1 < P) ? (double)v.y : 0.0;
+        return;
+    }
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const int q = tid + e * nthreads;
         const bool ok = i < nq && q < P;
-        const QT *src = ok ? Q + (long)i * P + q : qz + (tid & 7);
+        const QT *src = ok ? Q + (long)i * Ps + q : qz + (tid & 7);
         const double v = (double)*src;
         dst[e] = ok ? v : 0.0;
     }
@@ -287,15 +319,15 @@ __device__ __forceinline__ void qload(double (&dst)[E], const QT *Q, const QT *q
 // stage 1 of the dots e_i = q_i . z, i < nq (runtime): per wave the total by block_sums_dpp's tree,
 // written to shq[i * W + w]; a later barrier (the caller's block reduction) makes them visible.
 // Loads of the next vector are issued before the current one is reduced.
-template <int E, typename QT>
-__device__ void qdots_stage1(const QT *Q, const QT *qz, int P, int nq, const double (&zv)[E], int nthreads,
+template <int E, typename QT, bool PAIR = false>
+__device__ void qdots_stage1(const QT *Q, const QT *qz, int P, int Ps, int nq, const double (&zv)[E], int nthreads,
                              double *shq) {
 #pragma clang fp contract(off)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nwv = blockDim.x >> 6;
     if constexpr (E > 4) {          // many elements per thread: one vector at a time (register budget)
         for (int i = 0; i < nq; ++i) {
             double qa[E];
-            qload(qa, Q, qz, P, i, nq, nthreads);
+            qload<E, QT, PAIR>(qa, Q, qz, P, Ps, i, nq, nthreads);
             double t = 0.0;
 #pragma unroll
             for (int e = 0; e < E; ++e) t = __builtin_fma(qa[e], zv[e], t);
@@ -305,15 +337,15 @@ __device__ void qdots_stage1(const QT *Q, const QT *qz, int P, int nq, const dou
         return;
     }
     double qa[E], qb[E];
-    qload(qa, Q, qz, P, 0, nq, nthreads);
+    qload<E, QT, PAIR>(qa, Q, qz, P, Ps, 0, nq, nthreads);
     for (int i = 0; i < nq; i += 2) {
-        qload(qb, Q, qz, P, i + 1, nq, nthreads);
+        qload<E, QT, PAIR>(qb, Q, qz, P, Ps, i + 1, nq, nthreads);
         double t = 0.0;
 #pragma unroll
         for (int e = 0; e < E; ++e) t = __builtin_fma(qa[e], zv[e], t);
         t = wave_tree_sum(t);
         if (lane == 0) shq[i * nwv + w] = t;
-        qload(qa, Q, qz, P, i + 2, nq, nthreads);
+        qload<E, QT, PAIR>(qa, Q, qz, P, Ps, i + 2, nq, nthreads);
         if (i + 1 < nq) {
             t = 0.0;
 #pragma unroll
@@ -333,15 +365,15 @@ __device__ __forceinline__ double qdot_final(const double *shq, int i) {
 }
 
 // stage 3: rv -= sum_i c_i q_i with c_i = -alpha e_i (i < nq); returns sum_i c_i^2
-template <int E, typename QT>
-__device__ double qcorrect(const QT *Q, const QT *qz, int P, int nq, int nthreads, const double *shq,
+template <int E, typename QT, bool PAIR = false>
+__device__ double qcorrect(const QT *Q, const QT *qz, int P, int Ps, int nq, int nthreads, const double *shq,
                            double alpha, double (&rv)[E]) {
 #pragma clang fp contract(off)
     if constexpr (E > 4) {          // register budget, as qdots_stage1
         double cs = 0.0;
         for (int i = 0; i < nq; ++i) {
             double qa[E];
-            qload(qa, Q, qz, P, i, nq, nthreads);
+            qload<E, QT, PAIR>(qa, Q, qz, P, Ps, i, nq, nthreads);
             const double c = -alpha * qdot_final(shq, i);
             cs += c * c;
 #pragma unroll
@@ -350,14 +382,14 @@ __device__ double qcorrect(const QT *Q, const QT *qz, int P, int nq, int nthread
         return cs;
     }
     double qa[E], qb[E], cs = 0.0;
-    qload(qa, Q, qz, P, 0, nq, nthreads);
+    qload<E, QT, PAIR>(qa, Q, qz, P, Ps, 0, nq, nthreads);
     for (int i = 0; i < nq; i += 2) {
-        qload(qb, Q, qz, P, i + 1, nq, nthreads);
+        qload<E, QT, PAIR>(qb, Q, qz, P, Ps, i + 1, nq, nthreads);
         double c = -alpha * qdot_final(shq, i);
         cs += c * c;
 #pragma unroll
         for (int e = 0; e < E; ++e) rv[e] = __builtin_fma(-c, qa[e], rv[e]);
-        qload(qa, Q, qz, P, i + 2, nq, nthreads);
+        qload<E, QT, PAIR>(qa, Q, qz, P, Ps, i + 2, nq, nthreads);
         if (i + 1 < nq) {
             c = -alpha * qdot_final(shq, i + 1);
             cs += c * c;
@@ -369,14 +401,15 @@ __device__ double qcorrect(const QT *Q, const QT *qz, int P, int nq, int nthread
 }
 
 // block 0 stores the new basis vector q_it = r'' / |r''| (it < QCAP)
-template <int E, typename QT>
-__device__ __forceinline__ void qstore(QT *Q, int P, int it, double nr, const double (&rv)[E], int nthreads) {
+template <int E, typename QT, bool PAIR = false>
+__device__ __forceinline__ void qstore(QT *Q, int P, int Ps, int it, double nr, const double (&rv)[E],
+                                       int nthreads) {
     if (!Q || it >= QCAP) return;
     const double inv = nr > 0.0 ? 1.0 / sqrt(nr) : 0.0;
 #pragma unroll
     for (int e = 0; e < E; ++e) {
-        const int q = threadIdx.x + e * nthreads;
-        if (q < P) Q[(long)it * P + q] = (QT)(rv[e] * inv);
+        const int q = elem_of<PAIR>(e, nthreads);
+        if (q < P) Q[(long)it * Ps + q] = (QT)(rv[e] * inv);
     }
 }
 
@@ -843,6 +876,9 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
     };
     if constexpr (!CGK) load_static();
     constexpr int Tc[4] = {T0, T1, T2, T3};
+    // CG-step element layout: adjacent pairs (one 16-byte load per vector per thread) where two
+    // elements per thread cover P, else the strided layout (elem_of)
+    constexpr bool PAIR = C::EMAX == 2;
     // CG state for the fused update (src/TRPO_CG.c:77-103), loaded in the same round
     double pv[C::EMAX], rv[C::EMAX], zv[C::EMAX], xv[C::EMAX];
     int vm[C::VEMAX], ps[C::EMAX];
@@ -857,6 +893,29 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
         cth = A.ctl->resth;
         cmax = A.ctl->maxiter;
         const double *xs = blockIdx.x == 0 ? A.x : A.p_in;    // only block 0 needs x
+        if constexpr (PAIR) {
+            // replicas summed in replica order as below; rows of stride Ps, pairs 16-byte aligned
+            const double2 p2 = pair_at(A.p_in, 0, A.Ps), r2 = pair_at(A.r_in, 0, A.Ps), x2 = pair_at(xs, 0, A.Ps);
+            double2 za[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) za[k] = pair_at(A.acc_in, min(k, A.R_in - 1), A.Ps);
+            const int2 m2 = pair_at(A.pslot, 0, A.Ps);
+            const double p0[2] = {p2.x, p2.y}, r0[2] = {r2.x, r2.y}, x0[2] = {x2.x, x2.y};
+            const int mm[2] = {m2.x, m2.y};
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int q = 2 * tid + e;
+                const bool in = q < A.P;
+                double z = e ? za[0].y : za[0].x;
+#pragma unroll
+                for (int k = 1; k < 8; ++k) z += k < A.R_in ? (e ? za[k].y : za[k].x) : 0.0;
+                pv[e] = in ? p0[e] : 0.0;
+                rv[e] = in ? r0[e] : 0.0;
+                xv[e] = (in && blockIdx.x == 0) ? x0[e] : 0.0;
+                zv[e] = q < A.nw ? z : 0.0;
+                ps[e] = in ? mm[e] : -1;
+            }
+        } else {
 #pragma unroll
         for (int e = 0; e < C::EMAX; ++e) {
             const int q = tid + e * C::THREADS, qc = min(q, A.P - 1), qz = min(q, A.nw - 1);
@@ -867,7 +926,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
                 // up to 8 atomic replicas (small P only: 8 loads per element in flight)
                 double za[8];
 #pragma unroll
-                for (int k = 0; k < 8; ++k) za[k] = A.acc_in[(long)min(k, A.R_in - 1) * A.P + qz];
+                for (int k = 0; k < 8; ++k) za[k] = A.acc_in[(long)min(k, A.R_in - 1) * A.Ps + qz];
                 z = za[0];                                // R_in >= 1: no select on the first term
 #ifndef TRPO_ABL_R1
 #pragma unroll
@@ -882,12 +941,13 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
             zv[e] = q < A.nw ? z : 0.0;
         }
 #pragma unroll
-        for (int e = 0; e < C::VEMAX; ++e) vm[e] = vmap_at(net, Tc, tid + e * C::THREADS);
-#pragma unroll
         for (int e = 0; e < C::EMAX; ++e) {
             const int q = tid + e * C::THREADS, m = A.pslot[min(q, A.P - 1)];
             ps[e] = q < A.P ? m : -1;
         }
+        }
+#pragma unroll
+        for (int e = 0; e < C::VEMAX; ++e) vm[e] = vmap_at(net, Tc, tid + e * C::THREADS);
     } else if (ini) {
 #pragma unroll
         for (int e = 0; e < C::EMAX; ++e) {
@@ -907,7 +967,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
     [[maybe_unused]] double qv[QB > 0 ? QB : 1][C::EMAX];
     if constexpr (QB > 0) {
 #pragma unroll
-        for (int i = 0; i < QB; ++i) qload<C::EMAX>(qv[i], qf, qfz, A.P, i, upd ? A.nq : 0, C::THREADS);
+        for (int i = 0; i < QB; ++i) qload<C::EMAX, float, PAIR>(qv[i], qf, qfz, A.P, A.Ps, i, upd ? A.nq : 0, C::THREADS);
     }
     if constexpr (CGK) load_static();
     // plain FVP: the direction fragments gathered from v in the same load round
@@ -963,7 +1023,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
                     A.x[q] = 0.0;
                 }
             }
-            if (A.reorth) qstore<C::EMAX>(qf, A.P, 0, rr, pv, C::THREADS);     // q_0 = b / |b|
+            if (A.reorth) qstore<C::EMAX>(qf, A.P, A.Ps, 0, rr, pv, C::THREADS);     // q_0 = b / |b|
             if (tid == 0) {
                 A.st_out->rdotr = rr;
                 A.st_out->xx = 0.0;
@@ -991,7 +1051,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
         for (int k = 0; k < 5 + QB; ++k) red[k] = 0.0;
 #pragma unroll
         for (int e = 0; e < C::EMAX; ++e) {
-            const int q = tid + e * C::THREADS;
+            const int q = elem_of<PAIR>(e, C::THREADS);
             // contraction is off in this block: the fused multiply-adds are spelled out
             zv[e] = __builtin_fma(clam, pv[e], q < A.nw ? zv[e] / cn : 2.0 * pv[e]);
             red[0] = __builtin_fma(pv[e], zv[e], red[0]);
@@ -1003,7 +1063,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
             for (int i = 0; i < QB; ++i) red[5 + i] = __builtin_fma(qv[i][e], zv[e], red[5 + i]);
         }
         if constexpr (QB == 0) {
-            if (A.reorth && A.nq > 0) qdots_stage1<C::EMAX>(qf, qfz, A.P, A.nq, zv, C::THREADS, shq);
+            if (A.reorth && A.nq > 0) qdots_stage1<C::EMAX, float, PAIR>(qf, qfz, A.P, A.Ps, A.nq, zv, C::THREADS, shq);
         }
         STAMP(8);
 #ifndef TRPO_ABL_NORED
@@ -1034,7 +1094,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
                 for (int e = 0; e < C::EMAX; ++e) rv[e] = __builtin_fma(-c, qv[i][e], rv[e]);
             }
         } else {
-            if (A.reorth && A.nq > 0) cs += qcorrect<C::EMAX>(qf, qfz, A.P, A.nq, C::THREADS, shq, alpha, rv);
+            if (A.reorth && A.nq > 0) cs += qcorrect<C::EMAX, float, PAIR>(qf, qfz, A.P, A.Ps, A.nq, C::THREADS, shq, alpha, rv);
         }
         const double nr = sin.rdotr - 2.0 * alpha * red[1] + alpha * alpha * red[2] - cs;
         const double xn2 = sin.xx + 2.0 * alpha * red[3] + alpha * alpha * red[4];
@@ -1042,7 +1102,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
         const double beta = nr / sin.rdotr;
 #pragma unroll
         for (int e = 0; e < C::EMAX; ++e) {
-            const int q = tid + e * C::THREADS;
+            const int q = elem_of<PAIR>(e, C::THREADS);
             pv[e] = __builtin_fma(beta, pv[e], rv[e]);
             if (q < A.P && blockIdx.x == 0) {
                 A.p_out[q] = pv[e];
@@ -1052,7 +1112,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
         }
         const int it = sin.iter + 1;
         const int done = (nr < cth || it >= cmax) ? 1 : 0;
-        if (blockIdx.x == 0 && A.reorth) qstore<C::EMAX>(qf, A.P, it, nr, rv, C::THREADS);
+        if (blockIdx.x == 0 && A.reorth) qstore<C::EMAX, float, PAIR>(qf, A.P, A.Ps, it, nr, rv, C::THREADS);
         if (blockIdx.x == 0 && tid == 0) {
             A.st_out->rdotr = nr;
             A.st_out->xx = xn2;
@@ -1482,7 +1542,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
             for (int k = 0; k < C::NACC / 4; ++k) red[wave * (C::SLAB / 4) + k * 64 + lane] = acc[k];
             __syncthreads();
             STAMP(5);
-            double *dst = A.acc_out + (long)(blockIdx.x % A.R_out) * A.P;
+            double *dst = A.acc_out + (long)(blockIdx.x % A.R_out) * A.Ps;
 #pragma unroll
             for (int e = 0; e < C::EMAX; ++e) {
                 const int q = tid + e * C::THREADS;
@@ -1525,7 +1585,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
     if (A.acc_out) {
         // cross-block sum by fp64 atomics into R replicas: the fp32 block partials are added
         // exactly unless their exponents span > 29 bits, so the order cannot matter in practice
-        double *dst = A.acc_out + (long)(blockIdx.x % A.R_out) * A.P;
+        double *dst = A.acc_out + (long)(blockIdx.x % A.R_out) * A.Ps;
 #pragma unroll
         for (int j = 0; j < C::EPT; ++j)
 #pragma unroll
@@ -1804,7 +1864,7 @@ fvp_coop_kernel(IterArgs A, Net net) {
             s1[1] += rv[e] * zv[e];
         }
         const bool ro = A.reorth && sin.rdotr > 0.0;
-        if (ro && A.nq > 0) qdots_stage1<EP>((const T *)A.q, (const T *)A.qz, A.P, A.nq, zv, Q::THREADS, shq);
+        if (ro && A.nq > 0) qdots_stage1<EP>((const T *)A.q, (const T *)A.qz, A.P, A.Ps, A.nq, zv, Q::THREADS, shq);
         block_sums_dpp<2, Q::THREADS / 64>(s1, shc);
         const double alpha = sin.rdotr / s1[0];
         // residual reorthogonalisation (see QCAP): along r itself, then along the stored basis
@@ -1816,7 +1876,7 @@ fvp_coop_kernel(IterArgs A, Net net) {
             rv[e] -= alpha * zv[e];
             rv[e] -= cr * r0;
         }
-        if (ro && A.nq > 0) qcorrect<EP>((const T *)A.q, (const T *)A.qz, A.P, A.nq, Q::THREADS, shq, alpha, rv);
+        if (ro && A.nq > 0) qcorrect<EP>((const T *)A.q, (const T *)A.qz, A.P, A.Ps, A.nq, Q::THREADS, shq, alpha, rv);
         double s2[2] = {0.0, 0.0};
 #pragma unroll
         for (int e = 0; e < EP; ++e) {
@@ -1840,7 +1900,7 @@ fvp_coop_kernel(IterArgs A, Net net) {
         }
         const int it = sin.iter + 1;
         const int done = (nr < cth || it >= cmax) ? 1 : 0;
-        if (b0 && A.reorth) qstore<EP>((T *)A.q, A.P, it, nr, rv, Q::THREADS);
+        if (b0 && A.reorth) qstore<EP>((T *)A.q, A.P, A.Ps, it, nr, rv, Q::THREADS);
         if (b0 && tid == 0) {
             A.st_out->rdotr = nr;
             A.st_out->xx = s2[1];
@@ -2124,7 +2184,7 @@ fvp_coop_kernel(IterArgs A, Net net) {
 #pragma unroll
             for (int k = 0; k < Q::NW; ++k) acc[k] += LV[(((q - 1) * TH + w) * Q::NW + k) * 64 + lane];
         if (A.acc_out) {
-            double *dst = A.acc_out + (long)(blockIdx.x % A.R_out) * A.P;
+            double *dst = A.acc_out + (long)(blockIdx.x % A.R_out) * A.Ps;
 #pragma unroll
             for (int k = 0; k < Q::NW; ++k)
 #pragma unroll
@@ -2292,13 +2352,13 @@ __global__ void fvp_epilogue_kernel(const double *__restrict__ zacc, const doubl
 // zh (optional): a second copy of z into pinned, device-mapped host memory (the host-level FVP call
 // then needs no separate download copy)
 __global__ void acc_epilogue_kernel(double *__restrict__ acc, int R, const double *__restrict__ v,
-                                    double *__restrict__ z, int P, int nw, const Ctl *__restrict__ ctl,
+                                    double *__restrict__ z, int P, int Ps, int nw, const Ctl *__restrict__ ctl,
                                     double *__restrict__ zh) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= P) return;
     double a[8];
 #pragma unroll
-    for (int r = 0; r < 8; ++r) a[r] = acc[(long)min(r, R - 1) * P + min(q, nw - 1)];
+    for (int r = 0; r < 8; ++r) a[r] = acc[(long)min(r, R - 1) * Ps + min(q, nw - 1)];
     double s = a[0];
 #pragma unroll
     for (int r = 1; r < 8; ++r) s += r < R ? a[r] : 0.0;
@@ -2307,7 +2367,7 @@ __global__ void acc_epilogue_kernel(double *__restrict__ acc, int R, const doubl
     z[q] = zq;
     if (zh) zh[q] = zq;
     if (q < nw)
-        for (int r = 0; r < R; ++r) acc[(long)r * P + q] = 0.0;
+        for (int r = 0; r < R; ++r) acc[(long)r * Ps + q] = 0.0;
 }
 
 // ---------------------------------------------------------------------------
@@ -2344,7 +2404,7 @@ template <int E, typename QT>
 __global__ void __launch_bounds__(1024)
 cg_init_kernel(const double *__restrict__ b, double *x, double *r, double *p, int P, Ctl *ctl, CgSt *st,
                double *hist, int maxiter, double resth, const int *__restrict__ vmap, void *vpack,
-               int vlen, int f64, double *acc_zero, int zero_len, void *qbuf_v) {
+               int vlen, int f64, double *acc_zero, int zero_len, void *qbuf_v, int Ps) {
     QT *qbuf = reinterpret_cast<QT *>(qbuf_v);
     __shared__ double sh[16];
     extern __shared__ double sp[];
@@ -2371,7 +2431,7 @@ cg_init_kernel(const double *__restrict__ b, double *x, double *r, double *p, in
         }
     }
     const double rr = block_sum(s, sh);
-    qstore<E>(qbuf, P, 0, rr, bv, 1024);              // q_0 = b / |b| (reorthogonalisation basis; NULL: off)
+    qstore<E>(qbuf, P, Ps, 0, rr, bv, 1024);              // q_0 = b / |b| (reorthogonalisation basis; NULL: off)
     if (threadIdx.x == 0) {
         ctl->maxiter = maxiter;
         ctl->resth = resth;
@@ -2396,7 +2456,7 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
                  const double *__restrict__ r_in, double *p_out, double *r_out, double *x, int P, int nw, Ctl *ctl,
                  const CgSt *st_in, CgSt *st_out, double *hist,
                  const int *__restrict__ vmap, void *vpack, int vlen, int f64,
-                 void *qbuf_v, const void *qz_v, int nq,
+                 void *qbuf_v, const void *qz_v, int nq, int Ps,
                  double *acc_zero = nullptr, int zero_len = 0) {
     // acc_zero: the atomic target of the NEXT solve's first FVP (which also runs the CG start),
     // zeroed here once this step has consumed its input
@@ -2424,7 +2484,7 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
         const double p0 = p_in[qc], x0 = x[qc], r0 = r_in[qc];
         double za[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) za[k] = acc[(long)min(k, R_in - 1) * P + qw];
+        for (int k = 0; k < 8; ++k) za[k] = acc[(long)min(k, R_in - 1) * Ps + qw];
         double z = za[0];                              // the summation order of the guarded form
 #pragma unroll
         for (int k = 1; k < 8; ++k) z += k < R_in ? za[k] : 0.0;
@@ -2436,7 +2496,7 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
     [[maybe_unused]] double qv[QREG ? QCAP : 1][E];
     if constexpr (QREG) {
 #pragma unroll
-        for (int i = 0; i < QCAP; ++i) qload<E>(qv[i], qbuf, qz, P, i, qbuf ? nq : 0, 1024);
+        for (int i = 0; i < QCAP; ++i) qload<E>(qv[i], qbuf, qz, P, Ps, i, qbuf ? nq : 0, 1024);
     }
     if (done) {
         for (int e = threadIdx.x; e < zero_len; e += 1024) acc_zero[e] = 0.0;   // inputs unused
@@ -2458,7 +2518,7 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
     }
     const bool ro = qbuf != nullptr && sin.rdotr > 0.0;     // residual reorthogonalisation (QCAP)
     if constexpr (!QREG) {
-        if (ro && nq > 0) qdots_stage1<E>(qbuf, qz, P, nq, zv, 1024, shq);
+        if (ro && nq > 0) qdots_stage1<E>(qbuf, qz, P, Ps, nq, zv, 1024, shq);
     }
     block_sums_dpp<NS1, 16>(s1, sh);
     const double alpha = sin.rdotr / s1[0];
@@ -2480,7 +2540,7 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
             }
         }
     } else {
-        if (ro && nq > 0) qcorrect<E>(qbuf, qz, P, nq, 1024, shq, alpha, rv);
+        if (ro && nq > 0) qcorrect<E>(qbuf, qz, P, Ps, nq, 1024, shq, alpha, rv);
     }
     double rr = 0.0, xx = 0.0;
 #pragma unroll
@@ -2508,7 +2568,7 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
         __syncthreads();
         write_vpack(sp, vm, vpack, vlen, f64);
     }
-    qstore<E>(qbuf, P, sin.iter + 1, nr, rv, 1024);
+    qstore<E>(qbuf, P, Ps, sin.iter + 1, nr, rv, 1024);
     if (threadIdx.x == 0) {
         const int it = sin.iter + 1;
         st_out->rdotr = nr;
@@ -2680,6 +2740,7 @@ struct trpo_dev {
     hipStream_t stream;
     Net net;
     int P, nw;
+    int Ps;                     // even row stride of replica sets and the basis: P rounded up to even
     // fast path
     const FastEntry *fast;
     const CoopEntry *coop_e;    // cooperative kernel for wide hidden layers (else NULL)
@@ -2910,6 +2971,7 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
     n.A = n.L[nl - 1];
     n.P = pos + n.A;
     d->P = n.P;
+    d->Ps = (n.P + 1) & ~1;
     d->nw = n.P - n.A;
     if (d->P > 32 * 1024) FAIL("NumParams=%d exceeds the 32768 supported by the device CG", d->P);
 
@@ -2953,14 +3015,14 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
     } while (0)
     DMALLOC(d->theta64, sizeof(double) * d->P);
     DMALLOC(d->std64, sizeof(double) * n.A);
-    for (int i = 0; i < 5; ++i) DMALLOC(d->vec[i], sizeof(double) * d->P);
-    DMALLOC(d->r, sizeof(double) * d->P);
-    DMALLOC(d->zacc, sizeof(double) * d->P);
+    for (int i = 0; i < 5; ++i) DMALLOC(d->vec[i], sizeof(double) * d->Ps);
+    DMALLOC(d->r, sizeof(double) * d->Ps);
+    DMALLOC(d->zacc, sizeof(double) * d->Ps);
     DMALLOC(d->ctl, sizeof(Ctl));
     DMALLOC(d->st, 2 * sizeof(CgSt));
     for (int i = 0; i < 2; ++i) {
-        DMALLOC(d->pbuf[i], sizeof(double) * d->P);
-        DMALLOC(d->rbuf[i], sizeof(double) * d->P);
+        DMALLOC(d->pbuf[i], sizeof(double) * d->Ps);
+        DMALLOC(d->rbuf[i], sizeof(double) * d->Ps);
     }
     {
         const char *er = getenv("TRPO_REPLICAS");
@@ -2968,14 +3030,14 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
         if (d->R < 1) d->R = 1;
         if (d->R > 8) d->R = 8;
     }
-    DMALLOC(d->accbuf, sizeof(double) * 3 * d->R * d->P);
-    DMALLOC(d->qbuf, sizeof(double) * QCAP * d->P);
+    DMALLOC(d->accbuf, sizeof(double) * 3 * d->R * d->Ps);
+    DMALLOC(d->qbuf, sizeof(double) * QCAP * d->Ps);
     DMALLOC(d->qzero, sizeof(double) * 64);
     {
         const char *eo = getenv("TRPO_CG_REORTH");
         d->reorth = !(eo && atoi(eo) == 0);
     }
-    DMALLOC(d->pacc, sizeof(double) * 2 * d->R * d->P);
+    DMALLOC(d->pacc, sizeof(double) * 2 * d->R * d->Ps);
     d->Rc = d->R;
     if (d->fast) {
         Pack &pk = d->pack;
@@ -3006,7 +3068,7 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
         DMALLOC(d->vpack, d->esz * pk.vlen);
         DMALLOC(d->tmap, sizeof(int) * pk.tlen);
         DMALLOC(d->vmap, sizeof(int) * pk.vlen);
-        DMALLOC(d->pslot, sizeof(int) * d->P);
+        DMALLOC(d->pslot, sizeof(int) * d->Ps);
         hipLaunchKernelGGL(build_pslot_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, n, pk, d->pslot, d->P);
         const int len = pk.tlen > pk.vlen ? pk.tlen : pk.vlen;
         hipLaunchKernelGGL(build_maps_kernel, dim3(cdiv(len, 256)), dim3(256), 0, d->stream, n, pk, d->tmap, d->vmap,
@@ -3281,8 +3343,8 @@ static int choose_replicas(trpo_dev *d) {
     if (rc > d->R) rc = d->R;
     if (rc != d->Rc) {
         // a different prefix of each replica set is used from now on: start from all-zero sets
-        HCHK(hipMemsetAsync(d->accbuf, 0, sizeof(double) * 3 * d->R * d->P, d->stream));
-        HCHK(hipMemsetAsync(d->pacc, 0, sizeof(double) * 2 * d->R * d->P, d->stream));
+        HCHK(hipMemsetAsync(d->accbuf, 0, sizeof(double) * 3 * d->R * d->Ps, d->stream));
+        HCHK(hipMemsetAsync(d->pacc, 0, sizeof(double) * 2 * d->R * d->Ps, d->stream));
         HCHK(hipStreamSynchronize(d->stream));
         d->Rc = rc;
         if (d->cg_exec) {
@@ -3461,6 +3523,7 @@ static IterArgs plain_args(trpo_dev *d, const int *skip) {
     a.n = (int)d->n;
     a.ntiles = cdiv((long)d->n, 16);
     a.P = d->P;
+    a.Ps = d->Ps;
     a.nw = d->nw;
     a.tpack = (const float *)d->tpack;      // fp64 mode: the kernel reinterprets (element type T)
     a.vpack = (const float *)d->vpack;
@@ -3498,7 +3561,7 @@ static double *launch_fvp_plain(trpo_dev *d, IterArgs &a, bool sink = false) {
     if (d->atomic) {
         // fp64 atomics into R replicas, like the CG kernels (no slab round trip through HBM); the
         // set is zero on entry because its consumer, acc_epilogue_kernel, leaves it zeroed
-        acc = d->pacc + (sink ? (long)d->R * d->P : 0);
+        acc = d->pacc + (sink ? (long)d->R * d->Ps : 0);
         a.acc_out = acc;
         a.R_out = d->Rc;
     }
@@ -3548,9 +3611,9 @@ static int fvp_src(trpo_dev *d, const double *src, double **zh) {
         a.v_nat = src;
         double *acc = launch_fvp_plain(d, a);
         if (acc) {
-            if (allreduce(d, acc, (size_t)d->Rc * d->P)) return -4;
+            if (allreduce(d, acc, (size_t)d->Rc * d->Ps)) return -4;
             hipLaunchKernelGGL(acc_epilogue_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, acc, d->Rc,
-                               src, d->vec[TRPO_VEC_Z], d->P, d->nw, d->ctl, zhost);
+                               src, d->vec[TRPO_VEC_Z], d->P, d->Ps, d->nw, d->ctl, zhost);
             *zh = zhost;
         } else {
             launch_reduce(d, &d->ctl->zero, src, d->vec[TRPO_VEC_Z]);
@@ -3621,7 +3684,7 @@ static int ensure_hist(trpo_dev *d, size_t maxiter) {
     return 0;
 }
 
-static double *acc_slot(trpo_dev *d, long j) { return d->accbuf + (j % 3) * (long)d->R * d->P; }
+static double *acc_slot(trpo_dev *d, long j) { return d->accbuf + (j % 3) * (long)d->R * d->Ps; }
 
 // the one place every collective of the library goes through: RCCL, the in-process host group, or
 // nothing (one rank)
@@ -3659,7 +3722,7 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
     const size_t shm = d->fast ? sizeof(double) * d->P : 0;
     const int *done = &d->ctl->done;
     const long M = (long)maxiter;
-    const int RP = d->Rc * d->P;
+    const int RP = d->Rc * d->Ps;
     // the one-wave-per-tile kernel runs the CG start inside K_0 (IterArgs::init): no init launch.
     // Its atomic target acc_slot(0) is zero on entry: zeroed at allocation and by every solve's
     // final cg_update
@@ -3667,7 +3730,7 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
     if (!fused_init)
         CG_DISPATCH(E, cg_init_kernel, dim3(1), dim3(1024), shm, d->stream, b, x, d->rbuf[0], d->pbuf[0], d->P,
                     d->ctl, d->st, d->hist, (int)maxiter, resth, d->vmap, d->vpack, vlen, d->f64,
-                    d->atomic ? acc_slot(d, 0) : nullptr, d->atomic ? RP : 0, d->reorth ? d->qbuf : nullptr);
+                    d->atomic ? acc_slot(d, 0) : nullptr, d->atomic ? RP : 0, d->reorth ? d->qbuf : nullptr, d->Ps);
     if (d->fast && !d->coop) {
         for (long j = 0; j < M; ++j) {
             IterArgs a = plain_args(d, j == 0 ? &d->ctl->zero : done);
@@ -3726,7 +3789,7 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
                         d->atomic ? acc_slot(d, M - 1) : d->zacc, d->atomic ? d->Rc : 1, d->pbuf[in], d->rbuf[in],
                         d->pbuf[out], d->rbuf[out], x, d->P, d->nw, d->ctl, d->st + in, d->st + out, d->hist,
                         (const int *)nullptr, (void *)nullptr, 0, 0, d->reorth ? d->qbuf : nullptr,
-                        (const void *)d->qzero, cg_step_nq(d, M - 1), d->atomic ? acc_slot(d, 0) : nullptr,
+                        (const void *)d->qzero, cg_step_nq(d, M - 1), d->Ps, d->atomic ? acc_slot(d, 0) : nullptr,
                         d->atomic ? RP : 0);
         }
     } else if (d->coop_fused) {
@@ -3762,7 +3825,7 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
             CG_DISPATCH(E, cg_update_kernel, dim3(1), dim3(1024), 0, d->stream, d->zacc, 1, d->pbuf[in], d->rbuf[in],
                         d->pbuf[out], d->rbuf[out], x, d->P, d->nw, d->ctl, d->st + in, d->st + out, d->hist,
                         (const int *)nullptr, (void *)nullptr, 0, 0, d->reorth ? d->qbuf : nullptr,
-                        (const void *)d->qzero, cg_step_nq(d, M - 1));
+                        (const void *)d->qzero, cg_step_nq(d, M - 1), d->Ps);
         }
     } else {
         // generic or cooperative kernel: FVP, reduce, [all-reduce], CG step per iteration
@@ -3774,7 +3837,7 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
             CG_DISPATCH(E, cg_update_kernel, dim3(1), dim3(1024), d->coop ? shm : 0, d->stream, d->zacc, 1,
                         d->pbuf[cur], d->rbuf[cur], d->pbuf[nxt], d->rbuf[nxt], x, d->P, d->nw, d->ctl, d->st + cur,
                         d->st + nxt, d->hist, d->vmap, d->vpack, d->coop ? vlen : 0, d->f64,
-                        d->reorth ? d->qbuf : nullptr, (const void *)d->qzero, cg_step_nq(d, j));
+                        d->reorth ? d->qbuf : nullptr, (const void *)d->qzero, cg_step_nq(d, j), d->Ps);
         }
     }
     HCHK(hipGetLastError());
@@ -3921,7 +3984,7 @@ static int cg_iter_kernel_only(trpo_dev *d, long j, bool init) {
     if (d->atomic) {
         a.acc_in = acc_slot(d, 0);
         a.R_in = d->Rc;
-        a.acc_out = d->pacc + (long)d->R * d->P;      // the sink set: accumulates, never consumed
+        a.acc_out = d->pacc + (long)d->R * d->Ps;     // the sink set: accumulates, never consumed
         a.R_out = d->Rc;
     } else {
         a.acc_in = d->zacc;
