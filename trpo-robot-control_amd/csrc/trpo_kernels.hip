@@ -703,6 +703,10 @@ __device__ unsigned long long g_stamps[1024 * 32];
 #define TRPO_PF_PIN 1       // pin the next-tile observation prefetch to the top of the tile loop
 #endif
 constexpr int SCR_LD = 20;            // scratch row stride (floats): conflict-free b32 writes
+#ifndef TRPO_SCR_LD3
+#define TRPO_SCR_LD3 20
+#endif
+constexpr int SCR_LD3 = TRPO_SCR_LD3;  // fvp_mlp3_kernel's transpose scratch
 
 template <int T0, int T1, int T2, int T3>
 struct FastCfg {
@@ -728,7 +732,7 @@ struct FastCfg {
     // per-wave transpose scratch: max rows over the three contractions
     static constexpr int R0 = 16 * (T0 + T1), R1 = 16 * (T1 + T2), R2 = 16 * (T2 + T3);
     static constexpr int ROWS = R0 > R1 ? (R0 > R2 ? R0 : R2) : (R1 > R2 ? R1 : R2);
-    static constexpr int SCR = ROWS * SCR_LD;
+    static constexpr int SCR = ROWS * SCR_LD3;
     // accumulator registers per lane; the block's partial sums are written in this
     // "accumulator order" (f4 k, lane, r) -- SLAB floats per block, mapped back to
     // natural parameter order by the reduce kernel (imap)
@@ -784,10 +788,10 @@ __device__ __forceinline__ float rowsum16(float v) {
 
 __device__ __forceinline__ void scr_put(float *scr, int row0, f4 t, int c, int g) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) scr[(row0 + 4 * g + r) * SCR_LD + c] = t[r];
+    for (int r = 0; r < 4; ++r) scr[(row0 + 4 * g + r) * SCR_LD3 + c] = t[r];
 }
 __device__ __forceinline__ f4 scr_get(const float *scr, int row0, int c, int g) {
-    return *reinterpret_cast<const f4 *>(scr + (row0 + c) * SCR_LD + 4 * g);
+    return *reinterpret_cast<const f4 *>(scr + (row0 + c) * SCR_LD3 + 4 * g);
 }
 
 // ACT >= 0: activations of layers 1..3 fixed at compile time (a1 | a2 << 2 | a3 << 4);
