@@ -37,6 +37,9 @@ def test_compiled_caller_on_fixtures(binary, tmp_path):
     out = p.stdout
     iters = re.findall(r"CG Iter\[(\d+)\] Residual Norm=(\S+), Soln Norm=(\S+)", out)
     assert iters and iters[0][0] == "0" and iters[0][1].startswith("9.05595253")
+    # CG(10, 1e-10) and TRPO_Update's CG each stop after 8 FVPs on the fixture, as the reference does:
+    # 9 "CG Iter[...]" lines each (src/TRPO_CG.c:56 prints before the threshold test)
+    assert len(iters) == 18 and [int(i[0]) for i in iters] == list(range(9)) * 2
     assert re.search(r"shs: \S+", out) and re.search(r"lagrange multiplier: \S+, gnorm: \S+", out)
     assert re.search(r"a/e/r \S+ / \S+ / \S+", out)
     assert "[ERROR] Cannot open Model File" in p.stderr          # the bad-path call, reference message

@@ -39,12 +39,10 @@ def test_context_matches_reference_golden(name):
             out = ctx.cg(x["vin"], c["maxiter"], c["resth"])
             assert cases.rel_l2(out, cases.expected(c)) <= CG_TOL, ctx.kernel_name
             rr, xn, iters = ctx.cg_history()
-            if c["resth"] == 0.0:
-                assert iters == c["iters"]
-            else:
-                # fp32 FVP: the recurrence residual floors near 1e-9*|b|^2, so a threshold
-                # below that floor (1e-10 on the fixture) may cost one extra iteration.
-                assert c["iters"] <= iters <= c["iters"] + 1
+            # the reference's iteration count, ResidualTh 1e-10 included: without the residual
+            # reorthogonalisation the fp32 recurrence residual floors near 1e-9 |b|^2 and
+            # the fixture solve takes one iteration more (TRPO_CG_REORTH=0, tools/reorth_table.py)
+            assert iters == c["iters"]
             np.testing.assert_allclose(rr[:5], c["rdotr"][:5], rtol=1e-3)
 
 
@@ -205,3 +203,47 @@ def test_cooperative_kernel_shapes_against_oracle(layers, mode, monkeypatch):
         r = ctx.update()
         bref, _ = oracle.policy_grad(layers, "lttl", th, obs, mean, action, adv)
         assert cases.rel_l2(r["b"], bref) <= 2e-6
+
+
+def _fvp_cg_runs(layers, obs, reps=6):
+    from trpo_amd import synth
+    th = synth.make_theta(layers)
+    P = synth.num_params(layers)
+    std = np.array([0.6065306597126334, 0.8, 1.3])
+    v, b = synth.make_v(P), synth.make_b(P)
+    zs, xs = [], []
+    with trpo_amd.Context(layers, "lttl", th, obs, std, 0.1) as ctx:
+        for _ in range(reps):
+            zs.append(ctx.fvp(v))
+            xs.append(ctx.cg(b, 10, 0.0))
+    return zs, xs
+
+
+def test_atomic_path_bitwise_repeatable():
+    """The small-net path sums the per-block fp32 partials with fp64 atomics into replicas (DESIGN
+    §5.3): the adds are exact, so the arrival order cannot change a bit -- FVP and the 10-step CG
+    repeat bit for bit across launches at the bench size (256 blocks, 8 replicas)."""
+    from trpo_amd import synth
+    zs, xs = _fvp_cg_runs([15, 16, 16, 3], synth.make_obs(50000, 15))
+    for z in zs[1:]:
+        np.testing.assert_array_equal(z, zs[0])
+    for x in xs[1:]:
+        np.testing.assert_array_equal(x, xs[0])
+
+
+def test_atomic_path_wide_dynamic_range():
+    """Observations spread over 12 decades (rows scaled 1e-6 .. 1e6): the block partials of one
+    parameter then span far more than the 29 bits an fp64 sum of fp32 values absorbs exactly, so the
+    atomic order may move the last bits.  The guarantee that remains, and is checked here: every run
+    agrees with every other to fp64 rounding of the partial sums (<= 1e-13 relative).  (Against the
+    fp64 oracle such inputs sit at 2e-4: fp32 arithmetic on 1e6-scaled observations, not the sums.)"""
+    from trpo_amd import synth
+    n = 20000
+    obs = synth.make_obs(n, 15)
+    scale = 10.0 ** np.linspace(-6, 6, n)
+    obs = obs * scale[:, None]
+    zs, xs = _fvp_cg_runs([15, 16, 16, 3], obs, reps=8)
+    for z in zs[1:]:
+        assert cases.rel_l2(z, zs[0]) <= 1e-13
+    for x in xs[1:]:
+        assert np.all(np.isfinite(x)) and cases.rel_l2(x, xs[0]) <= 1e-10
