@@ -2588,6 +2588,173 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
     for (int e = threadIdx.x; e < zero_len; e += 1024) acc_zero[e] = 0.0;
 }
 
+// ---------------------------------------------------------------------------
+// Distributed CG step for the large-P paths (cooperative kernel: 2x64 and the fp64 mode), SURVEY §8a
+// src/TRPO_CG.c:65-103.  The fused form (every FVP block redoing the step on all P elements, the
+// basis streamed twice) re-reads ~(4 + 2 nq) P-vectors per block -- at P = 5 443 that is 0.2-0.6 MB
+// per CU per iteration.  Here the step is split over natural-order slices instead:
+//   cg_dots_kernel : z = zacc / N + lambda p (log-std block 2p + lambda p) for its slice, and the
+//                    slice's partial dots p.z, r.z, z.z, x.p, p.p, q_i.z (i < nq) -> dots[block][21]
+//   cg_axpy_kernel : every block sums the partial dots over the blocks in block order (fixed order:
+//                    every block gets the same bits), forms alpha, the reorthogonalisation
+//                    coefficients, |r'|^2 and beta as in the fused step, and updates its slice:
+//                    x += alpha p, r' = r - alpha z - c_r r - sum_i c_i q_i, p' = r' + beta p, the new
+//                    basis vector r' / |r'|; block 0 publishes the scalars and the history.
+// The next FVP gathers its direction fragments from p' (natural order).  Elements as adjacent pairs
+// (one 16-byte load per vector per thread), CGS_T threads per block.
+// ---------------------------------------------------------------------------
+constexpr int CGS_T = 256, CGS_K = 5 + QCAP;
+template <typename QT>
+__global__ void __launch_bounds__(CGS_T)
+cg_dots_kernel(const double *__restrict__ zacc, const double *__restrict__ p, const double *__restrict__ r,
+               const double *__restrict__ x, double *__restrict__ zbuf, double *__restrict__ dots, const void *qbuf_v,
+               const void *qz_v, int nq, int P, int Ps, int nw, const Ctl *__restrict__ ctl, const int *__restrict__ skip) {
+#pragma clang fp contract(off)
+    __shared__ double sh[CGS_K > 16 ? 32 * (CGS_T / 64) : 16 * (CGS_T / 64)];
+    const QT *Q = reinterpret_cast<const QT *>(qbuf_v);
+    const QT *qz = reinterpret_cast<const QT *>(qz_v);
+    const int tid = threadIdx.x, t = blockIdx.x * CGS_T + tid;        // pair index
+    const int tc = min(t, (Ps >> 1) - 1);
+    const double2 p2 = reinterpret_cast<const double2 *>(p)[tc], r2 = reinterpret_cast<const double2 *>(r)[tc];
+    const double2 x2 = reinterpret_cast<const double2 *>(x)[tc], a2 = reinterpret_cast<const double2 *>(zacc)[tc];
+    double qv[QCAP][2];
+    typedef typename V2T<QT>::type QV2;
+#pragma unroll
+    for (int i = 0; i < QCAP; ++i) {
+        const bool ok = i < nq;
+        const QV2 *src = ok ? reinterpret_cast<const QV2 *>(Q + (long)i * Ps) + tc
+                            : reinterpret_cast<const QV2 *>(qz) + (tid & 7);
+        const QV2 v = *src;
+        qv[i][0] = ok ? (double)v.x : 0.0;
+        qv[i][1] = ok ? (double)v.y : 0.0;
+    }
+    const double cn = ctl->n_total, lam = ctl->damping;
+    if (*skip) return;                                    // grid-uniform
+    const double pe[2] = {p2.x, p2.y}, re[2] = {r2.x, r2.y}, xe[2] = {x2.x, x2.y}, ae[2] = {a2.x, a2.y};
+    double red[CGS_K];
+#pragma unroll
+    for (int k = 0; k < CGS_K; ++k) red[k] = 0.0;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        const int q = 2 * t + e;
+        const bool in = q < P;
+        const double pv = in ? pe[e] : 0.0, rv = in ? re[e] : 0.0, xv = in ? xe[e] : 0.0;
+        const double zv = in ? __builtin_fma(lam, pv, q < nw ? ae[e] / cn : 2.0 * pv) : 0.0;
+        if (in) zbuf[q] = zv;
+        red[0] = __builtin_fma(pv, zv, red[0]);
+        red[1] = __builtin_fma(rv, zv, red[1]);
+        red[2] = __builtin_fma(zv, zv, red[2]);
+        red[3] = __builtin_fma(xv, pv, red[3]);
+        red[4] = __builtin_fma(pv, pv, red[4]);
+#pragma unroll
+        for (int i = 0; i < QCAP; ++i) red[5 + i] = __builtin_fma(in ? qv[i][e] : 0.0, zv, red[5 + i]);
+    }
+    block_sums_dpp<CGS_K, CGS_T / 64>(red, sh);
+    if (tid < CGS_K) {
+        double v = red[0];
+#pragma unroll
+        for (int k = 1; k < CGS_K; ++k) v = tid == k ? red[k] : v;
+        dots[(long)blockIdx.x * CGS_K + tid] = v;
+    }
+}
+
+template <typename QT>
+__global__ void __launch_bounds__(CGS_T)
+cg_axpy_kernel(const double *__restrict__ dots, int G, const double *__restrict__ zbuf,
+               const double *__restrict__ p_in, const double *__restrict__ r_in, double *__restrict__ p_out,
+               double *__restrict__ r_out, double *__restrict__ x, void *qbuf_v, const void *qz_v, int nq, int reorth,
+               int P, int Ps, Ctl *__restrict__ ctl, const CgSt *__restrict__ st_in, CgSt *__restrict__ st_out,
+               double *__restrict__ hist, const int *__restrict__ skip) {
+#pragma clang fp contract(off)
+    __shared__ double tot[CGS_K];
+    QT *Q = reinterpret_cast<QT *>(qbuf_v);
+    const QT *qz = reinterpret_cast<const QT *>(qz_v);
+    const int tid = threadIdx.x, t = blockIdx.x * CGS_T + tid;
+    const int tc = min(t, (Ps >> 1) - 1);
+    // the partial dots of every block, summed in block order by thread k (value k)
+    double part = 0.0;
+    if (tid < CGS_K) {
+        for (int b = 0; b < G; ++b) part += dots[(long)b * CGS_K + tid];
+    }
+    const double2 p2 = reinterpret_cast<const double2 *>(p_in)[tc], r2 = reinterpret_cast<const double2 *>(r_in)[tc];
+    const double2 x2 = reinterpret_cast<const double2 *>(x)[tc], z2 = reinterpret_cast<const double2 *>(zbuf)[tc];
+    double qv[QCAP][2];
+    typedef typename V2T<QT>::type QV2;
+#pragma unroll
+    for (int i = 0; i < QCAP; ++i) {
+        const bool ok = i < nq;
+        const QV2 *src = ok ? reinterpret_cast<const QV2 *>(Q + (long)i * Ps) + tc
+                            : reinterpret_cast<const QV2 *>(qz) + (tid & 7);
+        const QV2 v = *src;
+        qv[i][0] = ok ? (double)v.x : 0.0;
+        qv[i][1] = ok ? (double)v.y : 0.0;
+    }
+    const CgSt sin = *st_in;
+    const double cth = ctl->resth;
+    const int cmax = ctl->maxiter;
+    if (*skip) return;                                    // grid-uniform
+    if (tid < CGS_K) tot[tid] = part;
+    __syncthreads();
+    const double pz = tot[0], rz = tot[1], zz = tot[2], xp = tot[3], pp = tot[4];
+    const double alpha = sin.rdotr / pz;
+    // reorthogonalisation coefficients (as the fused step, fvp_mlp3_kernel / DESIGN §3)
+    double cs = 0.0, cr = 0.0;
+    const bool ro = reorth && sin.rdotr > 0.0;
+    if (ro) {
+        const double nrm = sqrt(sin.rdotr), cl = nrm - alpha * (rz / nrm);
+        cs = cl * cl;
+        cr = cl / nrm;
+    }
+    double c[QCAP];
+#pragma unroll
+    for (int i = 0; i < QCAP; ++i) {
+        c[i] = ro ? -alpha * tot[5 + i] : 0.0;             // zero for the slots >= nq
+        cs += c[i] * c[i];
+    }
+    const double nr = sin.rdotr - 2.0 * alpha * rz + alpha * alpha * zz - cs;
+    const double xn2 = sin.xx + 2.0 * alpha * xp + alpha * alpha * pp;
+    const double beta = nr / sin.rdotr;
+    const int it = sin.iter + 1;
+    const double pe[2] = {p2.x, p2.y}, re[2] = {r2.x, r2.y}, xe[2] = {x2.x, x2.y}, ze[2] = {z2.x, z2.y};
+    double xo[2], ro2[2], po[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        double rv = __builtin_fma(-alpha, ze[e], re[e]);
+        rv = __builtin_fma(-cr, re[e], rv);
+#pragma unroll
+        for (int i = 0; i < QCAP; ++i) rv = __builtin_fma(-c[i], qv[i][e], rv);
+        ro2[e] = rv;
+        xo[e] = __builtin_fma(alpha, pe[e], xe[e]);
+        po[e] = __builtin_fma(beta, pe[e], rv);
+    }
+    if (2 * t + 1 < P) {                                 // whole pairs: 16-byte stores
+        reinterpret_cast<double2 *>(x)[t] = make_double2(xo[0], xo[1]);
+        reinterpret_cast<double2 *>(r_out)[t] = make_double2(ro2[0], ro2[1]);
+        reinterpret_cast<double2 *>(p_out)[t] = make_double2(po[0], po[1]);
+    } else if (2 * t < P) {
+        x[2 * t] = xo[0];
+        r_out[2 * t] = ro2[0];
+        p_out[2 * t] = po[0];
+    }
+    if (reorth && it < QCAP) {                            // q_it = r' / |r'|
+        const double inv = nr > 0.0 ? 1.0 / sqrt(nr) : 0.0;
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+            if (2 * t + e < P) Q[(long)it * Ps + 2 * t + e] = (QT)(ro2[e] * inv);
+    }
+    if (blockIdx.x == 0 && tid == 0) {
+        const int done = (nr < cth || it >= cmax) ? 1 : 0;
+        st_out->rdotr = nr;
+        st_out->xx = xn2;
+        st_out->iter = it;
+        hist[2 * it] = nr;
+        hist[2 * it + 1] = sqrt(xn2);
+        ctl->rdotr = nr;
+        ctl->iter = it;
+        ctl->done = done;
+    }
+}
+
 // ===========================================================================
 // device layer (trpo_dev.h)
 // ===========================================================================
@@ -2750,6 +2917,8 @@ struct trpo_dev {
     const CoopEntry *coop_e;    // cooperative kernel for wide hidden layers (else NULL)
     int coop;
     int coop_fused;             // CG step fused into the cooperative FVP kernel (MODE 2)
+    int coop_dist;              // cooperative path: the CG step over slices (cg_dots / cg_axpy), TRPO_COOP_DIST
+    double *zbuf, *dotsbuf;     // its z (natural order, Ps) and per-block partial dots
     fast_launch_fn k_fvp, k_pg; // the tile kernel serving this shape, FVP and policy-gradient modes
     fast_launch_fn k_fvp_yc, k_cg_yc;   // the same kernel on the forward cache: standalone FVP, CG iteration
     fast_launch_fn k_cg_yc_q[4];        // one-wave-per-tile CG iteration by reorthogonalisation slots (kQB)
@@ -3104,6 +3273,15 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
             d->coop_fused = !(ef && atoi(ef) == 0) &&
                             (size_t)d->coop_e->main_bytes >=
                                 sizeof(double) * (d->P + 2 + 128 + QCAP * 4 * (d->coop_e->threads / 64));
+            // the distributed step forms |r'|^2 from the dots (|r|^2 - 2a r.z + a^2 z.z - sum c^2), as
+            // the fused small-net step does: in fp32 the FVP noise floor keeps |r'|^2 / |r|^2 far above
+            // fp64 rounding, but an fp64 solve that converges to ~1e-14 and keeps iterating (ResidualTh 0)
+            // cancels that difference to noise (measured: [32,16,16,1] 'lotl' fp64 9e-2 off), so the fp64
+            // mode keeps the fused cooperative step with its direct |r'|^2 reduction
+            const char *ed = getenv("TRPO_COOP_DIST");
+            d->coop_dist = !d->f64 && !(ed && atoi(ed) == 0);
+            DMALLOC(d->zbuf, sizeof(double) * d->Ps);
+            DMALLOC(d->dotsbuf, sizeof(double) * CGS_K * cdiv(d->Ps / 2, CGS_T));
             DMALLOC(d->imap, sizeof(int) * d->slab);
             hipLaunchKernelGGL(build_imap_coop_kernel, dim3(cdiv(d->slab, 256)), dim3(256), 0, d->stream, n, T[0],
                                T[1], d->f64, d->imap, d->slab);
@@ -3162,7 +3340,7 @@ extern "C" void trpo_dev_destroy(trpo_dev *d) {
     if (d->cg_exec) hipGraphExecDestroy(d->cg_exec);
     if (d->comm) ncclCommDestroy(d->comm);
     trpo_update_state_free(d->upd);
-    void *ptrs[] = {d->obs64, d->pg_d, d->pg_adv, d->pg_iv, d->st, d->pbuf[0], d->pbuf[1], d->rbuf[0], d->rbuf[1], d->accbuf, d->pacc, d->imap, d->tpack, d->vpack, d->tmap, d->vmap, d->pslot, d->obs4, d->yc, d->th32, d->v32, d->iv32, d->obs32, d->scratch,
+    void *ptrs[] = {d->zbuf, d->dotsbuf, d->obs64, d->pg_d, d->pg_adv, d->pg_iv, d->st, d->pbuf[0], d->pbuf[1], d->rbuf[0], d->rbuf[1], d->accbuf, d->pacc, d->imap, d->tpack, d->vpack, d->tmap, d->vmap, d->pslot, d->obs4, d->yc, d->th32, d->v32, d->iv32, d->obs32, d->scratch,
                     d->theta64, d->std64, d->r, d->zacc, d->slabs, d->ctl, d->hist, d->tscr, d->qbuf, d->qzero};
     for (void *p : ptrs)
         if (p) hipFree(p);
@@ -3796,6 +3974,40 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
                         (const void *)d->qzero, cg_step_nq(d, M - 1), d->Ps, d->atomic ? acc_slot(d, 0) : nullptr,
                         d->atomic ? RP : 0);
         }
+    } else if (d->coop && d->coop_dist) {
+        // cooperative kernel, distributed CG step: FVP j (direction gathered from p_j; K_0 recomputes
+        // the forward pass and writes the cache, K_1.. read it), the slab reduce [+ all-reduce], then
+        // the step over natural-order slices (cg_dots_kernel, cg_axpy_kernel)
+        const int G = cdiv(d->Ps / 2, CGS_T);
+        for (long j = 0; j < M; ++j) {
+            const int cur = (int)(j & 1), nxt = (int)((j + 1) & 1);
+            IterArgs a = plain_args(d, done);
+            a.v_nat = d->pbuf[cur];
+            if (d->yc_on) a.yc = reinterpret_cast<float4 *>(d->yc);
+            (j > 0 && d->yc_on ? d->k_fvp_yc : d->k_fvp)(dim3(d->grid), d->k_lds, d->stream, a, d->net);
+            launch_reduce(d, done);
+            int rc = allreduce(d, d->zacc, d->nw);
+            if (rc) return rc;
+            const int nq = cg_step_nq(d, j);
+            void *qb = d->reorth ? d->qbuf : (void *)d->qzero;
+            if (d->f64) {
+                hipLaunchKernelGGL(cg_dots_kernel<double>, dim3(G), dim3(CGS_T), 0, d->stream, d->zacc, d->pbuf[cur],
+                                   d->rbuf[cur], x, d->zbuf, d->dotsbuf, (const void *)qb, (const void *)d->qzero,
+                                   d->reorth ? nq : 0, d->P, d->Ps, d->nw, d->ctl, done);
+                hipLaunchKernelGGL(cg_axpy_kernel<double>, dim3(G), dim3(CGS_T), 0, d->stream, d->dotsbuf, G, d->zbuf,
+                                   d->pbuf[cur], d->rbuf[cur], d->pbuf[nxt], d->rbuf[nxt], x, qb,
+                                   (const void *)d->qzero, d->reorth ? nq : 0, d->reorth, d->P, d->Ps, d->ctl,
+                                   d->st + cur, d->st + nxt, d->hist, done);
+            } else {
+                hipLaunchKernelGGL(cg_dots_kernel<float>, dim3(G), dim3(CGS_T), 0, d->stream, d->zacc, d->pbuf[cur],
+                                   d->rbuf[cur], x, d->zbuf, d->dotsbuf, (const void *)qb, (const void *)d->qzero,
+                                   d->reorth ? nq : 0, d->P, d->Ps, d->nw, d->ctl, done);
+                hipLaunchKernelGGL(cg_axpy_kernel<float>, dim3(G), dim3(CGS_T), 0, d->stream, d->dotsbuf, G, d->zbuf,
+                                   d->pbuf[cur], d->rbuf[cur], d->pbuf[nxt], d->rbuf[nxt], x, qb,
+                                   (const void *)d->qzero, d->reorth ? nq : 0, d->reorth, d->P, d->Ps, d->ctl,
+                                   d->st + cur, d->st + nxt, d->hist, done);
+            }
+        }
     } else if (d->coop_fused) {
         // cooperative kernel: K_0 = FVP of p_0 (packed by cg_init); K_j (j >= 1) = CG step j-1 -> j
         // fused with FVP j (MODE 2); each followed by the slab reduce [+ all-reduce]
@@ -3854,7 +4066,7 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
 // through enqueue_fvp_core without the cache.
 static bool cg_writes_ycache(const trpo_dev *d, size_t maxiter) {
     if (!d->yc_on || maxiter == 0 || !d->fast) return false;
-    return !d->coop || d->coop_fused;
+    return !d->coop || d->coop_fused || d->coop_dist;
 }
 
 // after a CG solve whose K_0 wrote the forward-activation cache it holds the current theta's
