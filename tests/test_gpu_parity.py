@@ -222,7 +222,7 @@ def _fvp_cg_runs(layers, obs, reps=6):
 def test_atomic_path_bitwise_repeatable():
     """The small-net path sums the per-block fp32 partials with fp64 atomics into replicas (DESIGN
     §5.3): the adds are exact, so the arrival order cannot change a bit -- FVP and the 10-step CG
-    repeat bit for bit across launches at the bench size (256 blocks, 8 replicas)."""
+    repeat bit for bit across launches at the bench size (256 blocks, 6 replicas)."""
     from trpo_amd import synth
     zs, xs = _fvp_cg_runs([15, 16, 16, 3], synth.make_obs(50000, 15))
     for z in zs[1:]:

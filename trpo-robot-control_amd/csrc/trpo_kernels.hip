@@ -268,6 +268,10 @@ __device__ void block_sum2(double a, double b, double *sh, double &sa, double &s
 // the basis (6e-8) would itself exceed the FVP noise, so that mode keeps fp64.
 // ---------------------------------------------------------------------------
 constexpr int QCAP = 16;
+// fp64 atomic replica sets of the small-net FVP partial sums: at most RMAX, RMAX by
+// default (6 measured 1.6 % faster than 8 and 4 at N = 50k / 6 250: fewer prologue loads against
+// more adds per address)
+constexpr int RMAX = 6;
 
 // the thread's E elements (q = tid + e * nthreads) of basis vector i, or zeros for i >= nq / q >= P:
 // the load is unconditional (a select on the address: qz is a small zero line every lane may read)
@@ -900,9 +904,9 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
         if constexpr (PAIR) {
             // replicas summed in replica order as below; rows of stride Ps, pairs 16-byte aligned
             const double2 p2 = pair_at(A.p_in, 0, A.Ps), r2 = pair_at(A.r_in, 0, A.Ps), x2 = pair_at(xs, 0, A.Ps);
-            double2 za[8];
+            double2 za[RMAX];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) za[k] = pair_at(A.acc_in, min(k, A.R_in - 1), A.Ps);
+            for (int k = 0; k < RMAX; ++k) za[k] = pair_at(A.acc_in, min(k, A.R_in - 1), A.Ps);
             const int2 m2 = pair_at(A.pslot, 0, A.Ps);
             const double p0[2] = {p2.x, p2.y}, r0[2] = {r2.x, r2.y}, x0[2] = {x2.x, x2.y};
             const int mm[2] = {m2.x, m2.y};
@@ -912,7 +916,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
                 const bool in = q < A.P;
                 double z = e ? za[0].y : za[0].x;
 #pragma unroll
-                for (int k = 1; k < 8; ++k) z += k < A.R_in ? (e ? za[k].y : za[k].x) : 0.0;
+                for (int k = 1; k < RMAX; ++k) z += k < A.R_in ? (e ? za[k].y : za[k].x) : 0.0;
                 pv[e] = in ? p0[e] : 0.0;
                 rv[e] = in ? r0[e] : 0.0;
                 xv[e] = (in && blockIdx.x == 0) ? x0[e] : 0.0;
@@ -928,13 +932,13 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
             double z = 0.0;
             if constexpr (C::EMAX <= C::EMAX_REPLICAS) {
                 // up to 8 atomic replicas (small P only: 8 loads per element in flight)
-                double za[8];
+                double za[RMAX];
 #pragma unroll
-                for (int k = 0; k < 8; ++k) za[k] = A.acc_in[(long)min(k, A.R_in - 1) * A.Ps + qz];
+                for (int k = 0; k < RMAX; ++k) za[k] = A.acc_in[(long)min(k, A.R_in - 1) * A.Ps + qz];
                 z = za[0];                                // R_in >= 1: no select on the first term
 #ifndef TRPO_ABL_R1
 #pragma unroll
-                for (int k = 1; k < 8; ++k) z += k < A.R_in ? za[k] : 0.0;
+                for (int k = 1; k < RMAX; ++k) z += k < A.R_in ? za[k] : 0.0;
 #endif
             } else {
                 z = A.acc_in[qz];                         // slab mode: one reduced vector
@@ -3199,9 +3203,9 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
     }
     {
         const char *er = getenv("TRPO_REPLICAS");
-        d->R = er ? atoi(er) : 8;
+        d->R = er ? atoi(er) : RMAX;
         if (d->R < 1) d->R = 1;
-        if (d->R > 8) d->R = 8;
+        if (d->R > RMAX) d->R = RMAX;
     }
     DMALLOC(d->accbuf, sizeof(double) * 3 * d->R * d->Ps);
     DMALLOC(d->qbuf, sizeof(double) * QCAP * d->Ps);
