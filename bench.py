@@ -45,6 +45,8 @@ def parse_args():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--comm", choices=("rccl", "peer"), default="rccl",
+                    help="N > 1: collective of the headline solve (peer: the peer-window exchange over xGMI)")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the secondary configs (C2, C3 2x64, fp64, C5, baseline, N sweep)")
     return ap.parse_args()
@@ -114,6 +116,13 @@ class Dist:
         self.dist.broadcast_object_list(obj, src=0)
         return obj[0]
 
+    def allgather_bytes(self, b):
+        if self.world == 1:
+            return [b]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, b)
+        return out
+
     def max(self, x: float) -> float:
         if self.world == 1:
             return x
@@ -127,8 +136,9 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def make_ctx(L, n_total, dist, device, precision=None):
-    """This rank's context: all weights, its contiguous shard of the seeded observation stream."""
+def make_ctx(L, n_total, dist, device, precision=None, comm="rccl"):
+    """This rank's context: all weights, its contiguous shard of the seeded observation stream.
+    comm: "rccl" (RCCL communicator) or "peer" (the peer-window exchange over xGMI, csrc/trpo_peer.hip)."""
     import numpy as np
     import trpo_amd
     from trpo_amd import synth
@@ -137,9 +147,13 @@ def make_ctx(L, n_total, dist, device, precision=None):
     lo, hi = shard_range(n_total, dist.rank, dist.world)
     obs = synth.make_obs(hi - lo, L[0], start=lo)
     ctx = trpo_amd.Context(L, "lttl", theta, obs, np.ones(L[-1]), DAMPING, device=device, precision=precision)
-    if dist.world > 1:
+    if dist.world > 1 and comm == "peer":
+        handles = dist.allgather_bytes(ctx.peer_handle())
+        ctx.attach_peers(dist.rank, dist.world, handles)
+    elif dist.world > 1:
         uid = dist.bcast_bytes(trpo_amd.unique_id() if dist.rank == 0 else None)
         ctx.attach_comm(dist.rank, dist.world, uid)
+    if dist.world > 1:
         info = ctx.comm_info()
         if info["world"] != dist.world:
             raise SystemExit("RCCL communicator has %d ranks, expected %d" % (info["world"], dist.world))
@@ -342,12 +356,66 @@ def extras_single(device, dist, reps):
     return extra
 
 
-def sweep(device, dist, steps=10):
+def extras_multi(device, dist, b, x_rccl, comm="rccl"):
+    """N > 1: the same sharded solve with the peer-window exchange in place of RCCL (A/B on the driver's
+    multi-GPU node), and one sharded TRPO update (config C5) under RCCL."""
+    import numpy as np
+    from trpo_amd import synth
+    out = {}
+    res, ctx = None, None
+    other = "rccl" if comm == "peer" else "peer"
+    try:
+        ctx, _, _ = make_ctx(ARM, N_TOTAL, dist, device, comm=other)
+        ok = 1.0
+    except Exception as e:                      # noqa: BLE001 -- recorded, every rank skips together
+        res = {"error": "%s: %s" % (type(e).__name__, e)}
+        ok = 0.0
+    if dist.max(1.0 - ok) == 0.0:               # all ranks attached
+        try:
+            t = time_steps(ctx, dist, 50, 5, b)
+            x = ctx.download_x()
+            res = {"ms_per_step": 1e3 * t / 50, "fvp_samples_per_s": CG_ITERS * N_TOTAL / (t / 50),
+                   "backend": ctx.comm_backend, "n_gpus": dist.world,
+                   "x_relL2_vs_headline": float(np.linalg.norm(x - x_rccl) / np.linalg.norm(x_rccl))}
+        except Exception as e:                  # noqa: BLE001
+            res = {"error": "%s: %s" % (type(e).__name__, e)}
+    elif res is None:
+        res = {"error": "another rank failed to attach"}
+    if ctx is not None:
+        ctx.close()
+    out["C4_%s_exchange" % other] = res
+    # C5: one TRPO policy update over the sharded rollout (policy-gradient / FVP / surrogate all-reduces)
+    theta = synth.make_theta(ARM)
+    obs_all = synth.make_obs(N_TOTAL, ARM[0])
+    std = np.ones(ARM[-1])
+    mean, action, adv = synth.make_rollout(ARM, "lttl", theta, obs_all, std)
+    ctx, _, obs = make_ctx(ARM, N_TOTAL, dist, device, comm=comm)
+    from trpo_amd.dist import shard_range
+    lo, hi = shard_range(N_TOTAL, dist.rank, dist.world)
+    ctx.set_rollout(mean[lo:hi], action[lo:hi], adv[lo:hi])
+    ctx_backend = ctx.comm_backend
+    for _ in range(3):
+        r = ctx.update()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(20):
+        r = ctx.update()
+    wall = dist.max((time.perf_counter() - t0) / 20)
+    ctx.close()
+    out["C5_update_armDOF_0_N50000"] = {"update_ms": 1e3 * wall, "accepted": r["accepted"],
+                                        "cg_iters": int(r["cg_iters"]), "samples": N_TOTAL, "n_gpus": dist.world,
+                                        "comm": ctx_backend,
+                                        "what": "sharded rollout; all-reduces of the policy gradient, every FVP "
+                                                "and the surrogate sums; host-visible wall per update (max over ranks)"}
+    return out
+
+
+def sweep(device, dist, steps=10, comm="rccl"):
     """C4's N sweep: the same sharded 10-iteration solve at larger batches (whole-job rates)."""
     from trpo_amd import synth
     out = {}
     for n in SWEEP_N:
-        ctx, _, _ = make_ctx(ARM, n, dist, device)
+        ctx, _, _ = make_ctx(ARM, n, dist, device, comm=comm)
         t = time_steps(ctx, dist, steps, 2, synth.make_b(num_params(ARM)))
         out["cg10_armDOF_0_N%d" % n] = {"ms_per_step": 1e3 * t / steps,
                                         "fvp_samples_per_s": CG_ITERS * n / (t / steps), "n_gpus": dist.world}
@@ -369,7 +437,7 @@ def main():
         sys.exit(2)
     device = int(os.environ.get("TRPO_BENCH_DEVICE", dist.local_rank))   # override: testing only
 
-    ctx, theta, obs_local = make_ctx(ARM, N_TOTAL, dist, device)
+    ctx, theta, obs_local = make_ctx(ARM, N_TOTAL, dist, device, comm=args.comm)
     comm = ctx.comm_info()
     P = num_params(ARM)
     b = synth.make_b(P)
@@ -414,9 +482,10 @@ def main():
         "config": {"workload": "cg10_armDOF_0_N50000", "policy": "armDOF_0 [15,16,16,3] lttl",
                    "samples": N_TOTAL, "samples_per_rank": n_local, "cg_iters": CG_ITERS, "residual_th": 0.0,
                    "damping": DAMPING,
-                   "parallelism": "dp%d (contiguous sample shards, RCCL all-reduce per FVP)" % dist.world,
+                   "parallelism": "dp%d (contiguous sample shards, %s all-reduce per FVP)"
+                                  % (dist.world, "RCCL" if args.comm == "rccl" else "peer-window"),
                    "cg_scalars": "fp64", "fvp_kernel": ctx.kernel_name, "geometry": ctx.geometry},
-        "comm": {"backend": "rccl" if dist.world > 1 else "none", "ranks": comm["world"],
+        "comm": {"backend": comm["backend"], "ranks": comm["world"],
                  "replicas_per_fvp": comm["replicas"]},
         "cg_wall_ms": ms_per_step,
         "roofline": {"bound": "hbm" if hbm_bound else "mfma",
@@ -436,7 +505,9 @@ def main():
     if not args.no_extra:
         if dist.world == 1:
             result["extra"] = extras_single(device, dist, 200)
-        result.setdefault("extra", {})["C4_sweep"] = sweep(device, dist)
+        else:
+            result["extra"] = extras_multi(device, dist, b, x, args.comm)
+        result.setdefault("extra", {})["C4_sweep"] = sweep(device, dist, comm=args.comm)
 
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
         threads_all = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)

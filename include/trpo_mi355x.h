@@ -145,6 +145,23 @@ int trpo_ctx_attach_group(trpo_ctx *ctx, trpo_group *g, int rank);
  * all-reduces (0 when the block-slab reduction is in use). */
 int trpo_ctx_comm_info(const trpo_ctx *ctx, int *rank, int *world, int *replicas);
 
+/* Peer-window exchange over xGMI (one-shot all-reduce; no reference counterpart -- it replaces the
+ * collective under the sharded CG of src/TRPO_CG.c:45-104).  Each rank allocates an exchange window
+ * in its own HBM and exports it: trpo_ctx_peer_handle() writes TRPO_PEER_HANDLE_BYTES; the caller
+ * all-gathers the handles (its own bootstrap, as for the RCCL unique id) and every rank calls
+ * trpo_ctx_attach_peers() concurrently with the world's handles in rank order.  Every collective of
+ * the context then goes through the exchange kernel (rank-order sums: identical bits on every rank);
+ * the CG graph's per-FVP all-reduce is one kernel.  Contexts of ONE process (tests; any devices)
+ * attach with trpo_ctx_attach_peers_local() after each has called trpo_ctx_peer_handle(ctx, NULL).
+ * A rank that never arrives makes the exchange give up after ~1 s: later calls return an error. */
+#define TRPO_PEER_HANDLE_BYTES 64
+#define TRPO_PEER_MAX_RANKS 16
+int trpo_ctx_peer_handle(trpo_ctx *ctx, void *handle_64);
+int trpo_ctx_attach_peers(trpo_ctx *ctx, int rank, int world, const void *handles);
+int trpo_ctx_attach_peers_local(trpo_ctx *ctx, int rank, int world, trpo_ctx *const *all);
+/* "rccl", "peer-xgmi (...)", "host-group" or "none" */
+const char *trpo_ctx_comm_backend(const trpo_ctx *ctx);
+
 /* Host-pointer convenience entry points (copy in / compute / copy out).
  * Return elapsed seconds (>= 0) or a negative error code. */
 double trpo_ctx_fvp(trpo_ctx *ctx, const double *v, double *out);

@@ -1,0 +1,45 @@
+"""One rank of tests/test_gpu_peer.py::test_peer_ipc_two_processes (run as a child process):
+    python tests/peer_worker.py RANK WORLD DIR
+Builds its contiguous shard of the syn_arm_cg_n50000 golden, exports its peer window handle to
+DIR/h<rank>.bin, waits for every rank's handle, attaches, solves CG and writes DIR/x<rank>.npy."""
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path[:0] = [HERE, os.path.join(ROOT, "trpo-robot-control_amd")]
+
+import numpy as np  # noqa: E402
+
+import cases  # noqa: E402
+import trpo_amd  # noqa: E402
+from trpo_amd.dist import shard_range  # noqa: E402
+
+
+def main():
+    rank, world, d = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
+    c = cases.case("syn_arm_cg_n50000")
+    x = cases.inputs(c)
+    lo, hi = shard_range(x["obs"].shape[0], rank, world)
+    with trpo_amd.Context(x["layers"], x["acfunc"], x["theta"], x["obs"][lo:hi], x["std"], x["damping"]) as ctx:
+        h = ctx.peer_handle()
+        with open(os.path.join(d, "h%d.tmp" % rank), "wb") as f:
+            f.write(h)
+        os.rename(os.path.join(d, "h%d.tmp" % rank), os.path.join(d, "h%d.bin" % rank))
+        paths = [os.path.join(d, "h%d.bin" % r) for r in range(world)]
+        t0 = time.time()
+        while not all(os.path.exists(p) for p in paths):
+            if time.time() - t0 > 60:
+                raise SystemExit("rank %d: handles missing" % rank)
+            time.sleep(0.01)
+        handles = [open(p, "rb").read() for p in paths]
+        ctx.attach_peers(rank, world, handles)
+        xs = ctx.cg(x["vin"], c["maxiter"], c["resth"])
+        np.save(os.path.join(d, "x%d.npy" % rank), xs)
+        with open(os.path.join(d, "backend%d.txt" % rank), "w") as f:
+            f.write(ctx.comm_backend)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,184 @@
+"""The peer-window exchange (csrc/trpo_peer.hip) on ONE GPU: the one-shot all-reduce over xGMI that
+replaces RCCL under the sharded CG (reference CG loop src/TRPO_CG.c:45-104 around the
+per-sample FVP loop src/TRPO_FVP.c:771-921).
+
+Two ways of running several ranks on one device:
+  * in-process: contexts of one process, one thread per rank, windows joined by pointer
+    (trpo_ctx_attach_peers_local) -- the CG runs from its captured graph, one exchange kernel per FVP;
+  * multi-process: one process per rank (tests/peer_worker.py), windows exported and opened as IPC
+    handles (trpo_ctx_attach_peers) -- the path bench.py takes across GPUs.
+Checked: every rank ends with a bit-identical x (rank-order sums), x within the north-star bound of
+the reference's golden and within rounding of the host-group exchange, standalone FVPs and the full
+TRPO_Update through the generic in-place exchange, and that a rank that never arrives makes the
+exchange give up with an error instead of hanging the GPU.
+"""
+import os
+import subprocess
+import sys
+import tempfile
+import threading
+
+import numpy as np
+import pytest
+
+import cases
+import trpo_amd
+from trpo_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CG_TOL = 1e-4
+
+
+def run_peer_ranks(ctxs, fn, timeout=120.0):
+    """Open every window, then attach and run fn(ctx, rank) on all contexts concurrently."""
+    for c in ctxs:
+        c.peer_handle()
+    world = len(ctxs)
+    out, err = [None] * world, [None] * world
+
+    def work(r):
+        try:
+            ctxs[r].attach_peers_local(r, ctxs)
+            out[r] = fn(ctxs[r], r)
+        except BaseException as e:          # noqa: BLE001 -- reported below
+            err[r] = e
+
+    ts = [threading.Thread(target=work, args=(r,), daemon=True) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout)
+    assert not any(t.is_alive() for t in ts), "a rank did not finish"
+    for e in err:
+        if e is not None:
+            raise e
+    return out
+
+
+def _shards(x, bounds):
+    return [trpo_amd.Context(x["layers"], x["acfunc"], x["theta"], x["obs"][lo:hi], x["std"], x["damping"])
+            for lo, hi in bounds]
+
+
+@pytest.mark.parametrize("bounds", [[(0, 25000), (25000, 50000)], [(0, 10000), (10000, 30001), (30001, 50000)]])
+def test_peer_cg_lockstep_and_golden(bounds):
+    c = cases.case("syn_arm_cg_n50000")
+    x = cases.inputs(c)
+    ctxs = _shards(x, bounds)
+    try:
+        res = run_peer_ranks(ctxs, lambda ctx, r: (ctx.cg(x["vin"], c["maxiter"], c["resth"]),
+                                                   ctx.cg(x["vin"], c["maxiter"], c["resth"]),   # graph replay
+                                                   ctx.cg_history(), ctx.comm_info()))
+    finally:
+        for ctx in ctxs:
+            ctx.close()
+    x0 = res[0][0]
+    for r, (xa, xb, (rr, xn, it), info) in enumerate(res):
+        np.testing.assert_array_equal(xa, x0)            # lockstep: identical bits on every rank
+        np.testing.assert_array_equal(xb, x0)            # the replayed graph repeats the solve
+        assert it == c["iters"]
+        assert info["rank"] == r and info["world"] == len(bounds)
+        assert info["backend"].startswith("peer-xgmi"), info
+    assert cases.rel_l2(x0, cases.expected(c)) <= CG_TOL
+
+
+def test_peer_matches_host_group():
+    """The same shards through the host-staged group: the exchange only changes the summation order
+    (per-rank replica sums first), so the steps agree to rounding."""
+    from test_gpu_shard import run_ranks
+    c = cases.case("syn_arm_cg_n50000")
+    x = cases.inputs(c)
+    bounds = [(0, 20000), (20000, 50000)]
+    ctxs = _shards(x, bounds)
+    try:
+        xg = run_ranks(ctxs, lambda ctx, r: ctx.cg(x["vin"], c["maxiter"], c["resth"]))[0]
+    finally:
+        for ctx in ctxs:
+            ctx.close()
+    ctxs = _shards(x, bounds)
+    try:
+        xp = run_peer_ranks(ctxs, lambda ctx, r: ctx.cg(x["vin"], c["maxiter"], c["resth"]))[0]
+    finally:
+        for ctx in ctxs:
+            ctx.close()
+    assert cases.rel_l2(xp, xg) <= 1e-9
+
+
+def test_peer_fvp_and_update():
+    """Standalone FVP (atomic replica sets all-reduced in place) and TRPO_Update (policy-gradient,
+    FVP(x) and surrogate sums) through the generic exchange, against one context over all samples."""
+    c = cases.case("fix_fvp_n3150")
+    x = cases.inputs(c)
+    ctxs = _shards(x, [(0, 1000), (1000, 3150)])
+    try:
+        res = run_peer_ranks(ctxs, lambda ctx, r: ctx.fvp(x["vin"]))
+    finally:
+        for ctx in ctxs:
+            ctx.close()
+    np.testing.assert_array_equal(res[0], res[1])
+    assert cases.rel_l2(res[0], cases.expected(c)) <= 1e-5
+
+    layers, n = [15, 16, 16, 3], 6000
+    th, obs = synth.make_theta(layers), synth.make_obs(n, layers[0])
+    std = np.ones(layers[-1])
+    mean, action, adv = synth.make_rollout(layers, "lttl", th, obs, std)
+    with trpo_amd.Context(layers, "lttl", th, obs, std, 0.1) as one:
+        one.set_rollout(mean, action, adv)
+        ref = one.update()
+    bounds = [(0, 2500), (2500, n)]
+    ctxs = [trpo_amd.Context(layers, "lttl", th, obs[lo:hi], std, 0.1) for lo, hi in bounds]
+    for ctx, (lo, hi) in zip(ctxs, bounds):
+        ctx.set_rollout(mean[lo:hi], action[lo:hi], adv[lo:hi])
+    try:
+        res = run_peer_ranks(ctxs, lambda ctx, r: ctx.update())
+    finally:
+        for ctx in ctxs:
+            ctx.close()
+    for key in ("theta", "x", "b"):
+        np.testing.assert_array_equal(res[0][key], res[1][key])
+    assert res[0]["accepted"] == ref["accepted"]
+    assert cases.rel_l2(res[0]["b"], ref["b"]) <= 2e-6
+    assert cases.rel_l2(res[0]["x"], ref["x"]) <= 1e-4
+
+
+def test_peer_missing_rank_times_out():
+    """Only rank 0 of a world of 2 attaches: its exchange (the shard-size all-reduce of the attach)
+    waits 3 s for rank 1, then gives up with an error -- the GPU is released, nothing hangs."""
+    c = cases.case("fix_fvp_n3150")
+    x = cases.inputs(c)
+    ctxs = _shards(x, [(0, 1000), (1000, 3150)])
+    try:
+        for ctx in ctxs:
+            ctx.peer_handle()
+        with pytest.raises(trpo_amd.TRPOError):
+            ctxs[0].attach_peers_local(0, ctxs)
+    finally:
+        for ctx in ctxs:
+            ctx.close()
+
+
+def test_peer_ipc_two_processes():
+    """One process per rank on the same GPU, windows exchanged as IPC handles through files."""
+    c = cases.case("syn_arm_cg_n50000")
+    world = 2
+    with tempfile.TemporaryDirectory() as tmp:
+        procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "peer_worker.py"), str(r), str(world), tmp],
+                                  stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+                 for r in range(world)]
+        outs = []
+        try:
+            for p in procs:
+                outs.append(p.communicate(timeout=150)[0])
+        finally:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+        for p, o in zip(procs, outs):
+            assert p.returncode == 0, o
+        xs = [np.load(os.path.join(tmp, "x%d.npy" % r)) for r in range(world)]
+        backends = [open(os.path.join(tmp, "backend%d.txt" % r)).read() for r in range(world)]
+    np.testing.assert_array_equal(xs[0], xs[1])
+    assert all(b.startswith("peer-xgmi") for b in backends), backends
+    assert cases.rel_l2(xs[0], cases.expected(c)) <= CG_TOL

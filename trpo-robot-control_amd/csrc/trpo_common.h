@@ -91,4 +91,19 @@ void trpo_dev_ycache_written(trpo_dev *d);
 void **trpo_dev_update_state(trpo_dev *d);
 void trpo_update_state_free(void *state);
 
+// Peer-window exchange (trpo_peer.hip): one-shot all-reduce of small fp64 vectors over xGMI.
+#define PEER_WMAX 16                 // ranks
+#define PEER_HANDLE_BYTES 64         // one exported window (hipIpcMemHandle_t)
+struct trpo_peer;
+trpo_peer *trpo_peer_create(int device, size_t slot_doubles);
+void trpo_peer_destroy(trpo_peer *p);
+int trpo_peer_handle(trpo_peer *p, void *h64);
+void *trpo_peer_window(trpo_peer *p);
+int trpo_peer_connect(trpo_peer *p, int rank, int world, const void *handles, void *const *local);
+int trpo_peer_allreduce(trpo_peer *p, hipStream_t st, const double *in, int R, int Rstride, int count, double *out,
+                        const int *done);
+int trpo_peer_error(const trpo_peer *p);
+size_t trpo_peer_slot(const trpo_peer *p);
+int trpo_peer_uncached(const trpo_peer *p);
+
 #endif

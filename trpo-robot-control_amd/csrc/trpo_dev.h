@@ -37,6 +37,14 @@ trpo_hgroup *trpo_hgroup_create(int world);
 void trpo_hgroup_destroy(trpo_hgroup *g);
 int trpo_dev_set_group(trpo_dev *d, trpo_hgroup *g, int rank);
 int trpo_dev_comm_info(const trpo_dev *d, int *rank, int *world, int *replicas);
+/* peer-window exchange over xGMI (trpo_peer.hip): open the own window (its 64-byte IPC handle into
+ * handle64 when non-NULL), then attach with the world's handles (rank order) or, in one process,
+ * the contexts' window pointers; replaces RCCL / the host group for this context */
+int trpo_dev_peer_open(trpo_dev *d, void *handle64);
+void *trpo_dev_peer_window(trpo_dev *d);
+int trpo_dev_set_peers(trpo_dev *d, int rank, int world, const void *handles, void *const *local);
+int trpo_dev_comm_error(const trpo_dev *d);
+const char *trpo_dev_comm_backend(const trpo_dev *d);
 
 int trpo_dev_upload(trpo_dev *d, int slot, const double *host);
 int trpo_dev_download(trpo_dev *d, int slot, double *host);

@@ -170,6 +170,35 @@ int trpo_ctx_comm_info(const trpo_ctx *c, int *rank, int *world, int *replicas) 
     return c ? trpo_dev_comm_info(c->dev, rank, world, replicas) : TRPO_E_INVALID;
 }
 
+int trpo_ctx_peer_handle(trpo_ctx *c, void *handle_64) {
+    if (!c) return TRPO_E_INVALID;
+    const int rc = trpo_dev_peer_open(c->dev, handle_64);
+    if (rc) set_err("peer window open / IPC export failed (code %d)", rc);
+    return rc;
+}
+int trpo_ctx_attach_peers(trpo_ctx *c, int rank, int world, const void *handles) {
+    if (!c || !handles) return TRPO_E_INVALID;
+    int rc = trpo_dev_peer_open(c->dev, NULL);
+    if (!rc) rc = trpo_dev_set_peers(c->dev, rank, world, handles, NULL);
+    if (rc) set_err("attach_peers(rank %d of %d) failed (code %d)", rank, world, rc);
+    return rc;
+}
+int trpo_ctx_attach_peers_local(trpo_ctx *c, int rank, int world, trpo_ctx *const *all) {
+    if (!c || !all || world < 1 || world > TRPO_PEER_MAX_RANKS) return TRPO_E_INVALID;
+    void *w[TRPO_PEER_MAX_RANKS];
+    for (int r = 0; r < world; ++r) {
+        w[r] = all[r] ? trpo_dev_peer_window(all[r]->dev) : NULL;
+        if (!w[r]) {
+            set_err("attach_peers_local: rank %d has no open peer window (trpo_ctx_peer_handle first)", r);
+            return TRPO_E_INVALID;
+        }
+    }
+    const int rc = trpo_dev_set_peers(c->dev, rank, world, NULL, w);
+    if (rc) set_err("attach_peers_local(rank %d of %d) failed (code %d)", rank, world, rc);
+    return rc;
+}
+const char *trpo_ctx_comm_backend(const trpo_ctx *c) { return c ? trpo_dev_comm_backend(c->dev) : ""; }
+
 double trpo_ctx_fvp(trpo_ctx *c, const double *v, double *out) {
     if (!c || !v || !out) return TRPO_E_INVALID;
     const double t0 = now_s();

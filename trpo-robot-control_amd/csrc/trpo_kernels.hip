@@ -2996,6 +2996,12 @@ struct trpo_dev {
     trpo_hgroup *group;
     double *gbuf;               // pinned host staging for the group exchange
     size_t gbuf_cap;
+    // peer-window exchange over xGMI (trpo_peer.hip): when peer_on, every collective goes through it
+    // and the CG graph's per-FVP all-reduce becomes one exchange kernel into zred
+    trpo_peer *peer;
+    int peer_on;
+    double *zred;               // [2][Ps] exchanged partial sums (the next CG-iteration kernel's input)
+    double *ptmp;               // [slot] staging of an in-place all-reduce
     int rank, world;
     char name[64];
 };
@@ -3343,9 +3349,10 @@ extern "C" void trpo_dev_destroy(trpo_dev *d) {
     if (d->stream) hipStreamSynchronize(d->stream);
     if (d->cg_exec) hipGraphExecDestroy(d->cg_exec);
     if (d->comm) ncclCommDestroy(d->comm);
+    trpo_peer_destroy(d->peer);
     trpo_update_state_free(d->upd);
     void *ptrs[] = {d->zbuf, d->dotsbuf, d->obs64, d->pg_d, d->pg_adv, d->pg_iv, d->st, d->pbuf[0], d->pbuf[1], d->rbuf[0], d->rbuf[1], d->accbuf, d->pacc, d->imap, d->tpack, d->vpack, d->tmap, d->vmap, d->pslot, d->obs4, d->yc, d->th32, d->v32, d->iv32, d->obs32, d->scratch,
-                    d->theta64, d->std64, d->r, d->zacc, d->slabs, d->ctl, d->hist, d->tscr, d->qbuf, d->qzero};
+                    d->theta64, d->std64, d->r, d->zacc, d->slabs, d->ctl, d->hist, d->tscr, d->qbuf, d->qzero, d->zred, d->ptmp};
     for (void *p : ptrs)
         if (p) hipFree(p);
     for (int i = 0; i < 5; ++i)
@@ -3544,7 +3551,7 @@ static int choose_replicas(trpo_dev *d) {
 // N is the global sample count: local n, or the all-reduced n under RCCL
 static int refresh_n_total(trpo_dev *d) {
     const size_t n = d->n;
-    if (d->comm || d->group) {
+    if (d->comm || d->group || d->peer_on) {
         // every rank's shard size in one sum-all-reduce (rank r contributes n at slot r): N is the
         // total, and the replica sizing below reads the LARGEST shard -- both identical on all ranks
         const int W = d->world;
@@ -3598,6 +3605,7 @@ extern "C" int trpo_dev_set_group(trpo_dev *d, trpo_hgroup *g, int rank) {
     g->attached[rank] = 1;
     pthread_mutex_unlock(&g->mu);
     if (taken) return -1;
+    d->peer_on = 0;
     d->group = g;
     d->rank = rank;
     d->world = g->world;
@@ -3628,6 +3636,7 @@ extern "C" int trpo_dev_set_comm(trpo_dev *d, int rank, int world, const void *i
     if (!d || world < 1 || rank < 0 || rank >= world) return -1;
     HCHK(hipSetDevice(d->device));
     d->group = NULL;
+    d->peer_on = 0;
     if (d->comm) {
         ncclCommDestroy(d->comm);
         d->comm = NULL;
@@ -3650,6 +3659,71 @@ extern "C" int trpo_dev_set_comm(trpo_dev *d, int rank, int world, const void *i
         d->cg_exec = NULL;
     }
     return refresh_n_total(d);
+}
+
+// ---------------------------------------------------------------------------
+// Peer-window exchange (trpo_peer.hip).  Two steps, like RCCL's unique id: every rank opens its
+// window and hands the exported handle to the caller's bootstrap; then every rank attaches with the
+// world's handles in rank order (or, for contexts of one process, their window pointers).  Attaching
+// replaces an RCCL communicator or host group: all collectives of the context then go through the
+// exchange kernel.  All ranks must attach concurrently (the attach all-reduces the shard sizes).
+// ---------------------------------------------------------------------------
+static size_t peer_slot_doubles(const trpo_dev *d) {
+    size_t s = (size_t)d->R * d->Ps;                       // a standalone FVP's replica sets
+    if (s < (size_t)d->P + 1) s = (size_t)d->P + 1;        // the policy-gradient sums
+    if (s < 64) s = 64;                                    // line-search sums, shard sizes
+    return s;
+}
+
+extern "C" int trpo_dev_peer_open(trpo_dev *d, void *handle64) {
+    if (!d) return -1;
+    HCHK(hipSetDevice(d->device));
+    if (!d->peer) {
+        d->peer = trpo_peer_create(d->device, peer_slot_doubles(d));
+        if (!d->peer) return -2;
+        HCHK(hipMalloc((void **)&d->zred, sizeof(double) * 2 * d->Ps));
+        HCHK(hipMemset(d->zred, 0, sizeof(double) * 2 * d->Ps));
+        HCHK(hipMalloc((void **)&d->ptmp, sizeof(double) * trpo_peer_slot(d->peer)));
+    }
+    return handle64 ? trpo_peer_handle(d->peer, handle64) : 0;
+}
+
+extern "C" void *trpo_dev_peer_window(trpo_dev *d) { return d && d->peer ? trpo_peer_window(d->peer) : NULL; }
+
+extern "C" int trpo_dev_comm_error(const trpo_dev *d);
+extern "C" int trpo_dev_set_peers(trpo_dev *d, int rank, int world, const void *handles, void *const *local) {
+    if (!d || !d->peer || world < 1 || world > PEER_WMAX || rank < 0 || rank >= world) return -1;
+    HCHK(hipSetDevice(d->device));
+    HCHK(hipStreamSynchronize(d->stream));
+    const int rc = trpo_peer_connect(d->peer, rank, world, handles, local);
+    if (rc) return rc;
+    if (d->comm) {
+        ncclCommDestroy(d->comm);
+        d->comm = NULL;
+    }
+    d->group = NULL;
+    d->peer_on = world > 1;
+    d->rank = rank;
+    d->world = world;
+    if (d->cg_exec) {
+        hipGraphExecDestroy(d->cg_exec);
+        d->cg_exec = NULL;
+    }
+    const int rn = refresh_n_total(d);
+    return rn ? rn : trpo_dev_comm_error(d);
+}
+
+// -4 after a peer exchange whose wait timed out (a rank missing); 0 otherwise
+extern "C" int trpo_dev_comm_error(const trpo_dev *d) {
+    return d && d->peer_on && trpo_peer_error(d->peer) ? -4 : 0;
+}
+
+extern "C" const char *trpo_dev_comm_backend(const trpo_dev *d) {
+    if (!d) return "";
+    if (d->peer_on) return trpo_peer_uncached(d->peer) ? "peer-xgmi (uncached window)" : "peer-xgmi (fine-grained window)";
+    if (d->comm) return "rccl";
+    if (d->group) return "host-group";
+    return "none";
 }
 
 // Host <-> device vector moves through a pinned, device-mapped host buffer and a copy kernel: a
@@ -3699,7 +3773,7 @@ extern "C" int trpo_dev_download(trpo_dev *d, int slot, double *host) {
     HCHK(hipStreamSynchronize(d->stream));
     d->hst_pending = 0;
     memcpy(host, d->hst, sizeof(double) * d->P);
-    return 0;
+    return trpo_dev_comm_error(d);
 }
 
 static IterArgs plain_args(trpo_dev *d, const int *skip) {
@@ -3871,10 +3945,17 @@ static int ensure_hist(trpo_dev *d, size_t maxiter) {
 }
 
 static double *acc_slot(trpo_dev *d, long j) { return d->accbuf + (j % 3) * (long)d->R * d->Ps; }
+static double *zred_slot(trpo_dev *d, long j) { return d->zred + (j & 1) * (long)d->Ps; }
 
 // the one place every collective of the library goes through: RCCL, the in-process host group, or
 // nothing (one rank)
 static int allreduce(trpo_dev *d, double *buf, size_t count) {
+    if (d->peer_on) {
+        // in place through the staging vector (the exchange kernel's output must not alias its input)
+        if (count > trpo_peer_slot(d->peer)) return -1;
+        HCHK(hipMemcpyAsync(d->ptmp, buf, sizeof(double) * count, hipMemcpyDeviceToDevice, d->stream));
+        return trpo_peer_allreduce(d->peer, d->stream, d->ptmp, 1, 0, (int)count, buf, nullptr);
+    }
     if (d->group) return hgroup_allreduce(d, buf, count);
     if (!d->comm) return 0;
     return ncclAllReduce(buf, buf, count, ncclFloat64, ncclSum, d->comm, d->stream) == ncclSuccess ? 0 : -4;
@@ -3943,8 +4024,8 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
             if (j > 0) {
                 const int in = (int)((j - 1) & 1), out = (int)(j & 1);
                 a.update = 1;
-                a.acc_in = d->atomic ? acc_slot(d, j - 1) : d->zacc;
-                a.R_in = d->atomic ? d->Rc : 1;
+                a.acc_in = d->atomic ? (d->peer_on ? zred_slot(d, j - 1) : acc_slot(d, j - 1)) : d->zacc;
+                a.R_in = d->atomic && !d->peer_on ? d->Rc : 1;
                 a.p_in = d->pbuf[in];
                 a.r_in = d->rbuf[in];
                 a.p_out = d->pbuf[out];
@@ -3961,7 +4042,10 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
             if (d->yc_on) a.yc = reinterpret_cast<float4 *>(d->yc);
             (j > 0 ? cg_iter_kernel(d, a) : d->k_fvp)(dim3(d->grid), d->k_lds, d->stream, a, d->net);
             int rc;
-            if (d->atomic) {
+            if (d->atomic && d->peer_on) {
+                // one exchange kernel: local replica sum pushed to every peer, rank-order sum -> zred
+                rc = trpo_peer_allreduce(d->peer, d->stream, acc_slot(d, j), d->Rc, d->Ps, d->Ps, zred_slot(d, j), done);
+            } else if (d->atomic) {
                 rc = allreduce(d, acc_slot(d, j), (size_t)RP);
             } else {
                 launch_reduce(d, done);
@@ -3972,7 +4056,8 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
         if (M > 0) {
             const int in = (int)((M - 1) & 1), out = (int)(M & 1);
             CG_DISPATCH(E, cg_update_kernel, dim3(1), dim3(1024), 0, d->stream,
-                        d->atomic ? acc_slot(d, M - 1) : d->zacc, d->atomic ? d->Rc : 1, d->pbuf[in], d->rbuf[in],
+                        d->atomic ? (d->peer_on ? zred_slot(d, M - 1) : acc_slot(d, M - 1)) : d->zacc,
+                        d->atomic && !d->peer_on ? d->Rc : 1, d->pbuf[in], d->rbuf[in],
                         d->pbuf[out], d->rbuf[out], x, d->P, d->nw, d->ctl, d->st + in, d->st + out, d->hist,
                         (const int *)nullptr, (void *)nullptr, 0, 0, d->reorth ? d->qbuf : nullptr,
                         (const void *)d->qzero, cg_step_nq(d, M - 1), d->Ps, d->atomic ? acc_slot(d, 0) : nullptr,
@@ -4155,7 +4240,7 @@ extern "C" int trpo_dev_sync(trpo_dev *d) {
     if (!d) return -1;
     HCHK(hipSetDevice(d->device));
     HCHK(hipStreamSynchronize(d->stream));
-    return 0;
+    return trpo_dev_comm_error(d);
 }
 
 // Kernel-only timing of the fused CG-iteration kernel K_j (j >= 1: CG step j-1 -> j in the prologue,

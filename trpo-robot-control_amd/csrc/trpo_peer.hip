@@ -1,0 +1,233 @@
+// trpo_peer.hip -- one-shot all-reduce of a small fp64 vector between the ranks of one node through
+// peer-mapped HBM windows over xGMI.  It carries the per-FVP exchange of the sharded CG
+// solve: the reference's CG (src/TRPO_CG.c:45-104) around the per-sample FVP loop
+// (src/TRPO_FVP.c:771-921), split over GPUs by samples, needs the P-sized partial sum of every rank
+// once per iteration.  RCCL's all-reduce does that in several protocol steps per message; for a
+// 4.6 KB vector one push into every peer and one flag per rank is the whole job.
+//
+// Every rank owns a WINDOW in its own HBM, allocated uncached (hipDeviceMallocUncached: remote
+// writes land in HBM and no L2 line of the window can go stale) and exported by IPC handle:
+//     data [2 sets][PEER_WMAX slots][S] fp64   |   flag [PEER_WMAX] u64 (one 128-B line each)
+// One exchange is ONE kernel of `world` workgroups on each rank.  Workgroup t of rank r:
+//   1. sums rank r's local replicas of the vector in replica order,
+//   2. stores the sum into slot r of set (e & 1) of rank t's window (over xGMI unless t == r),
+//   3. drains its stores, fences at system scope and stores the exchange number e into rank t's
+//      flag[r],
+//   4. waits (bounded poll) until flag[s] of its OWN window reads e for every rank s,
+//   5. sums slice t of the elements over the world slots in RANK order into the output vector.
+// Rank-order sums give every rank the same bits (like RCCL's all-reduce, and like the in-process
+// host group).  e = 1 + the exchanges workgroup t has done so far: a per-workgroup-index counter in
+// device memory, written only by that workgroup; every rank runs the same exchange sequence, so e
+// agrees across ranks and the flags only grow.  Two sets suffice: workgroup t of rank r can only
+// write set (e & 1) for exchange e + 2 after passing step 4 of exchange e + 1, i.e. after every rank
+// has STARTED exchange e + 1 -- and a rank starts a kernel only after its previous one (exchange e,
+// which read that set) has completed.
+// A poll that does not see its flag within 3 s sets an error word (pinned host memory) instead of
+// spinning forever; later exchanges then skip the wait (results invalid, but the GPU is released).
+#include <hip/hip_runtime.h>
+
+#include <stdlib.h>
+#include <string.h>
+
+#include "trpo_common.h"
+
+constexpr int PEER_T = 256;                  // threads per exchange workgroup
+constexpr int FLAG_STRIDE = 16;              // u64 words between flags (128 B)
+constexpr unsigned long long WAIT_TICKS = 300000000ULL;   // 3 s of the 100 MHz real-time counter
+
+struct trpo_peer {
+    int device;
+    size_t S;                        // slot length (fp64)
+    double *win;                     // own window (device)
+    double **dwins;                  // device array [world] of the windows as mapped in this process
+    void *opened[PEER_WMAX];         // IPC-opened peer windows (closed at destroy)
+    unsigned long long *cnt;         // [PEER_WMAX] per-workgroup exchange counters
+    int *err_h, *err_d;              // pinned host error word and its device view
+    int rank, world;
+    int uncached;                    // 1: hipDeviceMallocUncached, 0: fine-grained fallback
+};
+
+static size_t win_doubles(size_t S) { return 2 * (size_t)PEER_WMAX * S + (size_t)PEER_WMAX * FLAG_STRIDE; }
+
+// global (not flat) address space for the window accesses: the window pointers come from memory,
+// where the compiler cannot infer it, and flat operations also count in lgkmcnt
+typedef __attribute__((address_space(1))) double gdouble;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+__device__ __forceinline__ gdouble *gptr(const double *p) { return (gdouble *)(size_t)p; }
+__device__ __forceinline__ void st_sys(double *p, double v) {
+    __hip_atomic_store(gptr(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ double ld_sys(const double *p) {
+    return __hip_atomic_load(gptr(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void __launch_bounds__(PEER_T)
+peer_exchange_kernel(const double *__restrict__ in, int R, int Rstride, int count, double *const *wins, int rank,
+                     int world, int S, double *__restrict__ out, unsigned long long *cnt, int *err, const int *done) {
+    if (done && *done) return;                     // converged CG: every rank skips the same exchanges
+    const int t = blockIdx.x, tid = threadIdx.x;
+    const unsigned long long e = cnt[t] + 1;
+    const int set = (int)(e & 1);
+    // 1 + 2: local replica sum (replica order) pushed into slot `rank` of rank t's window
+    double *dst = wins[t] + ((size_t)set * PEER_WMAX + rank) * S;
+    for (int i = tid; i < count; i += PEER_T) {
+        double v = in[i];
+        for (int k = 1; k < R; ++k) v += in[(long)k * Rstride + i];
+        st_sys(dst + i, v);
+    }
+    // 3: every storing wave drained, then one system-scope release and the flag
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        gu64 *flag = (gu64 *)(size_t)(wins[t] + 2 * (size_t)PEER_WMAX * S);
+        __hip_atomic_store(flag + (size_t)rank * FLAG_STRIDE, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    // 4: every rank's flag in the own window
+    const double *own = wins[rank];
+    if (tid < world) {
+        gu64 *f = (gu64 *)(size_t)(own + 2 * (size_t)PEER_WMAX * S) + (size_t)tid * FLAG_STRIDE;
+        if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0) {
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < e) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > WAIT_TICKS) {
+                    __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    // 5: slice t of the elements, summed over the slots in rank order
+    const int per = (count + world - 1) / world, lo = t * per, hi = min(count, lo + per);
+    const double *src = own + (size_t)set * PEER_WMAX * S;
+    for (int i = lo + tid; i < hi; i += PEER_T) {
+        double s = ld_sys(src + i);
+        for (int r = 1; r < world; ++r) s += ld_sys(src + (size_t)r * S + i);
+        out[i] = s;
+    }
+    if (tid == 0) cnt[t] = e;
+}
+
+static void peer_free(trpo_peer *p) {
+    if (!p) return;
+    hipSetDevice(p->device);
+    for (int r = 0; r < PEER_WMAX; ++r)
+        if (p->opened[r]) hipIpcCloseMemHandle(p->opened[r]);
+    if (p->win) hipFree(p->win);
+    if (p->dwins) hipFree(p->dwins);
+    if (p->cnt) hipFree(p->cnt);
+    if (p->err_h) hipHostFree(p->err_h);
+    free(p);
+}
+
+trpo_peer *trpo_peer_create(int device, size_t S) {
+    trpo_peer *p = (trpo_peer *)calloc(1, sizeof(trpo_peer));
+    if (!p) return NULL;
+    p->device = device;
+    p->S = (S + 15) & ~(size_t)15;
+    p->world = 1;
+    if (hipSetDevice(device) != hipSuccess) {
+        free(p);
+        return NULL;
+    }
+    const size_t bytes = sizeof(double) * win_doubles(p->S);
+    p->uncached = 1;
+    if (hipExtMallocWithFlags((void **)&p->win, bytes, hipDeviceMallocUncached) != hipSuccess) {
+        (void)hipGetLastError();
+        p->uncached = 0;
+        p->win = NULL;
+        if (hipExtMallocWithFlags((void **)&p->win, bytes, hipDeviceMallocFinegrained) != hipSuccess) {
+            (void)hipGetLastError();
+            p->win = NULL;
+        }
+    }
+    bool ok = p->win && hipMemset(p->win, 0, bytes) == hipSuccess &&
+              hipMalloc((void **)&p->dwins, sizeof(double *) * PEER_WMAX) == hipSuccess &&
+              hipMalloc((void **)&p->cnt, sizeof(unsigned long long) * PEER_WMAX) == hipSuccess &&
+              hipMemset(p->cnt, 0, sizeof(unsigned long long) * PEER_WMAX) == hipSuccess &&
+              hipHostMalloc((void **)&p->err_h, sizeof(int), hipHostMallocMapped) == hipSuccess;
+    if (ok) {
+        *p->err_h = 0;
+        ok = hipHostGetDevicePointer((void **)&p->err_d, p->err_h, 0) == hipSuccess &&
+             hipDeviceSynchronize() == hipSuccess;
+    }
+    if (!ok) {
+        (void)hipGetLastError();
+        peer_free(p);
+        return NULL;
+    }
+    return p;
+}
+
+void trpo_peer_destroy(trpo_peer *p) { peer_free(p); }
+
+int trpo_peer_handle(trpo_peer *p, void *h64) {
+    if (!p || !h64) return -1;
+    hipIpcMemHandle_t h;
+    static_assert(sizeof(h) <= PEER_HANDLE_BYTES, "IPC handle size");
+    HCHK(hipSetDevice(p->device));
+    HCHK(hipIpcGetMemHandle(&h, p->win));
+    memset(h64, 0, PEER_HANDLE_BYTES);
+    memcpy(h64, &h, sizeof h);
+    return 0;
+}
+
+void *trpo_peer_window(trpo_peer *p) { return p ? p->win : NULL; }
+
+// handles: world x PEER_HANDLE_BYTES (rank order; the own entry is ignored), or
+// local: world window pointers of contexts in this process (rank order)
+int trpo_peer_connect(trpo_peer *p, int rank, int world, const void *handles, void *const *local) {
+    if (!p || world < 1 || world > PEER_WMAX || rank < 0 || rank >= world || (!handles && !local)) return -1;
+    HCHK(hipSetDevice(p->device));
+    double *w[PEER_WMAX] = {NULL};
+    for (int r = 0; r < world; ++r) {
+        if (r == rank) {
+            w[r] = p->win;
+        } else if (local) {
+            w[r] = (double *)local[r];
+        } else {
+            if (p->opened[r]) {
+                hipIpcCloseMemHandle(p->opened[r]);
+                p->opened[r] = NULL;
+            }
+            hipIpcMemHandle_t h;
+            memcpy(&h, (const char *)handles + (size_t)r * PEER_HANDLE_BYTES, sizeof h);
+            void *q = NULL;
+            const hipError_t e = hipIpcOpenMemHandle(&q, h, hipIpcMemLazyEnablePeerAccess);
+            if (e != hipSuccess) {
+                fprintf(stderr, "[trpo_mi355x] hipIpcOpenMemHandle(rank %d of %d, from rank %d): %s\n", r, world,
+                        rank, hipGetErrorString(e));
+                (void)hipGetLastError();
+                return -4;
+            }
+            p->opened[r] = q;
+            w[r] = (double *)q;
+        }
+        if (!w[r]) return -1;
+    }
+    HCHK(hipMemcpy(p->dwins, w, sizeof(double *) * world, hipMemcpyHostToDevice));
+    __atomic_store_n(p->err_h, 0, __ATOMIC_RELEASE);     // a new attach starts without a timed-out exchange
+    p->rank = rank;
+    p->world = world;
+    return 0;
+}
+
+// out[i] = sum over ranks (rank order) of sum_{k < R} in[k * Rstride + i], i < count; out != in.
+// done (device, may be NULL): skip the exchange when *done (every rank reads the same flag value).
+int trpo_peer_allreduce(trpo_peer *p, hipStream_t st, const double *in, int R, int Rstride, int count, double *out,
+                        const int *done) {
+    if (!p || count < 0 || (size_t)count > p->S || R < 1 || in == out) return -1;
+    if (count == 0) return 0;
+    hipLaunchKernelGGL(peer_exchange_kernel, dim3(p->world), dim3(PEER_T), 0, st, in, R, Rstride, count, p->dwins,
+                       p->rank, p->world, (int)p->S, out, p->cnt, p->err_d, done);
+    HCHK(hipGetLastError());
+    return 0;
+}
+
+int trpo_peer_error(const trpo_peer *p) { return p && p->err_h ? __atomic_load_n(p->err_h, __ATOMIC_ACQUIRE) : 0; }
+size_t trpo_peer_slot(const trpo_peer *p) { return p ? p->S : 0; }
+int trpo_peer_uncached(const trpo_peer *p) { return p ? p->uncached : 0; }

@@ -99,6 +99,14 @@ def lib():
     L.trpo_ctx_attach_group.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
     L.trpo_ctx_comm_info.restype = C.c_int
     L.trpo_ctx_comm_info.argtypes = [C.c_void_p, P(C.c_int), P(C.c_int), P(C.c_int)]
+    L.trpo_ctx_peer_handle.restype = C.c_int
+    L.trpo_ctx_peer_handle.argtypes = [C.c_void_p, C.c_char_p]
+    L.trpo_ctx_attach_peers.restype = C.c_int
+    L.trpo_ctx_attach_peers.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_char_p]
+    L.trpo_ctx_attach_peers_local.restype = C.c_int
+    L.trpo_ctx_attach_peers_local.argtypes = [C.c_void_p, C.c_int, C.c_int, P(C.c_void_p)]
+    L.trpo_ctx_comm_backend.restype = C.c_char_p
+    L.trpo_ctx_comm_backend.argtypes = [C.c_void_p]
     L.trpo_ctx_fvp.restype = C.c_double
     L.trpo_ctx_fvp.argtypes = [C.c_void_p, _dp, _dp]
     L.trpo_ctx_cg.restype = C.c_double
@@ -142,6 +150,7 @@ def lib():
 
 
 MAX_BACKTRACKS = 32
+PEER_HANDLE_BYTES = 64      # include/trpo_mi355x.h TRPO_PEER_HANDLE_BYTES
 
 
 class TRPOBaselineParam(C.Structure):
@@ -379,11 +388,35 @@ class Context:
         """Join an in-process host group as `rank` (call concurrently from one thread per rank)."""
         self._chk(lib().trpo_ctx_attach_group(self._h, group._h, rank), "attach_group")
 
+    def peer_handle(self) -> bytes:
+        """Open this rank's peer exchange window; returns its exported handle (PEER_HANDLE_BYTES)."""
+        buf = C.create_string_buffer(PEER_HANDLE_BYTES)
+        self._chk(lib().trpo_ctx_peer_handle(self._h, buf), "peer_handle")
+        return buf.raw
+
+    def attach_peers(self, rank: int, world: int, handles):
+        """Attach the peer-window exchange (every rank concurrently): handles = the world's
+        peer_handle() bytes in rank order."""
+        blob = b"".join(bytes(h) for h in handles)
+        if len(blob) != world * PEER_HANDLE_BYTES:
+            raise ValueError("need %d handles of %d bytes" % (world, PEER_HANDLE_BYTES))
+        self._chk(lib().trpo_ctx_attach_peers(self._h, rank, world, blob), "attach_peers")
+
+    def attach_peers_local(self, rank: int, ctxs):
+        """In-process peer exchange: ctxs = the contexts of all ranks in rank order, each with an open
+        window (peer_handle()); call concurrently, one thread per rank."""
+        arr = (C.c_void_p * len(ctxs))(*[c._h for c in ctxs])
+        self._chk(lib().trpo_ctx_attach_peers_local(self._h, rank, len(ctxs), arr), "attach_peers_local")
+
+    @property
+    def comm_backend(self) -> str:
+        return lib().trpo_ctx_comm_backend(self._h).decode()
+
     def comm_info(self):
-        """dict(rank, world, replicas): the communicator as the collective library reports it."""
+        """dict(rank, world, replicas, backend): the communicator as the collective library reports it."""
         r, w, rep = C.c_int(0), C.c_int(0), C.c_int(0)
         self._chk(lib().trpo_ctx_comm_info(self._h, C.byref(r), C.byref(w), C.byref(rep)), "comm_info")
-        return dict(rank=r.value, world=w.value, replicas=rep.value)
+        return dict(rank=r.value, world=w.value, replicas=rep.value, backend=self.comm_backend)
 
     def fvp(self, v):
         out = np.zeros(self.P)
