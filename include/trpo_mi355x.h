@@ -209,6 +209,10 @@ int trpo_ctx_set_rollout(trpo_ctx *ctx, const double *mean, const double *action
 double trpo_ctx_update(trpo_ctx *ctx, size_t cg_max_iter, double cg_residual_th, double max_kl,
                        int max_backtracks, double accept_ratio, double *theta_out, double *b_out,
                        double *x_out, trpo_update_info *info, int verbose);
+/* The line search's surrogate sums (src/TRPO_Update.c:951-981) on their own: surr[j] =
+ * sum over ALL ranks' samples of Adv exp(LLD) at theta + 0.5^(k0 + j) fullstep, j < nk (nk <= 64),
+ * for the context's current theta and rollout. */
+int trpo_ctx_surrogate(trpo_ctx *ctx, const double *fullstep, int k0, int nk, double *surr);
 
 /* Value-baseline context: data uploaded once per fit, then one device evaluation per L-BFGS
  * callback.  layer_size[0] = observation dim + 1 (the time feature). */

@@ -178,9 +178,9 @@ def test_output_widths_and_activations_against_oracle(layers, acts):
 @pytest.mark.parametrize("layers", [[15, 32, 32, 3], [20, 32, 32, 2], [30, 64, 64, 4], [15, 64, 64, 3]])
 @pytest.mark.parametrize("mode", ["fused", "unfused", "off"])
 def test_cooperative_kernel_shapes_against_oracle(layers, mode, monkeypatch):
-    """Wide hidden layers run the cooperative tile kernel, by default with the CG step fused into
-    its prologue (TRPO_COOP_FUSED=0: separate cg_update kernel; TRPO_COOP=0: the one-wave-per-tile
-    kernel); FVP, CG and the policy gradient against the oracle."""
+    """Wide hidden layers run the cooperative tile kernel (fp32: the CG step distributed over slices,
+    cg_dots + cg_axpy); TRPO_COOP_FUSED=0 / TRPO_COOP=0 select the older step placements and the
+    one-wave-per-tile kernel; FVP, CG and the policy gradient against the oracle."""
     import oracle
     from trpo_amd import synth
     coop = "0" if mode == "off" else "1"

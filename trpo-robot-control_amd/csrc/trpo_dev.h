@@ -72,9 +72,10 @@ int trpo_dev_surrogate(trpo_dev *d, const double *fullstep, int k0, int nk, doub
  * pinned host memory. */
 int trpo_dev_update_solve(trpo_dev *d, size_t maxiter, double resth, double *b, double *x, double *z,
                           double *adv_sum, size_t *iters, double *rdotr_hist, double *xnorm_hist,
-                          double max_kl, double *surr0);
-/* surr0 (optional): also the step size (host arithmetic, bit for bit) and the surrogate sum of the full
- * step theta + fullstep, the line search's first candidate, in the same synchronisation. */
+                          double max_kl, double *surr0, double *shs_lm);
+/* shs_lm (optional, 2): the step size shs = 0.5 x.Fx and lm = sqrt(shs / max_kl) as the device computed
+ * them (fullstep = x / lm, fixed-order sum); surr0 (optional): the surrogate sum of the full step
+ * theta + fullstep, the line search's first candidate, in the same synchronisation. */
 
 /* Value-baseline objective (src/TRPO_Baseline.c), its own small device object. */
 typedef struct trpo_bdev trpo_bdev;

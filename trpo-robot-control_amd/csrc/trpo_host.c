@@ -199,6 +199,17 @@ int trpo_ctx_attach_peers_local(trpo_ctx *c, int rank, int world, trpo_ctx *cons
 }
 const char *trpo_ctx_comm_backend(const trpo_ctx *c) { return c ? trpo_dev_comm_backend(c->dev) : ""; }
 
+int trpo_ctx_surrogate(trpo_ctx *c, const double *fullstep, int k0, int nk, double *surr) {
+    if (!c || !fullstep || !surr || k0 < 0 || nk < 1 || nk > 64) return TRPO_E_INVALID;
+    if (!c->have_roll) {
+        set_err("surrogate: no rollout uploaded for the current samples (trpo_ctx_set_rollout)");
+        return TRPO_E_INVALID;
+    }
+    const int rc = trpo_dev_surrogate(c->dev, fullstep, k0, nk, surr);
+    if (rc) set_err("surrogate failed on the device (code %d)", rc);
+    return rc;
+}
+
 double trpo_ctx_fvp(trpo_ctx *c, const double *v, double *out) {
     if (!c || !v || !out) return TRPO_E_INVALID;
     const double t0 = now_s();
@@ -269,14 +280,14 @@ double trpo_ctx_update(trpo_ctx *c, size_t max_iter, double resth, double max_kl
     double ret = TRPO_E_NOMEM;
     if (!b || !x || !z || !fullstep) goto out;
     const double t0 = now_s();
-    double adv_sum = 0.0, surr0 = 0.0;
+    double adv_sum = 0.0, surr0 = 0.0, shs_lm[2] = {0.0, 0.0};
     /* policy gradient (:254-378), CG (:383-628) and FVP(x) (:633-832) on the device, one sync */
     double *rr = verbose ? (double *)malloc(sizeof(double) * (max_iter + 1)) : NULL;
     double *xn = verbose ? (double *)malloc(sizeof(double) * (max_iter + 1)) : NULL;
     int rc = (verbose && (!rr || !xn)) ? TRPO_E_NOMEM
                                        : trpo_dev_update_solve(c->dev, max_iter, resth, b, x, z, &adv_sum,
                                                                &inf.cg_iters, rr, xn, max_kl,
-                                                               max_bt > 0 ? &surr0 : NULL);
+                                                               max_bt > 0 ? &surr0 : NULL, shs_lm);
     if (!rc && verbose) /* src/TRPO_CG.c:56 -- one line per iteration */
         for (size_t i = 0; i <= inf.cg_iters && i <= max_iter; ++i)
             printf("CG Iter[%zu] Residual Norm=%.12e, Soln Norm=%.12e\n", i, rr[i], xn[i]);
@@ -288,11 +299,11 @@ double trpo_ctx_update(trpo_ctx *c, size_t max_iter, double resth, double max_kl
         goto out;
     }
     /* step size (src/TRPO_Update.c:834-868), fp64 on the host, reference order */
-    double shs = 0;
-    for (size_t i = 0; i < P; ++i) shs += z[i] * x[i];
-    shs = shs * 0.5;
+    /* shs = 0.5 x.Fx and lm = sqrt(shs / max_kl) (:836-846) as the device summed them: its fullstep
+     * x / lm -- the first line-search candidate it already evaluated -- is the one below, bit for bit */
+    const double shs = shs_lm[0];
     if (verbose) printf("shs: %.14f\n", shs);
-    const double lm = sqrt(shs / max_kl);
+    const double lm = shs_lm[1];
     double gnorm = 0;
     for (size_t i = 0; i < P; ++i) gnorm += b[i] * b[i];
     gnorm = sqrt(gnorm);

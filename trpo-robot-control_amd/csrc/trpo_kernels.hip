@@ -2675,10 +2675,29 @@ cg_axpy_kernel(const double *__restrict__ dots, int G, const double *__restrict_
     const QT *qz = reinterpret_cast<const QT *>(qz_v);
     const int tid = threadIdx.x, t = blockIdx.x * CGS_T + tid;
     const int tc = min(t, (Ps >> 1) - 1);
-    // the partial dots of every block, summed in block order by thread k (value k)
-    double part = 0.0;
-    if (tid < CGS_K) {
-        for (int b = 0; b < G; ++b) part += dots[(long)b * CGS_K + tid];
+    // the partial dots of the G producer blocks: wave w sums values k = w, w + 4, ...; lane l takes
+    // partials l, l + 64, l + 128, l + 192 (all loads issued together, unconditional), then the
+    // fixed-order wave tree (a serial chain of G dependent loads by one thread was measured ~100 us
+    // at G = 176 partials)
+    constexpr int NW = CGS_T / 64, NI = (CGS_K + NW - 1) / NW, NJ = 4;
+    const int lane = tid & 63, w = tid >> 6;
+    double pv_[NI];
+    {
+        double v[NI][NJ];
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int k = w + NW * i, b = lane + 64 * j;
+                const double d = dots[(long)min(b, G - 1) * CGS_K + min(k, CGS_K - 1)];
+                v[i][j] = (k < CGS_K && b < G) ? d : 0.0;
+            }
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            double a = (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
+            for (int b = lane + 64 * NJ; b < G; b += 64) a += dots[(long)b * CGS_K + min(w + NW * i, CGS_K - 1)];
+            pv_[i] = wave_tree_sum(a);
+        }
     }
     const double2 p2 = reinterpret_cast<const double2 *>(p_in)[tc], r2 = reinterpret_cast<const double2 *>(r_in)[tc];
     const double2 x2 = reinterpret_cast<const double2 *>(x)[tc], z2 = reinterpret_cast<const double2 *>(zbuf)[tc];
@@ -2697,7 +2716,11 @@ cg_axpy_kernel(const double *__restrict__ dots, int G, const double *__restrict_
     const double cth = ctl->resth;
     const int cmax = ctl->maxiter;
     if (*skip) return;                                    // grid-uniform
-    if (tid < CGS_K) tot[tid] = part;
+    if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+            if (w + NW * i < CGS_K) tot[w + NW * i] = pv_[i];
+    }
     __syncthreads();
     const double pz = tot[0], rz = tot[1], zz = tot[2], xp = tot[3], pp = tot[4];
     const double alpha = sin.rdotr / pz;
@@ -4074,11 +4097,11 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
             a.v_nat = d->pbuf[cur];
             if (d->yc_on) a.yc = reinterpret_cast<float4 *>(d->yc);
             (j > 0 && d->yc_on ? d->k_fvp_yc : d->k_fvp)(dim3(d->grid), d->k_lds, d->stream, a, d->net);
+            const int nq = cg_step_nq(d, j);
+            void *qb = d->reorth ? d->qbuf : (void *)d->qzero;
             launch_reduce(d, done);
             int rc = allreduce(d, d->zacc, d->nw);
             if (rc) return rc;
-            const int nq = cg_step_nq(d, j);
-            void *qb = d->reorth ? d->qbuf : (void *)d->qzero;
             if (d->f64) {
                 hipLaunchKernelGGL(cg_dots_kernel<double>, dim3(G), dim3(CGS_T), 0, d->stream, d->zacc, d->pbuf[cur],
                                    d->rbuf[cur], x, d->zbuf, d->dotsbuf, (const void *)qb, (const void *)d->qzero,

@@ -471,6 +471,200 @@ pg_logstd_kernel(const double *__restrict__ th, int P, int A, const double *__re
 }
 
 // ---------------------------------------------------------------------------
+// Line-search surrogate on the fp64 MFMA (v_mfma_f64_16x16x4_f64) for 3-weight-layer policies with
+// wide hidden layers (the 2x64 MLPs; src/TRPO_Update.c:951-981).  One wave per 16-sample tile,
+// neurons on the MFMA rows and samples on the columns: a layer is acc = B (bias rows) + W^T y, and
+// for the fp64 instruction lane (c, g) register r of the accumulator holds neuron g + 4r of sample c
+// -- which is exactly the B operand of k-step r of the next layer, so activations never leave the
+// registers.  Input neuron of k-step ks (of a 16-wide input tile kt) at lane group g: 16kt + g + 4r,
+// r = ks % 4; the candidate's weights are packed in that fragment order (surr_pack_kernel) and
+// staged in LDS once per workgroup (lane-contiguous fp64 reads).  Per sample the log-likelihood
+// terms of outputs i = g + 4r are gathered to the lane group g = 0 in ascending i, exp(0.5 LLD)
+// Adv is accumulated per lane, then the wave tree and the waves in order (fixed-order sums).  The
+// dot products round differently from the one-lane-per-sample kernel (MFMA accumulation order);
+// the sums agree to ~1e-16 relative.
+// ---------------------------------------------------------------------------
+static int ensure(double **p, size_t *cap, size_t count, hipStream_t st);
+typedef double sd4 __attribute__((ext_vector_type(4)));
+constexpr int SM_WAVES = 8;
+template <int T0, int T1, int T2>
+struct SurrCfg {
+    static constexpr int F1 = 0;                             // W1 fragments [T1][4 T0][64]
+    static constexpr int F2 = F1 + T1 * 4 * T0 * 64;         // W2 [T2][4 T1][64]
+    static constexpr int F3 = F2 + T2 * 4 * T1 * 64;         // W3 [1][4 T2][64]
+    static constexpr int B1 = F3 + 4 * T2 * 64;              // biases [16 T1], [16 T2], [16]
+    static constexpr int B2 = B1 + 16 * T1;
+    static constexpr int B3 = B2 + 16 * T2;
+    static constexpr int LS = B3 + 16;                       // LogStd [16]
+    static constexpr int LEN = LS + 16;
+};
+
+// natural parameter index of pack element e (-1: zero padding)
+template <int T0, int T1, int T2>
+__device__ int surr_pack_map(const Net &net, int e) {
+    using C = SurrCfg<T0, T1, T2>;
+    int lo, nks, layer;
+    if (e < C::F2) {
+        lo = C::F1, nks = 4 * T0, layer = 0;
+    } else if (e < C::F3) {
+        lo = C::F2, nks = 4 * T1, layer = 1;
+    } else if (e < C::B1) {
+        lo = C::F3, nks = 4 * T2, layer = 2;
+    } else {
+        const int A = net.A;
+        if (e < C::B2) return e - C::B1 < net.L[1] ? net.boff[0] + e - C::B1 : -1;
+        if (e < C::B3) return e - C::B2 < net.L[2] ? net.boff[1] + e - C::B2 : -1;
+        if (e < C::LS) return e - C::B3 < A ? net.boff[2] + e - C::B3 : -1;
+        return e - C::LS < A ? net.P - A + e - C::LS : -1;
+    }
+    const int local = e - lo, lane = local & 63, frag = local >> 6;
+    const int ot = frag / nks, ks = frag % nks, c = lane & 15, g = lane >> 4;
+    const int in = 16 * (ks >> 2) + g + 4 * (ks & 3), out = 16 * ot + c;
+    const int L_in = net.L[layer], L_out = net.L[layer + 1];
+    return (in < L_in && out < L_out) ? net.woff[layer] + in * L_out + out : -1;
+}
+
+// the nk candidates theta + 2^-(k0+k) fullstep in fragment order, [nk][LEN] (fs == nullptr: theta)
+template <int T0, int T1, int T2>
+__global__ void surr_pack_kernel(Net net, const double *__restrict__ th, const double *__restrict__ fs, int k0,
+                                 double *__restrict__ out) {
+    using C = SurrCfg<T0, T1, T2>;
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= C::LEN) return;
+    const int m = surr_pack_map<T0, T1, T2>(net, e);
+    const ThetaStep T{th, fs, ldexp(1.0, -(k0 + (int)blockIdx.y))};
+    out[(long)blockIdx.y * C::LEN + e] = m < 0 ? 0.0 : (fs ? T[m] : th[m]);
+}
+
+__device__ __forceinline__ sd4 act4_64(int a, sd4 x) {
+    sd4 y;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) y[r] = act_y64(a, x[r]);
+    return y;
+}
+
+template <int T0, int T1, int T2>
+__global__ void __launch_bounds__(64 * SM_WAVES)
+surr_mfma_kernel(Net net, const double *__restrict__ pk, const double *__restrict__ obs,
+                 const double *__restrict__ roll, const double *__restrict__ stdv, int n,
+                 double *__restrict__ parts) {
+    using C = SurrCfg<T0, T1, T2>;
+    __shared__ __attribute__((aligned(16))) double spl[C::LEN];
+    __shared__ double wsum[SM_WAVES];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, c = lane & 15, g = lane >> 4;
+    const int k = blockIdx.y, nk = gridDim.y;
+    static_assert(C::LEN % 2 == 0, "pack length");
+    {
+        const double2 *src = reinterpret_cast<const double2 *>(pk + (long)k * C::LEN);
+        double2 *dst = reinterpret_cast<double2 *>(spl);
+        for (int e = tid; e < C::LEN / 2; e += 64 * SM_WAVES) dst[e] = src[e];
+    }
+    __syncthreads();
+    const int L0 = net.L[0], A = net.A, W = 2 * A + 1;
+    const int a1 = net.act[1], a2 = net.act[2], a3 = net.act[3];
+    const int ntiles = (n + 15) / 16, nwaves = gridDim.x * SM_WAVES;
+    double acc = 0.0;
+    for (int tile = blockIdx.x * SM_WAVES + wave; tile < ntiles; tile += nwaves) {
+        const int s = tile * 16 + c;
+        const bool live = s < n;
+        const long sc = live ? s : 0;
+        // an opaque base per trip: keeps the compiler from hoisting all the (loop-invariant) weight
+        // fragment reads out of the loop into ~200 registers
+        int wb = 0;
+        asm volatile("" : "+v"(wb));
+        const double *sp = spl + wb;
+        double x0[4 * T0];
+#pragma unroll
+        for (int ks = 0; ks < 4 * T0; ++ks) {
+            const int in = 16 * (ks >> 2) + g + 4 * (ks & 3);
+            x0[ks] = (live && in < L0) ? obs[sc * L0 + in] : 0.0;
+        }
+        sd4 y1[T1], y2[T2];
+#pragma unroll
+        for (int ot = 0; ot < T1; ++ot) {
+            sd4 a;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) a[r] = sp[C::B1 + 16 * ot + g + 4 * r];
+#pragma unroll
+            for (int ks = 0; ks < 4 * T0; ++ks)
+                a = __builtin_amdgcn_mfma_f64_16x16x4f64(sp[C::F1 + (ot * 4 * T0 + ks) * 64 + lane], x0[ks], a, 0, 0, 0);
+            y1[ot] = act4_64(a1, a);
+        }
+#pragma unroll
+        for (int ot = 0; ot < T2; ++ot) {
+            sd4 a;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) a[r] = sp[C::B2 + 16 * ot + g + 4 * r];
+#pragma unroll
+            for (int kt = 0; kt < T1; ++kt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    a = __builtin_amdgcn_mfma_f64_16x16x4f64(sp[C::F2 + (ot * 4 * T1 + 4 * kt + r) * 64 + lane],
+                                                             y1[kt][r], a, 0, 0, 0);
+            y2[ot] = act4_64(a2, a);
+        }
+        sd4 m;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) m[r] = sp[C::B3 + g + 4 * r];
+#pragma unroll
+        for (int kt = 0; kt < T2; ++kt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                m = __builtin_amdgcn_mfma_f64_16x16x4f64(sp[C::F3 + (4 * kt + r) * 64 + lane], y2[kt][r], m, 0, 0, 0);
+        m = act4_64(a3, m);
+        // log-likelihood terms of outputs i = g + 4r (src/TRPO_Update.c:956-976), summed in ascending i
+        const double *rw = roll + sc * W;
+        double term[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = g + 4 * r;
+            term[r] = (live && i < A) ? lld_term(rw, A, i, m[r], sp[C::LS + i], stdv[i]) : 0.0;
+        }
+        double lld = 0.0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int gg = 0; gg < 4; ++gg)
+                if (gg + 4 * r < A) lld += __shfl(term[r], c + 16 * gg, 64);
+        lld = lld * 0.5;
+        if (g == 0 && live) acc += exp(lld) * rw[2 * A];
+    }
+    for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if (lane == 0) wsum[wave] = acc;
+    __syncthreads();
+    if (tid == 0) {
+        double t = 0.0;
+        for (int w = 0; w < SM_WAVES; ++w) t += wsum[w];
+        parts[(long)blockIdx.x * nk + k] = t;
+    }
+}
+
+// the MFMA surrogate's shape: 3 weight layers, inputs <= 32, hidden widths 17..64 (tiles of 16),
+// <= 16 outputs; returns the instantiation index or -1
+static int surr_mfma_shape(const Net &net) {
+    const char *e = getenv("TRPO_SURR_GENERIC");
+    if (e && atoi(e)) return -1;
+    if (net.nl != 4 || net.L[0] > 32 || net.L[3] > 16 || net.L[1] > 64 || net.L[2] > 64) return -1;
+    const int T0 = cdiv(net.L[0], 16), T1 = cdiv(net.L[1], 16), T2 = cdiv(net.L[2], 16);
+    if (T1 != T2 || T1 < 2) return -1;
+    return (T0 - 1) * 3 + (T1 - 2);      // T0 in {1, 2}, T1 = T2 in {2, 3, 4}
+}
+
+template <int T0, int T1>
+static int launch_surr_mfma(const Net &net, const double *th, const double *fs, int k0, int nk, double **pk,
+                            size_t *pk_cap, const double *obs, const double *roll, const double *stdv, int n, int G,
+                            double *parts, hipStream_t st) {
+    using C = SurrCfg<T0, T1, T1>;
+    if (ensure(pk, pk_cap, (size_t)C::LEN * nk, st)) return -2;
+    hipLaunchKernelGGL((surr_pack_kernel<T0, T1, T1>), dim3(cdiv(C::LEN, 256), nk), dim3(256), 0, st, net, th, fs, k0,
+                       *pk);
+    hipLaunchKernelGGL((surr_mfma_kernel<T0, T1, T1>), dim3(G, nk), dim3(64 * SM_WAVES), 0, st, net,
+                       (const double *)*pk, obs, roll, stdv, n, parts);
+    HCHK(hipGetLastError());
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
 // device-layer entry points (trpo_dev.h)
 // ---------------------------------------------------------------------------
 static UpdState *state(trpo_dev *d) {
@@ -522,37 +716,33 @@ __global__ void export_solve_kernel(const double *__restrict__ b, const double *
 // Step size of src/TRPO_Update.c:834-868 on the device, in the host code's exact arithmetic
 // (sequential, unfused fp64: the host recomputes the same values from b, x, z bit for bit):
 // shs = 0.5 sum z_i x_i, lm = sqrt(shs / max_kl), fullstep = x / lm
-constexpr int STEP_CHUNK = 4096;                 // products staged in LDS per round
-__global__ void step_kernel(const double *__restrict__ x, const double *__restrict__ z, int P, double max_kl,
-                            double *__restrict__ fs) {
+// Step size of the update (src/TRPO_Update.c:836-846): shs = 0.5 x.Fx, lm = sqrt(shs / max_kl),
+// fullstep = x / lm.  One 1024-thread workgroup: strided per-thread partial sums, then the wave tree
+// and the waves in order (a fixed order, so every call gives the same bits); shs and lm go to the
+// host with the solve's results and the host uses them as they are, so its fullstep x[i] / lm is the
+// device's bit for bit (the first line-search candidate is evaluated on the device with it).
+constexpr int STEP_T = 1024;
+__global__ void __launch_bounds__(STEP_T)
+step_kernel(const double *__restrict__ x, const double *__restrict__ z, int P, double max_kl,
+            double *__restrict__ fs, double *__restrict__ shs_lm) {
+    __shared__ double wpart[STEP_T / 64];
     __shared__ double lm_s;
-    __shared__ double prod[STEP_CHUNK];
-    // per chunk: the products in parallel (each correctly rounded, as the host's z[i] * x[i]), then
-    // ONE thread adds them in index order (the host's order) out of LDS, 16 loads ahead of the adds
-    double shs = 0.0;
-    for (int c0 = 0; c0 < P; c0 += STEP_CHUNK) {
-        const int len = P - c0 < STEP_CHUNK ? P - c0 : STEP_CHUNK;
-        for (int i = threadIdx.x; i < len; i += blockDim.x) prod[i] = __dmul_rn(z[c0 + i], x[c0 + i]);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            int i = 0;
-            for (; i + 16 <= len; i += 16) {
-                double t[16];
-#pragma unroll
-                for (int j = 0; j < 16; ++j) t[j] = prod[i + j];
-#pragma unroll
-                for (int j = 0; j < 16; ++j) shs = __dadd_rn(shs, t[j]);
-            }
-            for (; i < len; ++i) shs = __dadd_rn(shs, prod[i]);
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        shs = __dmul_rn(shs, 0.5);
-        lm_s = sqrt(__ddiv_rn(shs, max_kl));
+    const int tid = threadIdx.x;
+    double acc = 0.0;
+    for (int i = tid; i < P; i += STEP_T) acc += z[i] * x[i];
+    for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if ((tid & 63) == 0) wpart[tid >> 6] = acc;
+    __syncthreads();
+    if (tid == 0) {
+        double t = 0.0;
+        for (int w = 0; w < STEP_T / 64; ++w) t += wpart[w];
+        const double shs = t * 0.5, lm = sqrt(shs / max_kl);
+        lm_s = lm;
+        shs_lm[0] = shs;
+        shs_lm[1] = lm;
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < P; i += blockDim.x) fs[i] = __ddiv_rn(x[i], lm_s);
+    for (int i = tid; i < P; i += STEP_T) fs[i] = x[i] / lm_s;
 }
 
 // small vector copies to / from the mapped host buffer by a kernel (no copy-engine latency)
@@ -701,11 +891,11 @@ static int enqueue_update_device(trpo_dev *d, size_t maxiter, double resth, doub
     if (rc) return rc;
     UpdState *u = state(d);
     const int P = v.net.P, H = 2 * ((int)maxiter + 1);
+    // the step size (-> mapped host buffer) and, with surr, the full-step surrogate (the usual outcome
+    // of the line search) in the same submission: no host round trip before the first candidate
+    hipLaunchKernelGGL(step_kernel, dim3(1), dim3(STEP_T), 0, v.stream, (const double *)v.vec_x,
+                       (const double *)v.vec_z, P, max_kl, u->fs, u->hst_dev + 3 * P + 3 + H);
     if (surr) {
-        // the step size and the full-step surrogate (the usual outcome of the line search) in the same
-        // submission: no host round trip between the solve and the first line-search candidate
-        hipLaunchKernelGGL(step_kernel, dim3(1), dim3(256), 0, v.stream, (const double *)v.vec_x,
-                           (const double *)v.vec_z, P, max_kl, u->fs);
         rc = enqueue_surrogate(d, u->fs, 0, 1);
         if (rc) return rc;
         hipLaunchKernelGGL(copy64_kernel, dim3(1), dim3(64), 0, v.stream, (const double *)u->sums,
@@ -719,7 +909,7 @@ static int enqueue_update_device(trpo_dev *d, size_t maxiter, double resth, doub
 
 extern "C" int trpo_dev_update_solve(trpo_dev *d, size_t maxiter, double resth, double *b, double *x, double *z,
                                      double *adv_sum, size_t *iters, double *rdotr_hist, double *xnorm_hist,
-                                     double max_kl, double *surr0) {
+                                     double max_kl, double *surr0, double *shs_lm) {
     if (!d || !b || !x || !z || !adv_sum || maxiter > 100000) return -1;
     trpo_dev_view v;
     trpo_dev_get_view(d, &v);
@@ -730,7 +920,7 @@ extern "C" int trpo_dev_update_solve(trpo_dev *d, size_t maxiter, double resth, 
     const size_t bytes = sizeof(double) * P;
     const bool surr = surr0 != nullptr;
     // outside any graph: buffers, and the rollout rows of the policy-gradient kernel (new rollout only)
-    if (ensure_host(u, (size_t)3 * P + 3 + H)) return -2;
+    if (ensure_host(u, (size_t)3 * P + 5 + H)) return -2;
     if (!u->fs) HCHK(hipMalloc((void **)&u->fs, sizeof(double) * P));
     if (trpo_dev_pg_prepare(d, u->roll, u->roll_gen) < 0) return -2;
     // (capturing this whole sequence into one graph was measured: ~3 % faster per update, ~10 ms to
@@ -739,6 +929,10 @@ extern "C" int trpo_dev_update_solve(trpo_dev *d, size_t maxiter, double resth, 
     if (rc) return rc;
     HCHK(hipStreamSynchronize(v.stream));
     if (surr0) *surr0 = u->hst[3 * P + 2 + H];
+    if (shs_lm) {
+        shs_lm[0] = u->hst[3 * P + 3 + H];
+        shs_lm[1] = u->hst[3 * P + 4 + H];
+    }
     const double *h = u->hst;
     memcpy(b, h, bytes);
     memcpy(x, h + P, bytes);
@@ -766,6 +960,26 @@ static int enqueue_surrogate(trpo_dev *d, const double *fs, int k0, int nk) {
     const int Gs = n ? (cdiv(n, UT) < cap ? cdiv(n, UT) : cap) : 1;
     if (ensure(&u->slabs, &u->slab_cap, (size_t)Gs * nk, v.stream)) return -2;
     if (!u->sums) HCHK(hipMalloc((void **)&u->sums, sizeof(double) * 64));
+    const int ms = surr_mfma_shape(net);
+    if (ms >= 0) {
+        // one wave per 16-sample tile, SM_WAVES per workgroup
+        const int cap2 = 512 / nk > 0 ? 512 / nk : 1, Gm = n ? (cdiv(cdiv(n, 16), SM_WAVES) < cap2 ? cdiv(cdiv(n, 16), SM_WAVES) : cap2) : 1;
+        if (ensure(&u->slabs, &u->slab_cap, (size_t)Gm * nk, v.stream)) return -2;
+        int rc = 0;
+        switch (ms) {
+        case 0: rc = launch_surr_mfma<1, 2>(net, v.theta64, fs, k0, nk, &u->tpad, &u->tpad_cap, v.obs64, u->roll, v.std64, n, Gm, u->slabs, v.stream); break;
+        case 1: rc = launch_surr_mfma<1, 3>(net, v.theta64, fs, k0, nk, &u->tpad, &u->tpad_cap, v.obs64, u->roll, v.std64, n, Gm, u->slabs, v.stream); break;
+        case 2: rc = launch_surr_mfma<1, 4>(net, v.theta64, fs, k0, nk, &u->tpad, &u->tpad_cap, v.obs64, u->roll, v.std64, n, Gm, u->slabs, v.stream); break;
+        case 3: rc = launch_surr_mfma<2, 2>(net, v.theta64, fs, k0, nk, &u->tpad, &u->tpad_cap, v.obs64, u->roll, v.std64, n, Gm, u->slabs, v.stream); break;
+        case 4: rc = launch_surr_mfma<2, 3>(net, v.theta64, fs, k0, nk, &u->tpad, &u->tpad_cap, v.obs64, u->roll, v.std64, n, Gm, u->slabs, v.stream); break;
+        default: rc = launch_surr_mfma<2, 4>(net, v.theta64, fs, k0, nk, &u->tpad, &u->tpad_cap, v.obs64, u->roll, v.std64, n, Gm, u->slabs, v.stream); break;
+        }
+        if (rc) return rc;
+        hipLaunchKernelGGL(sum_slabs64_kernel, dim3(cdiv(nk, 16)), dim3(256), 0, v.stream, u->slabs, Gm, nk, u->sums);
+        HCHK(hipGetLastError());
+        if (trpo_dev_allreduce64(d, u->sums, (size_t)nk)) return -4;
+        return 0;
+    }
     if (reg_path(net)) {
         if (ensure(&u->tpad, &u->tpad_cap, (size_t)PADW * nk, v.stream)) return -2;
         hipLaunchKernelGGL(pad_theta_kernel, dim3(cdiv(PADW, 256), nk), dim3(256), 0, v.stream, net, v.theta64, fs, k0,

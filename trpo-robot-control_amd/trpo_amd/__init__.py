@@ -105,6 +105,8 @@ def lib():
     L.trpo_ctx_attach_peers.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_char_p]
     L.trpo_ctx_attach_peers_local.restype = C.c_int
     L.trpo_ctx_attach_peers_local.argtypes = [C.c_void_p, C.c_int, C.c_int, P(C.c_void_p)]
+    L.trpo_ctx_surrogate.restype = C.c_int
+    L.trpo_ctx_surrogate.argtypes = [C.c_void_p, _dp, C.c_int, C.c_int, _dp]
     L.trpo_ctx_comm_backend.restype = C.c_char_p
     L.trpo_ctx_comm_backend.argtypes = [C.c_void_p]
     L.trpo_ctx_fvp.restype = C.c_double
@@ -407,6 +409,13 @@ class Context:
         window (peer_handle()); call concurrently, one thread per rank."""
         arr = (C.c_void_p * len(ctxs))(*[c._h for c in ctxs])
         self._chk(lib().trpo_ctx_attach_peers_local(self._h, rank, len(ctxs), arr), "attach_peers_local")
+
+    def surrogate(self, fullstep, k0=0, nk=1):
+        """Line-search surrogate sums at theta + 0.5^(k0+j) fullstep, j < nk (all ranks)."""
+        out = np.zeros(nk)
+        self._chk(lib().trpo_ctx_surrogate(self._h, np.ascontiguousarray(fullstep, np.float64), k0, nk, out),
+                  "surrogate")
+        return out
 
     @property
     def comm_backend(self) -> str:
