@@ -810,9 +810,16 @@ __device__ __forceinline__ f4 scr_get(const float *scr, int row0, int c, int g) 
 // kernel trace separates the standalone FVP kernel from the fused CG-iteration kernels.
 // QB (MODE 3 only): basis vectors of the residual reorthogonalisation loaded in the prologue's single
 // load round (slots >= A.nq read zeros); QB = 0 with an update: the streaming form (qdots_stage1).
+// The leading scalar arguments duplicate the IterArgs fields the CG step's first load round needs
+// (acc_in, p_in, r_in, x, pslot, the basis; Ps | R_in << 20 | nq << 26 -- 13 dwords): built with
+// -mllvm -amdgpu-kernarg-preload-count (14 SGPRs at most besides the kernarg pointer) they arrive in
+// SGPRs at wave start, so those loads issue without waiting for a scalar load of the kernarg segment
+// (a byval aggregate is never preloaded).
 template <int T0, int T1, int T2, int T3, int ACT, int MODE, int QB = 0>
 __global__ void __launch_bounds__((64 * FastCfg<T0, T1, T2, T3>::WAVES))
-fvp_mlp3_kernel(IterArgs A, Net net) {
+fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p, const double *__restrict__ k_r,
+                const double *__restrict__ k_x, const int *__restrict__ k_pslot, const void *k_q, int k_meta,
+                IterArgs A, Net net) {
     constexpr bool FV = MODE != 1;
     constexpr bool YC = MODE == 2 || MODE == 3;     // forward activations from the cache
     constexpr int NYC = T1 + T2 + T3;               // cached f4 per lane per tile
@@ -827,6 +834,17 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
     double *shq = reinterpret_cast<double *>(lds + C::TLEN + C::VLEN);
     float *qf = reinterpret_cast<float *>(A.q);                     // fp32 reorthogonalisation basis
     const float *qfz = reinterpret_cast<const float *>(A.qz);
+#ifndef TRPO_KPRE
+#define TRPO_KPRE 1
+#endif
+#if TRPO_KPRE
+    const int kPs = k_meta & 0xFFFFF, kR = (k_meta >> 20) & 63, knq = (k_meta >> 26) & 63;
+    const float *kq = reinterpret_cast<const float *>(k_q);
+#else
+    const int kPs = A.Ps, kR = A.R_in, knq = A.nq;
+    const float *kq = qf;
+    k_acc = A.acc_in, k_p = A.p_in, k_r = A.r_in, k_x = A.x, k_pslot = A.pslot;
+#endif
     static_assert(C::SCRATCH >= 2 * QCAP * 4 * C::WAVES, "basis-dot scratch");
     float *tw = lds;                                   // theta pack
     float *vw = lds + C::TLEN;                         // v pack (fragment order, fp32)
@@ -903,11 +921,13 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
         const double *xs = blockIdx.x == 0 ? A.x : A.p_in;    // only block 0 needs x
         if constexpr (PAIR) {
             // replicas summed in replica order as below; rows of stride Ps, pairs 16-byte aligned
-            const double2 p2 = pair_at(A.p_in, 0, A.Ps), r2 = pair_at(A.r_in, 0, A.Ps), x2 = pair_at(xs, 0, A.Ps);
+            // (the preloaded scalar arguments: no wait for the kernarg segment before these loads)
+            const double *xk = blockIdx.x == 0 ? k_x : k_p;
+            const double2 p2 = pair_at(k_p, 0, kPs), r2 = pair_at(k_r, 0, kPs), x2 = pair_at(xk, 0, kPs);
             double2 za[RMAX];
 #pragma unroll
-            for (int k = 0; k < RMAX; ++k) za[k] = pair_at(A.acc_in, min(k, A.R_in - 1), A.Ps);
-            const int2 m2 = pair_at(A.pslot, 0, A.Ps);
+            for (int k = 0; k < RMAX; ++k) za[k] = pair_at(k_acc, min(k, kR - 1), kPs);
+            const int2 m2 = pair_at(k_pslot, 0, kPs);
             const double p0[2] = {p2.x, p2.y}, r0[2] = {r2.x, r2.y}, x0[2] = {x2.x, x2.y};
             const int mm[2] = {m2.x, m2.y};
 #pragma unroll
@@ -916,7 +936,7 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
                 const bool in = q < A.P;
                 double z = e ? za[0].y : za[0].x;
 #pragma unroll
-                for (int k = 1; k < RMAX; ++k) z += k < A.R_in ? (e ? za[k].y : za[k].x) : 0.0;
+                for (int k = 1; k < RMAX; ++k) z += k < kR ? (e ? za[k].y : za[k].x) : 0.0;
                 pv[e] = in ? p0[e] : 0.0;
                 rv[e] = in ? r0[e] : 0.0;
                 xv[e] = (in && blockIdx.x == 0) ? x0[e] : 0.0;
@@ -975,7 +995,18 @@ fvp_mlp3_kernel(IterArgs A, Net net) {
     [[maybe_unused]] double qv[QB > 0 ? QB : 1][C::EMAX];
     if constexpr (QB > 0) {
 #pragma unroll
-        for (int i = 0; i < QB; ++i) qload<C::EMAX, float, PAIR>(qv[i], qf, qfz, A.P, A.Ps, i, upd ? A.nq : 0, C::THREADS);
+        for (int i = 0; i < QB; ++i) {
+            if constexpr (PAIR) {
+                // QB > 0 implies nq >= 1 (qb_index): the clamped row is a stored basis vector, selected
+                // away for the slots >= nq (no zero-line pointer needed)
+                const float2 v = pair_at(kq, min(i, knq - 1), kPs);
+                const bool ok = i < knq;
+                qv[i][0] = (ok && 2 * tid < A.P) ? (double)v.x : 0.0;
+                qv[i][1] = (ok && 2 * tid + 1 < A.P) ? (double)v.y : 0.0;
+            } else {
+                qload<C::EMAX, float, PAIR>(qv[i], qf, qfz, A.P, A.Ps, i, upd ? A.nq : 0, C::THREADS);
+            }
+        }
     }
     if constexpr (CGK) load_static();
     // plain FVP: the direction fragments gathered from v in the same load round
@@ -2789,8 +2820,9 @@ typedef void (*fast_launch_fn)(dim3, int, hipStream_t, const IterArgs &, const N
 
 template <int T0, int T1, int T2, int T3, int ACT, int MODE, int QB = 0>
 static void fast_launch(dim3 g, int lds, hipStream_t st, const IterArgs &a, const Net &net) {
+    const int meta = (a.Ps & 0xFFFFF) | ((a.R_in & 63) << 20) | ((a.nq & 63) << 26);
     hipLaunchKernelGGL((fvp_mlp3_kernel<T0, T1, T2, T3, ACT, MODE, QB>), g, dim3(64 * FastCfg<T0, T1, T2, T3>::WAVES),
-                       lds, st, a, net);
+                       lds, st, a.acc_in, a.p_in, a.r_in, a.x, a.pslot, (const void *)a.q, meta, a, net);
 }
 // MODE 3 kernels by the reorthogonalisation basis they load in their prologue (QB slots)
 constexpr int kQB[4] = {0, 4, 8, QCAP};
