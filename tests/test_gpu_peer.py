@@ -4,9 +4,10 @@ per-sample FVP loop src/TRPO_FVP.c:771-921).
 
 Two ways of running several ranks on one device:
   * in-process: contexts of one process, one thread per rank, windows joined by pointer
-    (trpo_ctx_attach_peers_local) -- the CG runs from its captured graph, one exchange kernel per FVP;
+    (trpo_ctx_attach_peers_local) -- one exchange kernel per FVP, launched eagerly (contexts sharing
+    a device must not allocate while another's exchange spins: see run_peer_ranks);
   * multi-process: one process per rank (tests/peer_worker.py), windows exported and opened as IPC
-    handles (trpo_ctx_attach_peers) -- the path bench.py takes across GPUs.
+    handles (trpo_ctx_attach_peers) -- the path bench.py takes across GPUs, CG from its captured graph.
 Checked: every rank ends with a bit-identical x (rank-order sums), x within the north-star bound of
 the reference's golden and within rounding of the host-group exchange, standalone FVPs and the full
 TRPO_Update through the generic in-place exchange, and that a rank that never arrives makes the
@@ -31,9 +32,15 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CG_TOL = 1e-4
 
 
-def run_peer_ranks(ctxs, fn, timeout=120.0):
-    """Open every window, then attach and run fn(ctx, rank) on all contexts concurrently."""
+def run_peer_ranks(ctxs, fn, timeout=120.0, warm=None):
+    """Open every window, then attach and run fn(ctx, rank) on all contexts concurrently.
+    warm(ctx): run once per context BEFORE attaching, so that the lazily sized device buffers exist
+    already: in ONE process an allocation or free (which may wait for the whole device) in one
+    rank's thread while another rank's exchange kernel spins for it would stall until the exchange's
+    3 s timeout -- a hazard of contexts sharing one GPU, not of one process per GPU."""
     for c in ctxs:
+        if warm is not None:
+            warm(c)
         c.peer_handle()
     world = len(ctxs)
     out, err = [None] * world, [None] * world
@@ -69,15 +76,16 @@ def test_peer_cg_lockstep_and_golden(bounds):
     ctxs = _shards(x, bounds)
     try:
         res = run_peer_ranks(ctxs, lambda ctx, r: (ctx.cg(x["vin"], c["maxiter"], c["resth"]),
-                                                   ctx.cg(x["vin"], c["maxiter"], c["resth"]),   # graph replay
-                                                   ctx.cg_history(), ctx.comm_info()))
+                                                   ctx.cg(x["vin"], c["maxiter"], c["resth"]),   # repeat
+                                                   ctx.cg_history(), ctx.comm_info()),
+                             warm=lambda ctx: ctx.cg(x["vin"], c["maxiter"], c["resth"]))
     finally:
         for ctx in ctxs:
             ctx.close()
     x0 = res[0][0]
     for r, (xa, xb, (rr, xn, it), info) in enumerate(res):
         np.testing.assert_array_equal(xa, x0)            # lockstep: identical bits on every rank
-        np.testing.assert_array_equal(xb, x0)            # the replayed graph repeats the solve
+        np.testing.assert_array_equal(xb, x0)            # a second solve repeats the first
         assert it == c["iters"]
         assert info["rank"] == r and info["world"] == len(bounds)
         assert info["backend"].startswith("peer-xgmi"), info
@@ -99,7 +107,8 @@ def test_peer_matches_host_group():
             ctx.close()
     ctxs = _shards(x, bounds)
     try:
-        xp = run_peer_ranks(ctxs, lambda ctx, r: ctx.cg(x["vin"], c["maxiter"], c["resth"]))[0]
+        xp = run_peer_ranks(ctxs, lambda ctx, r: ctx.cg(x["vin"], c["maxiter"], c["resth"]),
+                            warm=lambda ctx: ctx.cg(x["vin"], c["maxiter"], c["resth"]))[0]
     finally:
         for ctx in ctxs:
             ctx.close()
@@ -113,7 +122,7 @@ def test_peer_fvp_and_update():
     x = cases.inputs(c)
     ctxs = _shards(x, [(0, 1000), (1000, 3150)])
     try:
-        res = run_peer_ranks(ctxs, lambda ctx, r: ctx.fvp(x["vin"]))
+        res = run_peer_ranks(ctxs, lambda ctx, r: ctx.fvp(x["vin"]), warm=lambda ctx: ctx.fvp(x["vin"]))
     finally:
         for ctx in ctxs:
             ctx.close()
@@ -132,7 +141,7 @@ def test_peer_fvp_and_update():
     for ctx, (lo, hi) in zip(ctxs, bounds):
         ctx.set_rollout(mean[lo:hi], action[lo:hi], adv[lo:hi])
     try:
-        res = run_peer_ranks(ctxs, lambda ctx, r: ctx.update())
+        res = run_peer_ranks(ctxs, lambda ctx, r: ctx.update(), warm=lambda ctx: ctx.update())
     finally:
         for ctx in ctxs:
             ctx.close()

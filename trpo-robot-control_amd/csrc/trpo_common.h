@@ -99,7 +99,7 @@ trpo_peer *trpo_peer_create(int device, size_t slot_doubles);
 void trpo_peer_destroy(trpo_peer *p);
 int trpo_peer_handle(trpo_peer *p, void *h64);
 void *trpo_peer_window(trpo_peer *p);
-int trpo_peer_connect(trpo_peer *p, int rank, int world, const void *handles, void *const *local);
+int trpo_peer_connect(trpo_peer *p, int rank, int world, const void *handles, void *const *local, hipStream_t st);
 int trpo_peer_allreduce(trpo_peer *p, hipStream_t st, const double *in, int R, int Rstride, int count, double *out,
                         const int *done);
 int trpo_peer_error(const trpo_peer *p);

@@ -710,7 +710,10 @@ constexpr int SCR_LD = 20;            // scratch row stride (floats): conflict-f
 #ifndef TRPO_SCR_LD3
 #define TRPO_SCR_LD3 20
 #endif
-constexpr int SCR_LD3 = TRPO_SCR_LD3;  // fvp_mlp3_kernel's transpose scratch
+constexpr int SCR_LD3 = TRPO_SCR_LD3;  // fvp_mlp3_kernel's transpose scratch (TRPO_SCR_SWZ=0 layout)
+#ifndef TRPO_SCR_SWZ
+#define TRPO_SCR_SWZ 1                  // swizzled conflict-free transpose layout (scr_off)
+#endif
 
 template <int T0, int T1, int T2, int T3>
 struct FastCfg {
@@ -736,7 +739,8 @@ struct FastCfg {
     // per-wave transpose scratch: max rows over the three contractions
     static constexpr int R0 = 16 * (T0 + T1), R1 = 16 * (T1 + T2), R2 = 16 * (T2 + T3);
     static constexpr int ROWS = R0 > R1 ? (R0 > R2 ? R0 : R2) : (R1 > R2 ? R1 : R2);
-    static constexpr int SCR = ROWS * SCR_LD3;
+    static constexpr int SCR = ROWS * 20;             // scr_off: 20 floats per row either way
+    static_assert(TRPO_SCR_SWZ == 0 || SCR_LD3 == 20, "swizzled scratch assumes the 20-float footprint");
     // accumulator registers per lane; the block's partial sums are written in this
     // "accumulator order" (f4 k, lane, r) -- SLAB floats per block, mapped back to
     // natural parameter order by the reduce kernel (imap)
@@ -790,12 +794,29 @@ __device__ __forceinline__ float rowsum16(float v) {
     return v;
 }
 
+// Transpose scratch of fvp_mlp3_kernel: scr_put writes lane (c, g)'s accumulator rows 4g + r of
+// column c (ds_write_b32), scr_get reads row c's columns 4g .. 4g + 3 (ds_read_b128).  Layout
+// (TRPO_SCR_SWZ, round 2): 16 floats per row, 16 floats of gap after every 4 rows, and the 4-float
+// chunk index XORed with s(q) = {0, 3, 2, 1}[q], q = (row / 4) mod 4 (rows start at multiples of
+// 16).  With gfx950's lane groups (MI355X_MICROARCH.md §LDS): a ds_write_b32 half-wave writes rows
+// r and r + 4, whose bases differ by 80 floats = 16 banks mod 32, into disjoint bank halves; the
+// ds_read_b128 groups ({0-3,12-15,20-27} and the three others) cover every bank exactly once.  The
+// round-1 row stride of 20 floats left 3 two-way conflicts per read group (42 % of the kernel's LDS
+// cycles were conflict cycles).  Same footprint: 20 floats per row.
+__device__ __forceinline__ int scr_off(int row, int chunk) {
+#if TRPO_SCR_SWZ
+    const int q = (row >> 2) & 3;
+    return row * 16 + (row >> 2) * 16 + ((chunk ^ ((4 - q) & 3)) << 2);
+#else
+    return row * SCR_LD3 + 4 * chunk;
+#endif
+}
 __device__ __forceinline__ void scr_put(float *scr, int row0, f4 t, int c, int g) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) scr[(row0 + 4 * g + r) * SCR_LD3 + c] = t[r];
+    for (int r = 0; r < 4; ++r) scr[scr_off(row0 + 4 * g + r, c >> 2) + (c & 3)] = t[r];
 }
 __device__ __forceinline__ f4 scr_get(const float *scr, int row0, int c, int g) {
-    return *reinterpret_cast<const f4 *>(scr + (row0 + c) * SCR_LD3 + 4 * g);
+    return *reinterpret_cast<const f4 *>(scr + scr_off(row0 + c, g));
 }
 
 // ACT >= 0: activations of layers 1..3 fixed at compile time (a1 | a2 << 2 | a3 << 4);
@@ -3057,6 +3078,7 @@ struct trpo_dev {
     int peer_on;
     double *zred;               // [2][Ps] exchanged partial sums (the next CG-iteration kernel's input)
     double *ptmp;               // [slot] staging of an in-place all-reduce
+    double *pn;                 // [PEER_WMAX] the shard sizes exchanged at attach
     int rank, world;
     char name[64];
 };
@@ -3407,7 +3429,7 @@ extern "C" void trpo_dev_destroy(trpo_dev *d) {
     trpo_peer_destroy(d->peer);
     trpo_update_state_free(d->upd);
     void *ptrs[] = {d->zbuf, d->dotsbuf, d->obs64, d->pg_d, d->pg_adv, d->pg_iv, d->st, d->pbuf[0], d->pbuf[1], d->rbuf[0], d->rbuf[1], d->accbuf, d->pacc, d->imap, d->tpack, d->vpack, d->tmap, d->vmap, d->pslot, d->obs4, d->yc, d->th32, d->v32, d->iv32, d->obs32, d->scratch,
-                    d->theta64, d->std64, d->r, d->zacc, d->slabs, d->ctl, d->hist, d->tscr, d->qbuf, d->qzero, d->zred, d->ptmp};
+                    d->theta64, d->std64, d->r, d->zacc, d->slabs, d->ctl, d->hist, d->tscr, d->qbuf, d->qzero, d->zred, d->ptmp, d->pn};
     for (void *p : ptrs)
         if (p) hipFree(p);
     for (int i = 0; i < 5; ++i)
@@ -3610,10 +3632,12 @@ static int refresh_n_total(trpo_dev *d) {
         // every rank's shard size in one sum-all-reduce (rank r contributes n at slot r): N is the
         // total, and the replica sizing below reads the LARGEST shard -- both identical on all ranks
         const int W = d->world;
-        double *hn = (double *)calloc(W, sizeof(double)), *dn = NULL;
+        double *hn = (double *)calloc(W, sizeof(double)), *dn = d->peer_on ? d->pn : NULL;
         if (!hn) return -3;
         hn[d->rank] = (double)n;
-        if (hipMalloc((void **)&dn, sizeof(double) * W) != hipSuccess) {
+        // the peer exchange uses a buffer allocated with its window: no allocation (which may wait for
+        // the whole device) while another context of this process already spins in its exchange
+        if (!dn && hipMalloc((void **)&dn, sizeof(double) * W) != hipSuccess) {
             free(hn);
             return -2;
         }
@@ -3621,7 +3645,7 @@ static int refresh_n_total(trpo_dev *d) {
         if (!rc) rc = allreduce(d, dn, (size_t)W);
         if (!rc && hipMemcpyAsync(hn, dn, sizeof(double) * W, hipMemcpyDeviceToHost, d->stream)) rc = -2;
         if (!rc && hipStreamSynchronize(d->stream)) rc = -2;
-        hipFree(dn);
+        if (dn != d->pn) hipFree(dn);
         if (!rc) {
             double tot = 0.0, mx = 0.0;
             for (int r = 0; r < W; ++r) {
@@ -3739,6 +3763,7 @@ extern "C" int trpo_dev_peer_open(trpo_dev *d, void *handle64) {
         HCHK(hipMalloc((void **)&d->zred, sizeof(double) * 2 * d->Ps));
         HCHK(hipMemset(d->zred, 0, sizeof(double) * 2 * d->Ps));
         HCHK(hipMalloc((void **)&d->ptmp, sizeof(double) * trpo_peer_slot(d->peer)));
+        HCHK(hipMalloc((void **)&d->pn, sizeof(double) * PEER_WMAX));
     }
     return handle64 ? trpo_peer_handle(d->peer, handle64) : 0;
 }
@@ -3750,7 +3775,7 @@ extern "C" int trpo_dev_set_peers(trpo_dev *d, int rank, int world, const void *
     if (!d || !d->peer || world < 1 || world > PEER_WMAX || rank < 0 || rank >= world) return -1;
     HCHK(hipSetDevice(d->device));
     HCHK(hipStreamSynchronize(d->stream));
-    const int rc = trpo_peer_connect(d->peer, rank, world, handles, local);
+    const int rc = trpo_peer_connect(d->peer, rank, world, handles, local, d->stream);
     if (rc) return rc;
     if (d->comm) {
         ncclCommDestroy(d->comm);
@@ -3760,6 +3785,9 @@ extern "C" int trpo_dev_set_peers(trpo_dev *d, int rank, int world, const void *
     d->peer_on = world > 1;
     d->rank = rank;
     d->world = world;
+    // contexts of ONE process sharing a device: the CG runs eagerly -- instantiating a graph may
+    // allocate (and wait for the device) while another rank's exchange already spins for this one
+    if (local) d->no_graph = 1;
     if (d->cg_exec) {
         hipGraphExecDestroy(d->cg_exec);
         d->cg_exec = NULL;

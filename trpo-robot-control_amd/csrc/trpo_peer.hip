@@ -180,7 +180,7 @@ void *trpo_peer_window(trpo_peer *p) { return p ? p->win : NULL; }
 
 // handles: world x PEER_HANDLE_BYTES (rank order; the own entry is ignored), or
 // local: world window pointers of contexts in this process (rank order)
-int trpo_peer_connect(trpo_peer *p, int rank, int world, const void *handles, void *const *local) {
+int trpo_peer_connect(trpo_peer *p, int rank, int world, const void *handles, void *const *local, hipStream_t st) {
     if (!p || world < 1 || world > PEER_WMAX || rank < 0 || rank >= world || (!handles && !local)) return -1;
     HCHK(hipSetDevice(p->device));
     double *w[PEER_WMAX] = {NULL};
@@ -209,7 +209,8 @@ int trpo_peer_connect(trpo_peer *p, int rank, int world, const void *handles, vo
         }
         if (!w[r]) return -1;
     }
-    HCHK(hipMemcpy(p->dwins, w, sizeof(double *) * world, hipMemcpyHostToDevice));
+    HCHK(hipMemcpyAsync(p->dwins, w, sizeof(double *) * world, hipMemcpyHostToDevice, st));
+    HCHK(hipStreamSynchronize(st));
     __atomic_store_n(p->err_h, 0, __ATOMIC_RELEASE);     // a new attach starts without a timed-out exchange
     p->rank = rank;
     p->world = world;
