@@ -714,6 +714,9 @@ constexpr int SCR_LD3 = TRPO_SCR_LD3;  // fvp_mlp3_kernel's transpose scratch (T
 #ifndef TRPO_SCR_SWZ
 #define TRPO_SCR_SWZ 1                  // swizzled conflict-free transpose layout (scr_off)
 #endif
+#ifndef TRPO_SKIPW
+#define TRPO_SKIPW 1                    // element-less waves skip the CG-state loads (pair layout)
+#endif
 
 template <int T0, int T1, int T2, int T3>
 struct FastCfg {
@@ -944,11 +947,22 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
             // replicas summed in replica order as below; rows of stride Ps, pairs 16-byte aligned
             // (the preloaded scalar arguments: no wait for the kernarg segment before these loads)
             const double *xk = blockIdx.x == 0 ? k_x : k_p;
-            const double2 p2 = pair_at(k_p, 0, kPs), r2 = pair_at(k_r, 0, kPs), x2 = pair_at(xk, 0, kPs);
+            // waves whose first pair lies beyond Ps hold no CG element (armDOF_0: waves 5-7): they skip
+            // the state loads in a wave-uniform scalar branch and keep zeros (TRPO_SKIPW)
+            const bool holds = !TRPO_SKIPW || 128 * __builtin_amdgcn_readfirstlane(wave) < kPs;
+            double2 p2 = {0.0, 0.0}, r2 = {0.0, 0.0}, x2 = {0.0, 0.0};
             double2 za[RMAX];
 #pragma unroll
-            for (int k = 0; k < RMAX; ++k) za[k] = pair_at(k_acc, min(k, kR - 1), kPs);
-            const int2 m2 = pair_at(k_pslot, 0, kPs);
+            for (int k = 0; k < RMAX; ++k) za[k] = make_double2(0.0, 0.0);
+            int2 m2 = make_int2(-1, -1);
+            if (holds) {
+                p2 = pair_at(k_p, 0, kPs);
+                r2 = pair_at(k_r, 0, kPs);
+                x2 = pair_at(xk, 0, kPs);
+#pragma unroll
+                for (int k = 0; k < RMAX; ++k) za[k] = pair_at(k_acc, min(k, kR - 1), kPs);
+                m2 = pair_at(k_pslot, 0, kPs);
+            }
             const double p0[2] = {p2.x, p2.y}, r0[2] = {r2.x, r2.y}, x0[2] = {x2.x, x2.y};
             const int mm[2] = {m2.x, m2.y};
 #pragma unroll
@@ -1019,8 +1033,9 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
         for (int i = 0; i < QB; ++i) {
             if constexpr (PAIR) {
                 // QB > 0 implies nq >= 1 (qb_index): the clamped row is a stored basis vector, selected
-                // away for the slots >= nq (no zero-line pointer needed)
-                const float2 v = pair_at(kq, min(i, knq - 1), kPs);
+                // away for the slots >= nq (no zero-line pointer needed); skipped by element-less waves
+                float2 v = make_float2(0.0f, 0.0f);
+                if (!TRPO_SKIPW || 128 * __builtin_amdgcn_readfirstlane(wave) < kPs) v = pair_at(kq, min(i, knq - 1), kPs);
                 const bool ok = i < knq;
                 qv[i][0] = (ok && 2 * tid < A.P) ? (double)v.x : 0.0;
                 qv[i][1] = (ok && 2 * tid + 1 < A.P) ? (double)v.y : 0.0;
