@@ -2570,8 +2570,17 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
     }
     [[maybe_unused]] double qv[QREG ? QCAP : 1][E];
     if constexpr (QREG) {
+        // qbuf == nullptr (no reorthogonalisation, or the LAST step of a solve -- whose r', p' nobody
+        // reads): no basis loads at all (a kernel-argument-uniform branch)
+        if (qbuf) {
 #pragma unroll
-        for (int i = 0; i < QCAP; ++i) qload<E>(qv[i], qbuf, qz, P, Ps, i, qbuf ? nq : 0, 1024);
+            for (int i = 0; i < QCAP; ++i) qload<E>(qv[i], qbuf, qz, P, Ps, i, nq, 1024);
+        } else {
+#pragma unroll
+            for (int i = 0; i < QCAP; ++i)
+#pragma unroll
+                for (int e = 0; e < E; ++e) qv[i][e] = 0.0;
+        }
     }
     if (done) {
         for (int e = threadIdx.x; e < zero_len; e += 1024) acc_zero[e] = 0.0;   // inputs unused
@@ -2634,8 +2643,10 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
         if (q < P) {
             const double pn = rv[e] + beta * pv[e];
             x[q] = xv[e];
-            r_out[q] = rv[e];
-            p_out[q] = pn;
+            if (r_out) {                               // nullptr: the last step (only x is read)
+                r_out[q] = rv[e];
+                p_out[q] = pn;
+            }
             if (vlen) sp[q] = pn;
         }
     }
@@ -4153,12 +4164,14 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
         }
         if (M > 0) {
             const int in = (int)((M - 1) & 1), out = (int)(M & 1);
+            // the last step: x only (its r', p' and basis vector are never read -- no basis loads,
+            // no reorthogonalisation of a residual that only feeds the printed history)
             CG_DISPATCH(E, cg_update_kernel, dim3(1), dim3(1024), 0, d->stream,
                         d->atomic ? (d->peer_on ? zred_slot(d, M - 1) : acc_slot(d, M - 1)) : d->zacc,
                         d->atomic && !d->peer_on ? d->Rc : 1, d->pbuf[in], d->rbuf[in],
-                        d->pbuf[out], d->rbuf[out], x, d->P, d->nw, d->ctl, d->st + in, d->st + out, d->hist,
-                        (const int *)nullptr, (void *)nullptr, 0, 0, d->reorth ? d->qbuf : nullptr,
-                        (const void *)d->qzero, cg_step_nq(d, M - 1), d->Ps, d->atomic ? acc_slot(d, 0) : nullptr,
+                        (double *)nullptr, (double *)nullptr, x, d->P, d->nw, d->ctl, d->st + in, d->st + out,
+                        d->hist, (const int *)nullptr, (void *)nullptr, 0, 0, (void *)nullptr,
+                        (const void *)d->qzero, 0, d->Ps, d->atomic ? acc_slot(d, 0) : nullptr,
                         d->atomic ? RP : 0);
         }
     } else if (d->coop && d->coop_dist) {
@@ -4226,9 +4239,9 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
         if (M > 0) {
             const int in = (int)((M - 1) & 1), out = (int)(M & 1);
             CG_DISPATCH(E, cg_update_kernel, dim3(1), dim3(1024), 0, d->stream, d->zacc, 1, d->pbuf[in], d->rbuf[in],
-                        d->pbuf[out], d->rbuf[out], x, d->P, d->nw, d->ctl, d->st + in, d->st + out, d->hist,
-                        (const int *)nullptr, (void *)nullptr, 0, 0, d->reorth ? d->qbuf : nullptr,
-                        (const void *)d->qzero, cg_step_nq(d, M - 1), d->Ps);
+                        (double *)nullptr, (double *)nullptr, x, d->P, d->nw, d->ctl, d->st + in, d->st + out,
+                        d->hist, (const int *)nullptr, (void *)nullptr, 0, 0, (void *)nullptr,
+                        (const void *)d->qzero, 0, d->Ps);                 // the last step: x only
         }
     } else {
         // generic or cooperative kernel: FVP, reduce, [all-reduce], CG step per iteration
