@@ -2685,6 +2685,91 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
 // The next FVP gathers its direction fragments from p' (natural order).  Elements as adjacent pairs
 // (one 16-byte load per vector per thread), CGS_T threads per block.
 // ---------------------------------------------------------------------------
+// The LAST step of a fused CG solve (src/TRPO_CG.c:65-103 for i = maxiter - 1) for P <= 1024: only x
+// is read afterwards, so no basis, no reorthogonalisation and no r' / p' stores.  One 512-thread
+// workgroup owns adjacent element pairs (16-byte loads of the replicas, p, r, x: the CG-iteration
+// kernel's layout); ONE block reduction of p.z, r.z, z.z, x.p, p.p gives alpha, |r'|^2 = |r|^2 -
+// 2a r.z + a^2 z.z and |x'|^2 = |x|^2 + 2a x.p + a^2 p.p (the fused step's expansion; direct = 1 -- the
+// fp64 mode -- sums |r'|^2 and |x'|^2 directly in a second reduction instead, as cg_update_kernel).
+// Zeroes acc_zero (the next solve's first atomic target) after consuming its input.
+constexpr int CGL_T = 512;
+__global__ void __launch_bounds__(CGL_T)
+cg_last_kernel(const double *__restrict__ acc, int R_in, const double *__restrict__ p_in,
+               const double *__restrict__ r_in, double *__restrict__ x, int P, int Ps, int nw, Ctl *ctl,
+               const CgSt *st_in, CgSt *st_out, double *hist, double *acc_zero, int zero_len, int direct) {
+#pragma clang fp contract(off)
+    __shared__ double sh[8 * 4 * (CGL_T / 64)];
+    const int tid = threadIdx.x;
+    const int done = ctl->done;
+    const double n = ctl->n_total, lam = ctl->damping, th = ctl->resth;
+    const int maxiter = ctl->maxiter;
+    const CgSt sin = *st_in;
+    const double2 p2 = pair_at(p_in, 0, Ps), r2 = pair_at(r_in, 0, Ps), x2 = pair_at(x, 0, Ps);
+    double2 za[RMAX];
+#pragma unroll
+    for (int k = 0; k < RMAX; ++k) za[k] = pair_at(acc, min(k, R_in - 1), Ps);
+    if (done) {
+        for (int e = tid; e < zero_len; e += CGL_T) acc_zero[e] = 0.0;   // inputs unused
+        return;
+    }
+    const double pe[2] = {p2.x, p2.y}, re[2] = {r2.x, r2.y}, xe[2] = {x2.x, x2.y};
+    double pv[2], rv[2], xv[2], zv[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        const int q = 2 * tid + e;
+        const bool in = q < P;
+        double z = e ? za[0].y : za[0].x;
+#pragma unroll
+        for (int k = 1; k < RMAX; ++k) z += k < R_in ? (e ? za[k].y : za[k].x) : 0.0;
+        pv[e] = in ? pe[e] : 0.0;
+        rv[e] = in ? re[e] : 0.0;
+        xv[e] = in ? xe[e] : 0.0;
+        zv[e] = in ? __builtin_fma(lam, pv[e], q < nw ? z / n : 2.0 * pv[e]) : 0.0;
+    }
+    double red[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        red[0] = __builtin_fma(pv[e], zv[e], red[0]);
+        red[1] = __builtin_fma(rv[e], zv[e], red[1]);
+        red[2] = __builtin_fma(zv[e], zv[e], red[2]);
+        red[3] = __builtin_fma(xv[e], pv[e], red[3]);
+        red[4] = __builtin_fma(pv[e], pv[e], red[4]);
+    }
+    block_sums_dpp<5, CGL_T / 64>(red, sh);
+    const double alpha = sin.rdotr / red[0];
+    double nr = sin.rdotr - 2.0 * alpha * red[1] + alpha * alpha * red[2];
+    double xn2 = sin.xx + 2.0 * alpha * red[3] + alpha * alpha * red[4];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        xv[e] = __builtin_fma(alpha, pv[e], xv[e]);
+        rv[e] = __builtin_fma(-alpha, zv[e], rv[e]);
+    }
+    if (direct) {                                       // kernel-argument-uniform
+        double s2[2] = {rv[0] * rv[0] + rv[1] * rv[1], xv[0] * xv[0] + xv[1] * xv[1]};
+        block_sums_dpp<2, CGL_T / 64>(s2, sh + 5 * 4 * (CGL_T / 64));
+        nr = s2[0];
+        xn2 = s2[1];
+    }
+    if (2 * tid + 1 < P) {
+        reinterpret_cast<double2 *>(x)[tid] = make_double2(xv[0], xv[1]);
+    } else if (2 * tid < P) {
+        x[2 * tid] = xv[0];
+    }
+    if (tid == 0) {
+        const int it = sin.iter + 1;
+        st_out->rdotr = nr;
+        st_out->xx = xn2;
+        st_out->iter = it;
+        ctl->iter = it;
+        ctl->rdotr = nr;
+        hist[2 * it] = nr;
+        hist[2 * it + 1] = sqrt(xn2);
+        ctl->done = (nr < th || it >= maxiter) ? 1 : 0;
+    }
+    // every thread's reads of acc were consumed before the block reduction's barrier
+    for (int e = tid; e < zero_len; e += CGL_T) acc_zero[e] = 0.0;
+}
+
 constexpr int CGS_T = 256, CGS_K = 5 + QCAP;
 template <typename QT>
 __global__ void __launch_bounds__(CGS_T)
@@ -3106,6 +3191,7 @@ struct trpo_dev {
     double *ptmp;               // [slot] staging of an in-place all-reduce
     double *pn;                 // [PEER_WMAX] the shard sizes exchanged at attach
     int rank, world;
+    int no_cg_last;             // TRPO_CG_LAST=0: the last step on cg_update_kernel (A/B)
     char name[64];
 };
 
@@ -3320,6 +3406,8 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
     DMALLOC(d->qbuf, sizeof(double) * QCAP * d->Ps);
     DMALLOC(d->qzero, sizeof(double) * 64);
     {
+        const char *el = getenv("TRPO_CG_LAST");
+        d->no_cg_last = el && atoi(el) == 0;
         const char *eo = getenv("TRPO_CG_REORTH");
         d->reorth = !(eo && atoi(eo) == 0);
     }
@@ -4166,6 +4254,13 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
             const int in = (int)((M - 1) & 1), out = (int)(M & 1);
             // the last step: x only (its r', p' and basis vector are never read -- no basis loads,
             // no reorthogonalisation of a residual that only feeds the printed history)
+            if (d->P <= 2 * CGL_T && !d->no_cg_last) {
+                hipLaunchKernelGGL(cg_last_kernel, dim3(1), dim3(CGL_T), 0, d->stream,
+                                   d->atomic ? (d->peer_on ? zred_slot(d, M - 1) : acc_slot(d, M - 1)) : d->zacc,
+                                   d->atomic && !d->peer_on ? d->Rc : 1, d->pbuf[in], d->rbuf[in], x, d->P, d->Ps,
+                                   d->nw, d->ctl, d->st + in, d->st + out, d->hist,
+                                   d->atomic ? acc_slot(d, 0) : nullptr, d->atomic ? RP : 0, d->f64);
+            } else
             CG_DISPATCH(E, cg_update_kernel, dim3(1), dim3(1024), 0, d->stream,
                         d->atomic ? (d->peer_on ? zred_slot(d, M - 1) : acc_slot(d, M - 1)) : d->zacc,
                         d->atomic && !d->peer_on ? d->Rc : 1, d->pbuf[in], d->rbuf[in],
