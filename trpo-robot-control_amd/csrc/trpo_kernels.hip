@@ -107,6 +107,7 @@ struct IterArgs {
     double init_resth;
     const double *b_init;
     const int *pslot;             // natural parameter -> v-pack slot (pslot_at), -1 for LogStd
+    const int *islot;             // natural parameter -> slab / accumulator position (islot_at), [nw]
     // residual reorthogonalisation (update / init): the basis q_0 .. q_{QCAP-1} (fp64 [QCAP][P]), the
     // number of stored vectors this step uses (nq = min(iteration before the step, QCAP)), a zero line,
     // and whether reorthogonalisation is on (TRPO_CG_REORTH, default 1)
@@ -629,6 +630,12 @@ __global__ void build_pslot_kernel(Net n, Pack pk, int *ps, int P) {
     const int T[4] = {pk.T[0], pk.T[1], pk.T[2], pk.T[3]};
     if (q < P) ps[q] = pslot_at(n, T, q);
 }
+// natural parameter -> accumulator (slab) position of the tile kernel's epilogue, q < nw
+__global__ void build_islot_kernel(Net n, Pack pk, int *is, int nw) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    const int T[4] = {pk.T[0], pk.T[1], pk.T[2], pk.T[3]};
+    if (q < nw) is[q] = islot_at(n, T, q);
+}
 
 __global__ void gather_pack_kernel(void *dst, const double *src, const int *map, int len, int f64) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -716,6 +723,9 @@ constexpr int SCR_LD3 = TRPO_SCR_LD3;  // fvp_mlp3_kernel's transpose scratch (T
 #endif
 #ifndef TRPO_SKIPW
 #define TRPO_SKIPW 1                    // element-less waves skip the CG-state loads (pair layout)
+#endif
+#ifndef TRPO_ISLOT_TABLE
+#define TRPO_ISLOT_TABLE 1              // epilogue slot positions from a table (not islot_at)
 #endif
 
 template <int T0, int T1, int T2, int T3>
@@ -1215,6 +1225,18 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
     if constexpr (CGK) stage_static();
     __syncthreads();
     STAMP(1);
+#if TRPO_NAT_ATOMICS
+    // the epilogue's natural -> accumulator positions (a table built at context creation: islot_at's
+    // integer divisions cost ~0.3 us per launch on the epilogue's critical path); loaded now, used
+    // after the tile loop, so the load's latency hides behind the tiles
+    [[maybe_unused]] int jslot[C::EMAX];
+    if constexpr (C::RW == C::WAVES && TRPO_ISLOT_TABLE) {
+        if (A.islot) {
+#pragma unroll
+            for (int e = 0; e < C::EMAX; ++e) jslot[e] = A.islot[min(tid + e * C::THREADS, A.nw - 1)];
+        }
+    }
+#endif
     [[maybe_unused]] bool first_tile = true;
 
     const int a1 = ACT >= 0 ? (ACT & 3) : net.act[1];
@@ -1622,7 +1644,7 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
             for (int e = 0; e < C::EMAX; ++e) {
                 const int q = tid + e * C::THREADS;
                 if (q < A.nw) {
-                    const int j = islot_at(net, Tc, q);
+                    const int j = (TRPO_ISLOT_TABLE && A.islot) ? jslot[e] : islot_at(net, Tc, q);
                     float t = 0.0f;
 #pragma unroll
                     for (int w = 0; w < C::WAVES; ++w) t += lds[w * C::SLAB + j];
@@ -3123,6 +3145,7 @@ struct trpo_dev {
     void *tpack, *vpack;
     int *tmap, *vmap;
     int *pslot;                 // natural parameter -> v-pack slot (-1: LogStd)
+    int *islot;                 // natural parameter -> the tile kernel's accumulator position (epilogue)
     int *imap;                  // slab position -> natural parameter (reduce kernel)
     int slab;                   // floats per block partial
     void *obs4;
@@ -3444,6 +3467,8 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
         DMALLOC(d->vmap, sizeof(int) * pk.vlen);
         DMALLOC(d->pslot, sizeof(int) * d->Ps);
         hipLaunchKernelGGL(build_pslot_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, n, pk, d->pslot, d->P);
+        DMALLOC(d->islot, sizeof(int) * (d->nw > 0 ? d->nw : 1));
+        hipLaunchKernelGGL(build_islot_kernel, dim3(cdiv(d->nw, 256)), dim3(256), 0, d->stream, n, pk, d->islot, d->nw);
         const int len = pk.tlen > pk.vlen ? pk.tlen : pk.vlen;
         hipLaunchKernelGGL(build_maps_kernel, dim3(cdiv(len, 256)), dim3(256), 0, d->stream, n, pk, d->tmap, d->vmap,
                            d->f64);
@@ -3542,7 +3567,7 @@ extern "C" void trpo_dev_destroy(trpo_dev *d) {
     if (d->comm) ncclCommDestroy(d->comm);
     trpo_peer_destroy(d->peer);
     trpo_update_state_free(d->upd);
-    void *ptrs[] = {d->zbuf, d->dotsbuf, d->obs64, d->pg_d, d->pg_adv, d->pg_iv, d->st, d->pbuf[0], d->pbuf[1], d->rbuf[0], d->rbuf[1], d->accbuf, d->pacc, d->imap, d->tpack, d->vpack, d->tmap, d->vmap, d->pslot, d->obs4, d->yc, d->th32, d->v32, d->iv32, d->obs32, d->scratch,
+    void *ptrs[] = {d->zbuf, d->dotsbuf, d->obs64, d->pg_d, d->pg_adv, d->pg_iv, d->st, d->pbuf[0], d->pbuf[1], d->rbuf[0], d->rbuf[1], d->accbuf, d->pacc, d->imap, d->tpack, d->vpack, d->tmap, d->vmap, d->pslot, d->islot, d->obs4, d->yc, d->th32, d->v32, d->iv32, d->obs32, d->scratch,
                     d->theta64, d->std64, d->r, d->zacc, d->slabs, d->ctl, d->hist, d->tscr, d->qbuf, d->qzero, d->zred, d->ptmp, d->pn};
     for (void *p : ptrs)
         if (p) hipFree(p);
@@ -3987,6 +4012,7 @@ static IterArgs plain_args(trpo_dev *d, const int *skip) {
     a.slabs = (float *)d->slabs;
     a.vmap = d->vmap;
     a.pslot = d->pslot;
+    a.islot = d->islot;
     a.imap = d->imap;
     a.skip = skip;
     a.R_out = 1;
