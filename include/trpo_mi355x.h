@@ -153,7 +153,9 @@ int trpo_ctx_comm_info(const trpo_ctx *ctx, int *rank, int *world, int *replicas
  * the context then goes through the exchange kernel (rank-order sums: identical bits on every rank);
  * the CG graph's per-FVP all-reduce is one kernel.  Contexts of ONE process (tests; any devices)
  * attach with trpo_ctx_attach_peers_local() after each has called trpo_ctx_peer_handle(ctx, NULL).
- * A rank that never arrives makes the exchange give up after ~1 s: later calls return an error. */
+ * A rank that never arrives makes the exchange give up after 3 s: later calls return an error.
+ * Attach once per context: the exchange numbering lives with the windows, so all ranks of a world
+ * must be fresh contexts attached together (re-attaching one rank alone desynchronises it). */
 #define TRPO_PEER_HANDLE_BYTES 64
 #define TRPO_PEER_MAX_RANKS 16
 int trpo_ctx_peer_handle(trpo_ctx *ctx, void *handle_64);
