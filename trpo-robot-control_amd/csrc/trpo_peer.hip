@@ -45,6 +45,7 @@ struct trpo_peer {
     int *err_h, *err_d;              // pinned host error word and its device view
     int rank, world;
     int uncached;                    // 1: hipDeviceMallocUncached, 0: fine-grained fallback
+    int connected;                   // windows carry the exchange numbering: one connect per window
 };
 
 static size_t win_doubles(size_t S) { return 2 * (size_t)PEER_WMAX * S + (size_t)PEER_WMAX * FLAG_STRIDE; }
@@ -182,6 +183,10 @@ void *trpo_peer_window(trpo_peer *p) { return p ? p->win : NULL; }
 // local: world window pointers of contexts in this process (rank order)
 int trpo_peer_connect(trpo_peer *p, int rank, int world, const void *handles, void *const *local, hipStream_t st) {
     if (!p || world < 1 || world > PEER_WMAX || rank < 0 || rank >= world || (!handles && !local)) return -1;
+    if (p->connected) {
+        fprintf(stderr, "[trpo_mi355x] peer window already attached (attach once per context)\n");
+        return -1;
+    }
     HCHK(hipSetDevice(p->device));
     double *w[PEER_WMAX] = {NULL};
     for (int r = 0; r < world; ++r) {
@@ -211,7 +216,8 @@ int trpo_peer_connect(trpo_peer *p, int rank, int world, const void *handles, vo
     }
     HCHK(hipMemcpyAsync(p->dwins, w, sizeof(double *) * world, hipMemcpyHostToDevice, st));
     HCHK(hipStreamSynchronize(st));
-    __atomic_store_n(p->err_h, 0, __ATOMIC_RELEASE);     // a new attach starts without a timed-out exchange
+    __atomic_store_n(p->err_h, 0, __ATOMIC_RELEASE);
+    p->connected = 1;
     p->rank = rank;
     p->world = world;
     return 0;
