@@ -76,12 +76,14 @@ peer_exchange_kernel(const double *__restrict__ in, int R, int Rstride, int coun
         for (int k = 1; k < R; ++k) v += in[(long)k * Rstride + i];
         st_sys(dst + i, v);
     }
-    // 3: every storing wave drained, then one system-scope release and the flag
+    // 3: every storing wave drained, a workgroup barrier, then the flag.  No release fence: every
+    // exchanged byte is stored and loaded at system scope (sc0 sc1) in uncached memory, so no cache
+    // holds a line to write back or invalidate -- the drained stores are in HBM before the flag
+    // store is issued (MI355X_MICROARCH.md, inter-workgroup hand-off: sc1 stores drained by every
+    // storing wave, one lane signalling behind a barrier, sc1 loads after the poll and a barrier)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         gu64 *flag = (gu64 *)(size_t)(wins[t] + 2 * (size_t)PEER_WMAX * S);
         __hip_atomic_store(flag + (size_t)rank * FLAG_STRIDE, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -101,8 +103,8 @@ peer_exchange_kernel(const double *__restrict__ in, int R, int Rstride, int coun
         }
     }
     __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    // 5: slice t of the elements, summed over the slots in rank order
+    // 5: slice t of the elements (system-scope loads of uncached memory: no acquire fence needed),
+    // summed over the slots in rank order
     const int per = (count + world - 1) / world, lo = t * per, hi = min(count, lo + per);
     const double *src = own + (size_t)set * PEER_WMAX * S;
     for (int i = lo + tid; i < hi; i += PEER_T) {
