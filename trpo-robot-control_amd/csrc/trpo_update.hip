@@ -639,15 +639,16 @@ surr_mfma_kernel(Net net, const double *__restrict__ pk, const double *__restric
     }
 }
 
-// the MFMA surrogate's shape: 3 weight layers, inputs <= 32, hidden widths 17..64 (tiles of 16),
-// <= 16 outputs; returns the instantiation index or -1
+// the MFMA surrogate's shape: 3 weight layers, inputs <= 32, hidden widths <= 64 with equal tile
+// counts (16-wide tiles), <= 16 outputs; returns the instantiation index or -1
+// (TRPO_SURR_GENERIC=1: the one-lane kernels -- the register kernel for widths <= 16)
 static int surr_mfma_shape(const Net &net) {
     const char *e = getenv("TRPO_SURR_GENERIC");
     if (e && atoi(e)) return -1;
     if (net.nl != 4 || net.L[0] > 32 || net.L[3] > 16 || net.L[1] > 64 || net.L[2] > 64) return -1;
     const int T0 = cdiv(net.L[0], 16), T1 = cdiv(net.L[1], 16), T2 = cdiv(net.L[2], 16);
-    if (T1 != T2 || T1 < 2) return -1;
-    return (T0 - 1) * 3 + (T1 - 2);      // T0 in {1, 2}, T1 = T2 in {2, 3, 4}
+    if (T1 != T2) return -1;
+    return (T0 - 1) * 4 + (T1 - 1);      // T0 in {1, 2}, T1 = T2 in {1, 2, 3, 4}
 }
 
 template <int T0, int T1>
@@ -966,14 +967,16 @@ static int enqueue_surrogate(trpo_dev *d, const double *fs, int k0, int nk) {
         const int cap2 = 512 / nk > 0 ? 512 / nk : 1, Gm = n ? (cdiv(cdiv(n, 16), SM_WAVES) < cap2 ? cdiv(cdiv(n, 16), SM_WAVES) : cap2) : 1;
         if (ensure(&u->slabs, &u->slab_cap, (size_t)Gm * nk, v.stream)) return -2;
         int rc = 0;
+#define SURR_CASE(i, a, b)                                                                                    \
+    case i: rc = launch_surr_mfma<a, b>(net, v.theta64, fs, k0, nk, &u->tpad, &u->tpad_cap, v.obs64, u->roll,    \
+                                        v.std64, n, Gm, u->slabs, v.stream);                                      \
+        break;
         switch (ms) {
-        case 0: rc = launch_surr_mfma<1, 2>(net, v.theta64, fs, k0, nk, &u->tpad, &u->tpad_cap, v.obs64, u->roll, v.std64, n, Gm, u->slabs, v.stream); break;
-        case 1: rc = launch_surr_mfma<1, 3>(net, v.theta64, fs, k0, nk, &u->tpad, &u->tpad_cap, v.obs64, u->roll, v.std64, n, Gm, u->slabs, v.stream); break;
-        case 2: rc = launch_surr_mfma<1, 4>(net, v.theta64, fs, k0, nk, &u->tpad, &u->tpad_cap, v.obs64, u->roll, v.std64, n, Gm, u->slabs, v.stream); break;
-        case 3: rc = launch_surr_mfma<2, 2>(net, v.theta64, fs, k0, nk, &u->tpad, &u->tpad_cap, v.obs64, u->roll, v.std64, n, Gm, u->slabs, v.stream); break;
-        case 4: rc = launch_surr_mfma<2, 3>(net, v.theta64, fs, k0, nk, &u->tpad, &u->tpad_cap, v.obs64, u->roll, v.std64, n, Gm, u->slabs, v.stream); break;
-        default: rc = launch_surr_mfma<2, 4>(net, v.theta64, fs, k0, nk, &u->tpad, &u->tpad_cap, v.obs64, u->roll, v.std64, n, Gm, u->slabs, v.stream); break;
+            SURR_CASE(0, 1, 1) SURR_CASE(1, 1, 2) SURR_CASE(2, 1, 3) SURR_CASE(3, 1, 4)
+            SURR_CASE(4, 2, 1) SURR_CASE(5, 2, 2) SURR_CASE(6, 2, 3) SURR_CASE(7, 2, 4)
+        default: return -1;
         }
+#undef SURR_CASE
         if (rc) return rc;
         hipLaunchKernelGGL(sum_slabs64_kernel, dim3(cdiv(nk, 16)), dim3(256), 0, v.stream, u->slabs, Gm, nk, u->sums);
         HCHK(hipGetLastError());
