@@ -1,4 +1,4 @@
-"""One rank of tests/test_gpu_peer.py::test_peer_ipc_two_processes (run as a child process):
+"""One rank of tests/test_gpu_peer.py::test_peer_ipc_processes (run as a child process):
     python tests/peer_worker.py RANK WORLD DIR
 Builds its contiguous shard of the syn_arm_cg_n50000 golden, exports its peer window handle to
 DIR/h<rank>.bin, waits for every rank's handle, attaches, solves CG and writes DIR/x<rank>.npy."""

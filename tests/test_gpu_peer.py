@@ -168,10 +168,11 @@ def test_peer_missing_rank_times_out():
             ctx.close()
 
 
-def test_peer_ipc_two_processes():
-    """One process per rank on the same GPU, windows exchanged as IPC handles through files."""
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_peer_ipc_processes(world):
+    """One process per rank on the same GPU, windows exchanged as IPC handles through files: the
+    8-rank case rehearses the protocol of an 8-GPU node (8 windows, 8 flag slots, rank-order sums)."""
     c = cases.case("syn_arm_cg_n50000")
-    world = 2
     with tempfile.TemporaryDirectory() as tmp:
         procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "peer_worker.py"), str(r), str(world), tmp],
                                   stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
@@ -188,6 +189,7 @@ def test_peer_ipc_two_processes():
             assert p.returncode == 0, o
         xs = [np.load(os.path.join(tmp, "x%d.npy" % r)) for r in range(world)]
         backends = [open(os.path.join(tmp, "backend%d.txt" % r)).read() for r in range(world)]
-    np.testing.assert_array_equal(xs[0], xs[1])
+    for r in range(1, world):
+        np.testing.assert_array_equal(xs[r], xs[0])
     assert all(b.startswith("peer-xgmi") for b in backends), backends
     assert cases.rel_l2(xs[0], cases.expected(c)) <= CG_TOL
