@@ -419,14 +419,27 @@ def _update_multi(device, dist, comm):
 
 
 def sweep(device, dist, steps=10, comm="rccl"):
-    """C4's N sweep: the same sharded 10-iteration solve at larger batches (whole-job rates)."""
+    """C4's N sweep: the same sharded 10-iteration solve at larger batches (whole-job rates).  At one
+    rank each row also carries the CG-iteration kernel's roofline at that N (HIP events, same units as
+    the headline `roofline`): the 50k headline is latency-bound, these rows show the kernel's
+    throughput regime.  At N > 1 ranks a weak-scaling row (50k samples per rank) is added."""
     from trpo_amd import synth
     out = {}
-    for n in SWEEP_N:
+    ns = list(SWEEP_N) + ([N_TOTAL * dist.world] if dist.world > 1 else [])
+    for n in ns:
         ctx, _, _ = make_ctx(ARM, n, dist, device, comm=comm)
         t = time_steps(ctx, dist, steps, 2, synth.make_b(num_params(ARM)))
-        out["cg10_armDOF_0_N%d" % n] = {"ms_per_step": 1e3 * t / steps,
-                                        "fvp_samples_per_s": CG_ITERS * n / (t / steps), "n_gpus": dist.world}
+        row = {"ms_per_step": 1e3 * t / steps, "fvp_samples_per_s": CG_ITERS * n / (t / steps),
+               "n_gpus": dist.world}
+        if dist.world > 1 and n == N_TOTAL * dist.world:
+            row["scaling"] = "weak (50000 samples per rank)"
+        if dist.world == 1:
+            k3 = ctx.time_ms(3, 5, CG_ITERS)
+            bytes_alg = bytes_per_fvp_cached(ARM, ctx.n) + bytes_cg_step(ARM)
+            row.update({"cg_iter_kernel_ms": k3, "alg_bytes_per_launch": bytes_alg,
+                        "hbm_frac_algorithmic": bytes_alg / (k3 * 1e-3) / 1e9 / PEAK_HBM_GBS,
+                        "fp32_frac": flops_per_sample_cached(ARM) * ctx.n / (k3 * 1e-3) / 1e12 / PEAK_FP32_TFLOPS})
+        out["cg10_armDOF_0_N%d" % n] = row
         ctx.close()
     return out
 
