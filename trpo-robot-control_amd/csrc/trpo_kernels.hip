@@ -2395,7 +2395,8 @@ template <typename ST>
 __global__ void __launch_bounds__(RS_THREADS)
 reduce_slabs_kernel(const ST *__restrict__ slabs, int G, int slab, const int *__restrict__ imap,
                     double *__restrict__ zacc, const int *__restrict__ skip, const double *__restrict__ vin,
-                    double *__restrict__ zout, const Ctl *__restrict__ ctl, int nw, int P) {
+                    double *__restrict__ zout, const Ctl *__restrict__ ctl, int nw, int P,
+                    double *__restrict__ zh) {
     constexpr int VE = 16 / sizeof(ST), LP = RS_POS / VE, SG = RS_THREADS / LP, NLD = 256 / SG;
     typedef ST VT __attribute__((ext_vector_type(VE)));
     __shared__ double part[SG][RS_POS + 1];
@@ -2425,12 +2426,19 @@ reduce_slabs_kernel(const ST *__restrict__ slabs, int G, int slab, const int *__
         double a = 0.0;
 #pragma unroll 8
         for (int k = 0; k < SG; ++k) a += part[k][t];
-        if (zout) zout[m] = a / ctl->n_total + ctl->damping * vin[m];   // fused FVP epilogue
-        else zacc[m] = a;
+        if (zout) {                                    // fused FVP epilogue
+            const double z = a / ctl->n_total + ctl->damping * vin[m];
+            zout[m] = z;
+            if (zh) zh[m] = z;                         // also into the caller's mapped host buffer
+        } else {
+            zacc[m] = a;
+        }
     }
     if (zout && blockIdx.x == 0 && t < P - nw) {      // log-std block: 2 v + damping v
         const double vq = vin[nw + t];
-        zout[nw + t] = 2.0 * vq + ctl->damping * vq;
+        const double z = 2.0 * vq + ctl->damping * vq;
+        zout[nw + t] = z;
+        if (zh) zh[nw + t] = z;
     }
 }
 
@@ -4022,15 +4030,16 @@ static IterArgs plain_args(trpo_dev *d, const int *skip) {
 
 // block partials (fp32, or fp64 in the fp64 mode) -> d->zacc, fixed order; with zout the FVP
 // epilogue (z = sum / N + damping v, log-std block 2 v + damping v) is applied on the way
-static void launch_reduce(trpo_dev *d, const int *skip, const double *vin = nullptr, double *zout = nullptr) {
+static void launch_reduce(trpo_dev *d, const int *skip, const double *vin = nullptr, double *zout = nullptr,
+                          double *zh = nullptr) {
     if (d->f64)
         hipLaunchKernelGGL(reduce_slabs_kernel<double>, dim3(d->slab / RS_POS), dim3(RS_THREADS), 0, d->stream,
                            (const double *)d->slabs, d->grid, d->slab, d->imap, d->zacc, skip, vin, zout, d->ctl,
-                           d->nw, d->P);
+                           d->nw, d->P, zh);
     else
         hipLaunchKernelGGL(reduce_slabs_kernel<float>, dim3(d->slab / RS_POS), dim3(RS_THREADS), 0, d->stream,
                            (const float *)d->slabs, d->grid, d->slab, d->imap, d->zacc, skip, vin, zout, d->ctl,
-                           d->nw, d->P);
+                           d->nw, d->P, zh);
 }
 
 // a standalone (never skipped) tile-kernel FVP: the first one after theta / the observations
@@ -4099,7 +4108,8 @@ static int fvp_src(trpo_dev *d, const double *src, double **zh) {
                                src, d->vec[TRPO_VEC_Z], d->P, d->Ps, d->nw, d->ctl, zhost);
             *zh = zhost;
         } else {
-            launch_reduce(d, &d->ctl->zero, src, d->vec[TRPO_VEC_Z]);
+            launch_reduce(d, &d->ctl->zero, src, d->vec[TRPO_VEC_Z], zhost);
+            *zh = zhost;
         }
         HCHK(hipGetLastError());
         return 0;
