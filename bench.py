@@ -452,10 +452,11 @@ def main():
     import numpy as np
     from trpo_amd import synth
 
-    dist = Dist()
-    if dist.world != args.gpus:
-        print("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, dist.world), file=sys.stderr)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:                       # before any rendezvous or device use
+        print("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world), file=sys.stderr)
         sys.exit(2)
+    dist = Dist()
     device = int(os.environ.get("TRPO_BENCH_DEVICE", dist.local_rank))   # override: testing only
 
     ctx, theta, obs_local = make_ctx(ARM, N_TOTAL, dist, device, comm=args.comm)
