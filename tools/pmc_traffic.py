@@ -19,7 +19,7 @@ f = per_dispatch(sys.argv[1], "FETCH_SIZE")
 w = per_dispatch(sys.argv[2], "WRITE_SIZE")
 fetch = 2.0 * statistics.median(f) * 1024
 write = statistics.median(w) * 1024
-out = {"kernel": KERNEL + " " + os.environ.get("LABEL", "(plain FVP, cached forward)"), "workload": "armDOF_0 N=50000",
+out = {"kernel": KERNEL + " " + os.environ.get("LABEL", "(plain FVP, cached forward)"), "workload": os.environ.get("WORKLOAD", "armDOF_0 N=50000"),
        "fetch_bytes": fetch, "write_bytes": write, "traffic_bytes": fetch + write,
        "raw_FETCH_SIZE_KiB": statistics.median(f), "raw_WRITE_SIZE_KiB": statistics.median(w),
        "dispatches": [len(f), len(w)], "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount)"}
