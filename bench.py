@@ -295,6 +295,7 @@ def bench_baseline(device, num_ep=20, ep_len=150, reps=50):
     from trpo_amd import synth
     L = [16, 16, 16, 1]
     x, obs, tgt = synth.make_baseline_problem(L, num_ep, ep_len)
+    from scipy.optimize import fmin_l_bfgs_b
     with trpo_amd.Baseline(L, "lttl", device=device) as b:
         b.set_data(obs, tgt, num_ep, ep_len)
         b.evaluate(x)
@@ -302,12 +303,26 @@ def bench_baseline(device, num_ep=20, ep_len=150, reps=50):
         for _ in range(reps):
             f, g = b.evaluate(x)
         dev = (time.perf_counter() - t0) / reps
+        # the whole baseline fit a trainer runs per iteration: L-BFGS (scipy's L-BFGS-B standing in for
+        # the caller's liblbfgs, at most 25 iterations) driving the device objective
+        fits = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            xd, fd, info = fmin_l_bfgs_b(lambda v: b.evaluate(v), x, maxiter=25)
+            fits.append(time.perf_counter() - t0)
     t0 = time.perf_counter()
     fo, go, _ = oracle.baseline_evaluate(L, "lttl", x, obs, tgt, num_ep, ep_len)
     cpu = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    xo, fo_fit, info_o = fmin_l_bfgs_b(lambda v: oracle.baseline_evaluate(L, "lttl", v, obs, tgt, num_ep, ep_len)[:2],
+                                       x, maxiter=25)
+    cpu_fit = time.perf_counter() - t0
     return {"evaluate_us": 1e6 * dev, "cpu_port_evaluate_us_1core": 1e6 * cpu, "samples": num_ep * ep_len,
             "grad_relL2_vs_cpu": float(np.linalg.norm(g - go) / np.linalg.norm(go)),
-            "what": "host-visible wall per L-BFGS callback incl. x upload and g/f download"}
+            "what": "host-visible wall per L-BFGS callback incl. x upload and g/f download",
+            "lbfgs_fit25_ms": 1e3 * sorted(fits)[1], "lbfgs_fit25_evals": int(info["funcalls"]),
+            "cpu_port_lbfgs_fit25_ms_1core": 1e3 * cpu_fit,
+            "fit_x_relL2_vs_cpu_fit": float(np.linalg.norm(xd - xo) / np.linalg.norm(xo))}
 
 
 def extras_single(device, dist, reps):
@@ -353,6 +368,13 @@ def extras_single(device, dist, reps):
     extra["C5_update_armDOF_0_N50000"] = bench_update(device)
     extra["C5_update_2x64_N50000"] = bench_update(device, L=L2, cpu_ref=False)
     extra["C5_baseline_evaluate_N3000"] = bench_baseline(device)
+    u, bl = extra["C5_update_armDOF_0_N50000"], extra["C5_baseline_evaluate_N3000"]
+    extra["C5_iteration_armDOF_0"] = {
+        "device_ms": u["update_ms"] + bl["lbfgs_fit25_ms"],
+        "cpu_reference_ms_1core": (1e3 * u["cpu_reference_compute_s_1core"] + bl["cpu_port_lbfgs_fit25_ms_1core"]
+                                   if "cpu_reference_compute_s_1core" in u else None),
+        "what": "sum of the two measured stages of one training iteration's learning step: TRPO_Update "
+                "(N=50000) + the L-BFGS baseline fit (at most 25 iterations, 20x150 batch); rollouts not included"}
     return extra
 
 
