@@ -2800,7 +2800,10 @@ cg_last_kernel(const double *__restrict__ acc, int R_in, const double *__restric
     for (int e = tid; e < zero_len; e += CGL_T) acc_zero[e] = 0.0;
 }
 
-constexpr int CGS_T = 256, CGS_K = 5 + QCAP;
+#ifndef TRPO_CGS_T
+#define TRPO_CGS_T 256
+#endif
+constexpr int CGS_T = TRPO_CGS_T, CGS_K = 5 + QCAP;
 template <typename QT>
 __global__ void __launch_bounds__(CGS_T)
 cg_dots_kernel(const double *__restrict__ zacc, const double *__restrict__ p, const double *__restrict__ r,
