@@ -2390,7 +2390,10 @@ fvp_generic_kernel(const float *__restrict__ obs, int n, const float *__restrict
 // layout (contiguous).  A block of 256 threads owns RS_POS consecutive slab positions; each
 // thread loads 16 B (4 fp32 / 2 fp64 positions) from every SG-th block partial (all its loads in
 // flight together), then the SG sub-sums are added in a fixed order through LDS.
-constexpr int RS_POS = 32, RS_THREADS = 256;
+#ifndef TRPO_RS_POS
+#define TRPO_RS_POS 32
+#endif
+constexpr int RS_POS = TRPO_RS_POS, RS_THREADS = 256;
 template <typename ST>
 __global__ void __launch_bounds__(RS_THREADS)
 reduce_slabs_kernel(const ST *__restrict__ slabs, int G, int slab, const int *__restrict__ imap,
