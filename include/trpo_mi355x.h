@@ -29,15 +29,23 @@
  * per-call file I/O, observations uploaded once per update, P-vectors resident
  * in HBM through the whole CG solve, optional RCCL sample sharding.
  *
- * Linkage is C; the header is safe to include from C and C++ (the reference's
- * build/Makefile.cpuonly compiles its callers with g++).
+ * Linkage.  The library exports every Part-1 entry point TWICE: with C linkage
+ * (FVPFast, CG, ...) and with C++ linkage (_Z7FVPFast9TRPOparamPdS0_m, ...;
+ * csrc/trpo_cxx_abi.cpp forwards those to the C ones).  The reference's own
+ * build/Makefile.cpuonly:5,11 compiles its callers with g++ against
+ * src/include/TRPO.h:81-104, which has no extern "C", so an UNCHANGED caller
+ * imports the mangled names and links as it is.  Included from C++, this
+ * header declares the C names by default; define TRPO_MI355X_CXX_LINKAGE to
+ * get the reference header's (C++-linkage) declarations of Part 1 instead.
+ * evaluate() and Part 2 are C linkage either way (src/include/lbfgs.h:32-34
+ * wraps the liblbfgs callback in extern "C").
  */
 #ifndef TRPO_MI355X_H
 #define TRPO_MI355X_H
 
 #include <stddef.h>
 
-#ifdef __cplusplus
+#if defined(__cplusplus) && !defined(TRPO_MI355X_CXX_LINKAGE)
 extern "C" {
 #endif
 
@@ -84,6 +92,14 @@ typedef struct {
     double *Target;          /* [NumSamples] */
     double *Predict;         /* [NumSamples], written on every call */
 } TRPOBaselineParam;
+#endif
+
+#if defined(__cplusplus) && !defined(TRPO_MI355X_CXX_LINKAGE)
+} /* extern "C" (Part 1) */
+#endif
+
+#ifdef __cplusplus
+extern "C" {
 #endif
 
 /* liblbfgs callback (double precision lbfgsfloatval_t): instance = TRPOBaselineParam*.

@@ -12,7 +12,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liboracle.so")
+# TRPO_ORACLE_LIB: another build of the same restatement (tests/test_asan.py: the ASan + UBSan one)
+LIB_PATH = os.environ.get("TRPO_ORACLE_LIB") or os.path.join(HERE, "liboracle.so")
 REF_DRIVER = os.path.join(HERE, "_ref", "ref_driver")
 REF_DRIVER_FAST = os.path.join(HERE, "_ref", "ref_driver_fast")
 

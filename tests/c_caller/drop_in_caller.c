@@ -3,8 +3,11 @@
  * entry points, the way src/TRPOCpuCode.c drives src/TRPO_FVP.c / TRPO_CG.c / TRPO_Update.c
  * (Test_FVP / Test_CG at src/TRPOCpuCode.c:15-135, Test_TRPO_Update at :314-372): a TRPOparam filled
  * field by field and passed BY VALUE, caller-owned fp64 vectors, the "< 0 means failure" return
- * convention.  Built twice by tests/c_caller/Makefile, as C (gcc) and as C++ (g++, as the reference's
- * build/Makefile.cpuonly compiles its callers), against include/trpo_mi355x.h only.
+ * convention.  Built by tests/c_caller/Makefile as C (gcc) and as C++ (g++, as the reference's
+ * build/Makefile.cpuonly compiles its callers) against include/trpo_mi355x.h -- C++ both with the C
+ * names and with TRPO_MI355X_CXX_LINKAGE (the mangled names an unchanged g++ caller imports) -- and,
+ * where /root/reference exists, as C++ against the reference's OWN src/include/TRPO.h
+ * (-DUSE_REFERENCE_HEADER): the unchanged-caller case of build/Makefile.cpuonly:5,11.
  *
  *   drop_in_caller FIXTURE_DIR OUT_DIR [NumSamples [NumThreads]]
  *
@@ -17,7 +20,11 @@
 #include <stdlib.h>
 #include <string.h>
 
+#ifdef USE_REFERENCE_HEADER
+#include "TRPO.h"
+#else
 #include "trpo_mi355x.h"
+#endif
 
 static int read_column(const char *path, int col, double *v, size_t n) {
     FILE *f = fopen(path, "r");

@@ -92,3 +92,79 @@ def test_compiled_caller_builds_and_links(compiler, tmp_path):
     syms = subprocess.run(["nm", "-D", "--undefined-only", exe], capture_output=True, text=True, check=True).stdout
     for name in ("NumParamsCalc", "FVPFast", "CG", "TRPO_Update"):
         assert re.search(r"\bU %s$" % name, syms, re.M), name
+
+
+# the seven TRPO.h:81-104 entry points and the Itanium names g++ gives them when TRPO.h is included
+# without extern "C" (build/Makefile.cpuonly:5,11 compiles every caller with g++ -std=c++11)
+MANGLED = {
+    "NumParamsCalc": "_Z13NumParamsCalcPmm",
+    "FVP": "_Z3FVP9TRPOparamPdS0_",
+    "FVPFast": "_Z7FVPFast9TRPOparamPdS0_m",
+    "CG": "_Z2CG9TRPOparamPdS0_mdm",
+    "FVP_FPGA": "_Z8FVP_FPGA9TRPOparamPdS0_",
+    "CG_FPGA": "_Z7CG_FPGA9TRPOparamPdS0_mdm",
+    "TRPO_Update": "_Z11TRPO_Update9TRPOparamPdm",
+}
+
+# a caller taking the address of every Part-1 entry point (so each is imported), header chosen by -D
+ALL_ENTRY_CALLER = textwrap.dedent("""
+    #include <stdio.h>
+    #ifdef USE_REFERENCE_HEADER
+    #include "TRPO.h"
+    #else
+    #include "trpo_mi355x.h"
+    #endif
+    int main(void) {
+        void *volatile f[] = {(void *)&NumParamsCalc, (void *)&FVP, (void *)&FVPFast, (void *)&CG,
+                     (void *)&FVP_FPGA, (void *)&CG_FPGA, (void *)&TRPO_Update};
+        size_t ls[] = {15, 16, 16, 3};
+        int all = 1;
+        for (int i = 0; i < 7; ++i) all &= f[i] != 0;
+        printf("%zu %d\\n", NumParamsCalc(ls, 4), all);
+        return NumParamsCalc(ls, 4) == 582 ? 0 : 1;
+    }
+""")
+
+
+def test_library_exports_cxx_linkage_twins():
+    """Every TRPO.h entry point is exported with C linkage AND with the C++ linkage an unchanged g++-built
+    caller of the reference's header imports (csrc/trpo_cxx_abi.cpp)."""
+    out = subprocess.run(["nm", "-D", "--defined-only", trpo_amd.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    for c_name, cxx_name in MANGLED.items():
+        assert re.search(r" T %s$" % c_name, out, re.M), c_name
+        assert re.search(r" T %s$" % cxx_name, out, re.M), cxx_name
+
+
+def _link_caller(tmp_path, defs, incdir):
+    src = tmp_path / "caller.cpp"
+    src.write_text(ALL_ENTRY_CALLER)
+    exe = str(tmp_path / "caller")
+    libdir = os.path.dirname(trpo_amd.LIB_PATH)
+    subprocess.run(["g++", "-std=c++11", "-O1", *defs, "-I", incdir, "-o", exe, str(src), "-L", libdir,
+                    "-ltrpo_mi355x", "-Wl,-rpath," + libdir], check=True)
+    und = subprocess.run(["nm", "-D", "--undefined-only", exe], capture_output=True, text=True, check=True).stdout
+    return exe, und
+
+
+def test_cxx_linkage_header_switch_links(tmp_path):
+    """include/trpo_mi355x.h with TRPO_MI355X_CXX_LINKAGE declares Part 1 as the reference's TRPO.h does;
+    the caller imports the mangled names and links against the library with nothing undefined."""
+    exe, und = _link_caller(tmp_path, ["-DTRPO_MI355X_CXX_LINKAGE"], os.path.dirname(trpo_amd.HEADER))
+    for cxx_name in MANGLED.values():
+        assert re.search(r"\bU %s$" % cxx_name, und, re.M), cxx_name
+    # NumParamsCalc is pure host code: the mangled twin runs without a GPU
+    assert subprocess.run([exe], capture_output=True, text=True).stdout.split() == ["582", "1"]
+
+
+REF_INC = "/root/reference/src/include"
+
+
+@pytest.mark.skipif(not os.path.isfile(os.path.join(REF_INC, "TRPO.h")), reason="reference header absent")
+def test_unchanged_reference_header_caller_links(tmp_path):
+    """a caller compiled exactly as build/Makefile.cpuonly:5 compiles one (g++ -std=c++11
+    against the reference's own src/include/TRPO.h, no extern "C") links with -ltrpo_mi355x."""
+    exe, und = _link_caller(tmp_path, ["-DUSE_REFERENCE_HEADER"], REF_INC)
+    for cxx_name in MANGLED.values():
+        assert re.search(r"\bU %s$" % cxx_name, und, re.M), cxx_name
+    assert subprocess.run([exe], capture_output=True, text=True).stdout.split() == ["582", "1"]

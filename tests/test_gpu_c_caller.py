@@ -21,9 +21,16 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-@pytest.mark.parametrize("binary", ["drop_in_caller_c", "drop_in_caller_cxx"])
+@pytest.mark.parametrize("binary", ["drop_in_caller_c", "drop_in_caller_cxx", "drop_in_caller_cxxmangle",
+                                    "drop_in_caller_refhdr"])
 def test_compiled_caller_on_fixtures(binary, tmp_path):
+    """_cxxmangle and _refhdr import the C++-LINKAGE entry points (_Z7FVPFast9TRPOparamPdS0_m, ...):
+    _refhdr is compiled against the reference's own src/include/TRPO.h with g++ -std=c++11, as
+    build/Makefile.cpuonly:5,11 compiles an unchanged caller; it is built only where /root/reference
+    exists (by __graft_entry__.build() in the build container, then shipped with the tree)."""
     exe = os.path.join(HERE, "c_caller", binary)
+    if binary == "drop_in_caller_refhdr" and not os.path.exists(exe):
+        pytest.skip("built only where the reference's TRPO.h exists (make -C tests/c_caller refhdr)")
     assert os.path.exists(exe), "build the callers first: make -C tests/c_caller (__graft_entry__.build)"
     p = subprocess.run([exe, cases.GOLDEN, str(tmp_path), "3150", "6"], capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]

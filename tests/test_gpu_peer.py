@@ -152,6 +152,49 @@ def test_peer_fvp_and_update():
     assert cases.rel_l2(res[0]["x"], ref["x"]) <= 1e-4
 
 
+@pytest.mark.parametrize("kind", ["2x64", "fp64"])
+def test_peer_fvp_and_update_slab_paths(kind):
+    """contexts WITHOUT atomic replica sets -- the 2x64 cooperative kernel (slab
+    reduce) and the fp64 precision mode -- must all-reduce a standalone FVP and the update's FVP(x)
+    under the peer exchange too; every rank then holds the global result (not its shard's), equal to
+    one context over all samples."""
+    layers = [15, 64, 64, 3] if kind == "2x64" else [15, 16, 16, 3]
+    prec = "fp64" if kind == "fp64" else "fp32"
+    n = 6000
+    th, obs = synth.make_theta(layers), synth.make_obs(n, layers[0])
+    std = np.ones(layers[-1])
+    P = synth.num_params(layers)
+    v = synth.make_v(P)
+    mean, action, adv = synth.make_rollout(layers, "lttl", th, obs, std)
+    with trpo_amd.Context(layers, "lttl", th, obs, std, 0.1, precision=prec) as one:
+        zref = one.fvp(v)
+        one.set_rollout(mean, action, adv)
+        ref = one.update()
+    bounds = [(0, 2500), (2500, n)]
+    ctxs = [trpo_amd.Context(layers, "lttl", th, obs[lo:hi], std, 0.1, precision=prec) for lo, hi in bounds]
+    for ctx, (lo, hi) in zip(ctxs, bounds):
+        ctx.set_rollout(mean[lo:hi], action[lo:hi], adv[lo:hi])
+
+    def work(ctx, r):
+        return ctx.fvp(v), ctx.update()
+
+    def warm(ctx):
+        ctx.fvp(v)
+        ctx.update()
+    try:
+        res = run_peer_ranks(ctxs, work, warm=warm)
+    finally:
+        for ctx in ctxs:
+            ctx.close()
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+    tol = 1e-12 if kind == "fp64" else 1e-5
+    assert cases.rel_l2(res[0][0], zref) <= tol
+    for key in ("theta", "x", "b"):
+        np.testing.assert_array_equal(res[0][1][key], res[1][1][key])
+    assert res[0][1]["accepted"] == ref["accepted"]
+    assert cases.rel_l2(res[0][1]["x"], ref["x"]) <= 1e-4
+
+
 def test_peer_missing_rank_times_out():
     """Only rank 0 of a world of 2 attaches: its exchange (the shard-size all-reduce of the attach)
     waits 3 s for rank 1, then gives up with an error -- the GPU is released, nothing hangs."""

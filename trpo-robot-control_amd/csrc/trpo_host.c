@@ -23,6 +23,7 @@
 
 #include "../../include/trpo_mi355x.h"
 #include "trpo_dev.h"
+#include "trpo_textio.h"
 
 #define MAX_LAYERS 8
 
@@ -385,87 +386,10 @@ int trpo_ctx_launch_geometry(const trpo_ctx *c, int *b, int *t, int *l) {
 /* ------------------------------------------------------------------------- */
 /* reference text formats                                                    */
 /* ------------------------------------------------------------------------- */
-static char *slurp(const char *path, size_t *len) {
-    FILE *f = fopen(path, "rb");
-    if (!f) return NULL;
-    fseek(f, 0, SEEK_END);
-    long sz = ftell(f);
-    fseek(f, 0, SEEK_SET);
-    char *buf = (char *)malloc((size_t)(sz < 0 ? 0 : sz) + 1);
-    size_t got = buf ? fread(buf, 1, (size_t)sz, f) : 0;
-    fclose(f);
-    if (!buf) return NULL;
-    buf[got] = 0;
-    if (len) *len = got;
-    return buf;
-}
-
-/* Parse up to `want` doubles from whitespace-separated text (fscanf("%lf") semantics). */
-static size_t parse_doubles(char *txt, double *out, size_t want) {
-    size_t k = 0;
-    char *p = txt;
-    while (k < want) {
-        while (*p == ' ' || *p == '\n' || *p == '\t' || *p == '\r') ++p;
-        if (!*p) break;
-        char *e;
-        double v = strtod(p, &e);
-        if (e == p) break;
-        out[k++] = v;
-        p = e;
-    }
-    return k;
-}
-
-/* Model file (src/TRPO_FVP.c:670-699): theta in flat order, one per line. */
-static int load_model(const char *path, size_t P, double *theta) {
-    char *t = slurp(path, NULL);
-    if (!t) {
-        fprintf(stderr, "[ERROR] Cannot open Model File [%s]. \n", path);
-        return -1;
-    }
-    size_t got = parse_doubles(t, theta, P);
-    free(t);
-    for (size_t i = got; i < P; ++i) theta[i] = 0.0;  /* fscanf leaves calloc'd zeros */
-    return 0;
-}
-
-/* Data file (src/TRPO_FVP.c:731-762, src/TRPO_Update.c:228-249): per sample
- * Mean[A] Std[A] Obs[O] Action[A] Adv.  Keeps Obs, the Std of the last parsed line
- * and (each optionally) Mean, Action and Adv. */
-static int load_data(const char *path, size_t O, size_t A, size_t n, double *obs, double *stdv, double *mean,
-                     double *action, double *adv) {
-    char *t = slurp(path, NULL);
-    if (!t) {
-        fprintf(stderr, "[ERROR] Cannot open Data File [%s]. \n", path);
-        return -1;
-    }
-    const size_t row = 3 * A + O + 1;
-    double *tmp = (double *)malloc(sizeof(double) * row);
-    char *p = t;
-    for (size_t s = 0; s < n; ++s) {
-        size_t got = 0;
-        while (got < row) {
-            while (*p == ' ' || *p == '\n' || *p == '\t' || *p == '\r') ++p;
-            if (!*p) break;
-            char *e;
-            double v = strtod(p, &e);
-            if (e == p) break;
-            tmp[got++] = v;
-            p = e;
-        }
-        if (got < row) { /* short file: the reference keeps whatever fscanf filled (zeros) */
-            for (size_t j = got; j < row; ++j) tmp[j] = (j >= A && j < 2 * A) ? stdv[j - A] : 0.0;
-        }
-        if (mean) memcpy(mean + s * A, tmp, A * sizeof(double));
-        memcpy(stdv, tmp + A, A * sizeof(double));
-        memcpy(obs + s * O, tmp + 2 * A, O * sizeof(double));
-        if (action) memcpy(action + s * A, tmp + 2 * A + O, A * sizeof(double));
-        if (adv) adv[s] = tmp[3 * A + O];
-    }
-    free(tmp);
-    free(t);
-    return 0;
-}
+/* slurp / load_model / load_data live in trpo_textio.c (a CPU-only unit, also built under
+ * AddressSanitizer + UBSan by `make -C oracle asan`) */
+#define load_model trpo_text_load_model
+#define load_data trpo_text_load_data
 
 /* Optional forward-pass check of the data file's Mean column (src/TRPO_FVP.c:839-844),
  * enabled with TRPO_CHECK_MEAN=1; done once when a data file is (re)loaded. */

@@ -3232,6 +3232,10 @@ struct trpo_dev {
     char name[64];
 };
 
+// this context's partial sums are one rank's share: every collective backend (RCCL, host group, peer
+// windows) counts, so FVP epilogues must wait for allreduce() whenever this holds
+static inline bool has_collective(const trpo_dev *d) { return d->comm || d->group || d->peer_on; }
+
 // ---------------------------------------------------------------------------
 // In-process host-staged all-reduce (trpo_dev_set_group).  The contexts of one process -- one
 // thread per context, on any devices -- exchange their partial sums through host memory: every rank
@@ -3282,22 +3286,26 @@ extern "C" void trpo_hgroup_destroy(trpo_hgroup *g) {
 // the same count, in the same order as the others (the library's fixed launch sequences do)
 static int hgroup_allreduce(trpo_dev *d, double *buf, size_t count) {
     trpo_hgroup *g = d->group;
+    // a local failure before the exchange still takes part in both barriers (a rank that returned
+    // early would leave the others waiting forever): it publishes count (size_t)-1, which every rank
+    // reads as a mismatch, so all of them return -4 together
+    bool ok = true;
     if (count > d->gbuf_cap) {
         if (d->gbuf) hipHostFree(d->gbuf);
         d->gbuf = NULL;
         d->gbuf_cap = 0;
-        HCHK(hipHostMalloc((void **)&d->gbuf, sizeof(double) * count, hipHostMallocDefault));
-        d->gbuf_cap = count;
+        ok = hipHostMalloc((void **)&d->gbuf, sizeof(double) * count, hipHostMallocDefault) == hipSuccess;
+        if (ok) d->gbuf_cap = count;
     }
-    HCHK(hipMemcpyAsync(d->gbuf, buf, sizeof(double) * count, hipMemcpyDeviceToHost, d->stream));
-    HCHK(hipStreamSynchronize(d->stream));
-    g->slot[d->rank] = d->gbuf;
-    g->count[d->rank] = count;
-    pthread_barrier_wait(&g->bar);                 // every rank's partial is in host memory
+    ok = ok && hipMemcpyAsync(d->gbuf, buf, sizeof(double) * count, hipMemcpyDeviceToHost, d->stream) == hipSuccess;
+    ok = ok && hipStreamSynchronize(d->stream) == hipSuccess;
+    g->slot[d->rank] = ok ? d->gbuf : NULL;
+    g->count[d->rank] = ok ? count : (size_t)-1;
+    pthread_barrier_wait(&g->bar);                 // every rank's partial (or failure) is published
     int bad = 0;
     for (int r = 0; r < g->world; ++r) bad |= g->count[r] != count;
-    double *sum = (double *)malloc(sizeof(double) * (count ? count : 1));
-    if (sum && !bad) {
+    double *sum = bad ? NULL : (double *)malloc(sizeof(double) * (count ? count : 1));
+    if (sum) {
         for (size_t i = 0; i < count; ++i) {
             double s = g->slot[0][i];
             for (int r = 1; r < g->world; ++r) s += g->slot[r][i];   // rank order: identical bits everywhere
@@ -3305,10 +3313,7 @@ static int hgroup_allreduce(trpo_dev *d, double *buf, size_t count) {
         }
     }
     pthread_barrier_wait(&g->bar);                 // every rank has read every slot
-    if (!sum || bad) {
-        free(sum);
-        return -4;
-    }
+    if (!sum) return -4;
     memcpy(d->gbuf, sum, sizeof(double) * count);
     free(sum);
     HCHK(hipMemcpyAsync(buf, d->gbuf, sizeof(double) * count, hipMemcpyHostToDevice, d->stream));
@@ -3781,7 +3786,7 @@ static int choose_replicas(trpo_dev *d) {
 // N is the global sample count: local n, or the all-reduced n under RCCL
 static int refresh_n_total(trpo_dev *d) {
     const size_t n = d->n;
-    if (d->comm || d->group || d->peer_on) {
+    if (has_collective(d)) {
         // every rank's shard size in one sum-all-reduce (rank r contributes n at slot r): N is the
         // total, and the replica sizing below reads the LARGEST shard -- both identical on all ranks
         const int W = d->world;
@@ -4102,7 +4107,7 @@ static int fvp_src(trpo_dev *d, const double *src, double **zh) {
     HCHK(hipSetDevice(d->device));
     double *zhost = *zh;
     *zh = NULL;
-    if (d->fast && (d->atomic || !(d->comm || d->group))) {
+    if (d->fast && (d->atomic || !has_collective(d))) {
         // two launches: the tile kernel gathers its direction fragments from v itself, then the
         // atomic-replica or slab reduce applies the epilogue (under RCCL after the all-reduce)
         IterArgs a = plain_args(d, &d->ctl->zero);
@@ -4318,7 +4323,9 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
         const int G = cdiv(d->Ps / 2, CGS_T);
         for (long j = 0; j < M; ++j) {
             const int cur = (int)(j & 1), nxt = (int)((j + 1) & 1);
-            IterArgs a = plain_args(d, done);
+            // K_0 runs even when cg_init found the solve already converged: it is what refreshes the
+            // forward-activation cache that trpo_dev_ycache_written() then marks valid
+            IterArgs a = plain_args(d, j == 0 ? &d->ctl->zero : done);
             a.v_nat = d->pbuf[cur];
             if (d->yc_on) a.yc = reinterpret_cast<float4 *>(d->yc);
             (j > 0 && d->yc_on ? d->k_fvp_yc : d->k_fvp)(dim3(d->grid), d->k_lds, d->stream, a, d->net);
@@ -4349,7 +4356,8 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
         // cooperative kernel: K_0 = FVP of p_0 (packed by cg_init); K_j (j >= 1) = CG step j-1 -> j
         // fused with FVP j (MODE 2); each followed by the slab reduce [+ all-reduce]
         for (long j = 0; j < M; ++j) {
-            IterArgs a = plain_args(d, done);
+            // K_0 is never skipped (see the distributed path above): it refreshes the cache
+            IterArgs a = plain_args(d, j == 0 ? &d->ctl->zero : done);
             if (j > 0) {
                 const int in = (int)((j - 1) & 1), out = (int)(j & 1);
                 a.update = 1;
@@ -4398,7 +4406,8 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
 }
 
 // Does the CG launch sequence of enqueue_cg_body(maxiter) write the forward-activation cache?  Only
-// the fused paths do, in their first FVP K_0 (launched with a.yc and never skipped); maxiter = 0
+// the fused paths do, in their first FVP K_0 (launched with a.yc and with the always-zero skip flag
+// &ctl->zero in all three fused paths, so it runs even when cg_init finds |b|^2 < resth); maxiter = 0
 // enqueues no FVP at all, and the unfused cooperative path (TRPO_COOP_FUSED=0) runs its FVPs
 // through enqueue_fvp_core without the cache.
 static bool cg_writes_ycache(const trpo_dev *d, size_t maxiter) {

@@ -11,8 +11,8 @@
 // One exchange is ONE kernel of `world` workgroups on each rank.  Workgroup t of rank r:
 //   1. sums rank r's local replicas of the vector in replica order,
 //   2. stores the sum into slot r of set (e & 1) of rank t's window (over xGMI unless t == r),
-//   3. drains its stores, fences at system scope and stores the exchange number e into rank t's
-//      flag[r],
+//   3. drains its stores (s_waitcnt vmcnt(0) in every storing wave, then a workgroup barrier; no
+//      fence -- see the kernel) and stores the exchange number e into rank t's flag[r],
 //   4. waits (bounded poll) until flag[s] of its OWN window reads e for every rank s,
 //   5. sums slice t of the elements over the world slots in RANK order into the output vector.
 // Rank-order sums give every rank the same bits (like RCCL's all-reduce, and like the in-process
@@ -44,7 +44,7 @@ struct trpo_peer {
     unsigned long long *cnt;         // [PEER_WMAX] per-workgroup exchange counters
     int *err_h, *err_d;              // pinned host error word and its device view
     int rank, world;
-    int uncached;                    // 1: hipDeviceMallocUncached, 0: fine-grained fallback
+    int uncached;                    // always 1: hipDeviceMallocUncached (creation fails without it)
     int connected;                   // windows carry the exchange numbering: one connect per window
 };
 
@@ -138,15 +138,12 @@ trpo_peer *trpo_peer_create(int device, size_t S) {
         return NULL;
     }
     const size_t bytes = sizeof(double) * win_doubles(p->S);
+    // uncached or nothing: the fence-free hand-off below is only argued for an uncached window (a
+    // fine-grained fallback would need release / acquire fences around the flag), so no fallback
     p->uncached = 1;
     if (hipExtMallocWithFlags((void **)&p->win, bytes, hipDeviceMallocUncached) != hipSuccess) {
         (void)hipGetLastError();
-        p->uncached = 0;
         p->win = NULL;
-        if (hipExtMallocWithFlags((void **)&p->win, bytes, hipDeviceMallocFinegrained) != hipSuccess) {
-            (void)hipGetLastError();
-            p->win = NULL;
-        }
     }
     bool ok = p->win && hipMemset(p->win, 0, bytes) == hipSuccess &&
               hipMalloc((void **)&p->dwins, sizeof(double *) * PEER_WMAX) == hipSuccess &&

@@ -714,14 +714,14 @@ __global__ void export_solve_kernel(const double *__restrict__ b, const double *
     if (i < H) out[3 * P + 2 + i] = hist[i];
 }
 
-// Step size of src/TRPO_Update.c:834-868 on the device, in the host code's exact arithmetic
-// (sequential, unfused fp64: the host recomputes the same values from b, x, z bit for bit):
-// shs = 0.5 sum z_i x_i, lm = sqrt(shs / max_kl), fullstep = x / lm
 // Step size of the update (src/TRPO_Update.c:836-846): shs = 0.5 x.Fx, lm = sqrt(shs / max_kl),
 // fullstep = x / lm.  One 1024-thread workgroup: strided per-thread partial sums, then the wave tree
 // and the waves in order (a fixed order, so every call gives the same bits); shs and lm go to the
 // host with the solve's results and the host uses them as they are, so its fullstep x[i] / lm is the
-// device's bit for bit (the first line-search candidate is evaluated on the device with it).
+// device's bit for bit (the first line-search candidate is evaluated on the device with it).  The
+// summation order is NOT the reference's sequential x.Fx (src/TRPO_Update.c:836-846), so shs differs
+// from it by rounding only (relative ~1e-16 of a positive sum); the update goldens' 1e-4 bound on the
+// step (tests/test_gpu_update.py) and the printed shs / lagrange lines cover it.
 constexpr int STEP_T = 1024;
 __global__ void __launch_bounds__(STEP_T)
 step_kernel(const double *__restrict__ x, const double *__restrict__ z, int P, double max_kl,
