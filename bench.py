@@ -478,6 +478,8 @@ def main():
     if world != args.gpus:                       # before any rendezvous or device use
         print("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world), file=sys.stderr)
         sys.exit(2)
+    import trpo_amd
+    trpo_amd.lib()                               # the system ROCm runtime before torch's (Dist)
     dist = Dist()
     device = int(os.environ.get("TRPO_BENCH_DEVICE", dist.local_rank))   # override: testing only
 
@@ -530,7 +532,7 @@ def main():
                                   % (dist.world, "RCCL" if args.comm == "rccl" else "peer-window"),
                    "cg_scalars": "fp64", "fvp_kernel": ctx.kernel_name, "geometry": ctx.geometry},
         "comm": {"backend": comm["backend"], "ranks": comm["world"],
-                 "replicas_per_fvp": comm["replicas"]},
+                 "replicas_per_fvp": comm["replicas"], "hip_runtime": trpo_amd.runtime_path()},
         "cg_wall_ms": ms_per_step,
         "roofline": {"bound": "hbm" if hbm_bound else "mfma",
                      "achieved": achieved_gbs if hbm_bound else achieved_tflops,

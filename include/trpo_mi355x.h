@@ -179,6 +179,11 @@ int trpo_ctx_attach_peers(trpo_ctx *ctx, int rank, int world, const void *handle
 int trpo_ctx_attach_peers_local(trpo_ctx *ctx, int rank, int world, trpo_ctx *const *all);
 /* "rccl", "peer-xgmi (...)", "host-group" or "none" */
 const char *trpo_ctx_comm_backend(const trpo_ctx *ctx);
+/* Path of the HIP runtime (libamdhip64) this library's calls resolved to.  The library is built and
+ * validated against the system ROCm (/opt/rocm); a process that loads another copy with the same
+ * soname first (e.g. the one a PyTorch wheel bundles, imported before this library) makes the
+ * library run on that one instead. */
+const char *trpo_hip_runtime_path(void);
 
 /* Host-pointer convenience entry points (copy in / compute / copy out).
  * Return elapsed seconds (>= 0) or a negative error code. */

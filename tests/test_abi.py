@@ -168,3 +168,11 @@ def test_unchanged_reference_header_caller_links(tmp_path):
     for cxx_name in MANGLED.values():
         assert re.search(r"\bU %s$" % cxx_name, und, re.M), cxx_name
     assert subprocess.run([exe], capture_output=True, text=True).stdout.split() == ["582", "1"]
+
+
+def test_library_runs_on_the_system_rocm_runtime():
+    """conftest.py loads libtrpo_mi355x.so before anything imports torch, so its HIP calls resolve to
+    the system ROCm's libamdhip64 (the one it is built against), not torch's bundled copy."""
+    import trpo_amd
+    rt = trpo_amd.runtime_path()
+    assert os.path.realpath(rt).startswith(os.path.realpath("/opt/rocm")), rt

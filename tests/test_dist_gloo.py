@@ -6,10 +6,12 @@ import socket
 
 import numpy as np
 import pytest
-import torch.distributed as dist
-import torch.multiprocessing as mp
 
 import cases
+
+# torch is imported inside the functions only: a module-level import would load torch's bundled
+# libamdhip64.so.7 into every pytest process that merely COLLECTS this file, including the GPU runs
+# (-m gpu), where libtrpo_mi355x.so must run on the system ROCm runtime (trpo_amd.lib()).
 
 
 def _free_port():
@@ -26,6 +28,7 @@ def _worker(rank, world, port, q):
     sys.path[:0] = [os.path.join(root, "trpo-robot-control_amd"), os.path.join(root, "oracle"),
                     os.path.join(root, "tests")]
     import torch
+    import torch.distributed as dist
     import oracle
     from trpo_amd import synth
     from trpo_amd.dist import shard_range
@@ -67,6 +70,7 @@ def _worker(rank, world, port, q):
 
 
 def test_sharded_cg_two_ranks_gloo():
+    import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -90,6 +94,7 @@ def _update_worker(rank, world, port, q):
     sys.path[:0] = [os.path.join(root, "trpo-robot-control_amd"), os.path.join(root, "oracle"),
                     os.path.join(root, "tests")]
     import torch
+    import torch.distributed as dist
     import oracle
     from trpo_amd import synth
     from trpo_amd.dist import shard_range
@@ -155,6 +160,7 @@ def _update_worker(rank, world, port, q):
 
 
 def test_sharded_update_two_ranks_gloo():
+    import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

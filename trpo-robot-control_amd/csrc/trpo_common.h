@@ -37,6 +37,14 @@ struct Net {
         }                                                                                  \
     } while (0)
 
+// Pinned host staging buffers that the host writes and kernels read (uploads), or kernels write and
+// the host reads (results through the mapped pointer), are allocated COHERENT.  hipHostMallocDefault
+// is non-coherent under HIP_HOST_COHERENT=0 (the default): the GPU may keep its lines in an XCD's L2,
+// and a kernel launched behind another kernel on the same queue acquires at agent scope, which does
+// not drop them -- so a host memcpy into the buffer between two calls could be read stale by the next
+// upload's copy kernel (seen as an intermittently wrong FVP direction on a few 128-B lines).
+#define TRPO_HOST_COHERENT (hipHostMallocMapped | hipHostMallocCoherent)
+
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 // fp64 tanh for the device fp64 paths (precision mode, policy gradient, line search, baseline):

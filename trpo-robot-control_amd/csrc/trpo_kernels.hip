@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <dlfcn.h>
 #include <math.h>
 #include <pthread.h>
 #include <stdarg.h>
@@ -3294,7 +3295,7 @@ static int hgroup_allreduce(trpo_dev *d, double *buf, size_t count) {
         if (d->gbuf) hipHostFree(d->gbuf);
         d->gbuf = NULL;
         d->gbuf_cap = 0;
-        ok = hipHostMalloc((void **)&d->gbuf, sizeof(double) * count, hipHostMallocDefault) == hipSuccess;
+        ok = hipHostMalloc((void **)&d->gbuf, sizeof(double) * count, TRPO_HOST_COHERENT) == hipSuccess;
         if (ok) d->gbuf_cap = count;
     }
     ok = ok && hipMemcpyAsync(d->gbuf, buf, sizeof(double) * count, hipMemcpyDeviceToHost, d->stream) == hipSuccess;
@@ -3959,6 +3960,12 @@ extern "C" int trpo_dev_comm_error(const trpo_dev *d) {
     return d && d->peer_on && trpo_peer_error(d->peer) ? -4 : 0;
 }
 
+extern "C" const char *trpo_hip_runtime_path(void) {
+    Dl_info info;
+    if (dladdr(reinterpret_cast<void *>(&hipGetDeviceCount), &info) && info.dli_fname) return info.dli_fname;
+    return "";
+}
+
 extern "C" const char *trpo_dev_comm_backend(const trpo_dev *d) {
     if (!d) return "";
     if (d->peer_on) return trpo_peer_uncached(d->peer) ? "peer-xgmi (uncached window)" : "peer-xgmi (fine-grained window)";
@@ -3984,7 +3991,7 @@ static int ensure_hst(trpo_dev *d, size_t count, bool host_writes = false) {
     if (d->hst) hipHostFree(d->hst);
     d->hst = d->hst_dev = NULL;
     d->hst_cap = 0;
-    HCHK(hipHostMalloc((void **)&d->hst, sizeof(double) * count, hipHostMallocDefault));
+    HCHK(hipHostMalloc((void **)&d->hst, sizeof(double) * count, TRPO_HOST_COHERENT));
     HCHK(hipHostGetDevicePointer((void **)&d->hst_dev, d->hst, 0));
     d->hst_cap = count;
     return 0;
@@ -4197,7 +4204,12 @@ static int allreduce(trpo_dev *d, double *buf, size_t count) {
     if (d->peer_on) {
         // in place through the staging vector (the exchange kernel's output must not alias its input)
         if (count > trpo_peer_slot(d->peer)) return -1;
-        HCHK(hipMemcpyAsync(d->ptmp, buf, sizeof(double) * count, hipMemcpyDeviceToDevice, d->stream));
+        // a copy KERNEL, not hipMemcpyAsync: under the HIP runtime torch bundles (ROCm 7.0) a
+        // device-to-device hipMemcpyAsync behind the slab reduce intermittently handed the exchange
+        // stale lines of buf (tests/test_gpu_peer.py::test_peer_fvp_and_update_slab_paths)
+        hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv((long)count, 256)), dim3(256), 0, d->stream, (const double *)buf,
+                           d->ptmp, (int)count);
+        HCHK(hipGetLastError());
         return trpo_peer_allreduce(d->peer, d->stream, d->ptmp, 1, 0, (int)count, buf, nullptr);
     }
     if (d->group) return hgroup_allreduce(d, buf, count);

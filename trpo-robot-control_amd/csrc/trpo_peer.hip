@@ -149,7 +149,7 @@ trpo_peer *trpo_peer_create(int device, size_t S) {
               hipMalloc((void **)&p->dwins, sizeof(double *) * PEER_WMAX) == hipSuccess &&
               hipMalloc((void **)&p->cnt, sizeof(unsigned long long) * PEER_WMAX) == hipSuccess &&
               hipMemset(p->cnt, 0, sizeof(unsigned long long) * PEER_WMAX) == hipSuccess &&
-              hipHostMalloc((void **)&p->err_h, sizeof(int), hipHostMallocMapped) == hipSuccess;
+              hipHostMalloc((void **)&p->err_h, sizeof(int), TRPO_HOST_COHERENT) == hipSuccess;
     if (ok) {
         *p->err_h = 0;
         ok = hipHostGetDevicePointer((void **)&p->err_d, p->err_h, 0) == hipSuccess &&

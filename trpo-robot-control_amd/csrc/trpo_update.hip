@@ -690,7 +690,7 @@ static int ensure_host(UpdState *u, size_t count) {
     if (u->hst) hipHostFree(u->hst);
     u->hst = u->hst_dev = nullptr;
     u->hst_cap = 0;
-    HCHK(hipHostMalloc((void **)&u->hst, sizeof(double) * count, hipHostMallocDefault));
+    HCHK(hipHostMalloc((void **)&u->hst, sizeof(double) * count, TRPO_HOST_COHERENT));
     HCHK(hipHostGetDevicePointer((void **)&u->hst_dev, u->hst, 0));
     u->hst_cap = count;
     return 0;
@@ -1222,7 +1222,7 @@ extern "C" int trpo_bdev_eval(trpo_bdev *b, const double *theta, double *gsum, d
         if (b->hst) hipHostFree(b->hst);
         b->hst = b->hst_dev = nullptr;
         b->hst_cap = 0;
-        HCHK(hipHostMalloc((void **)&b->hst, sizeof(double) * need, hipHostMallocDefault));
+        HCHK(hipHostMalloc((void **)&b->hst, sizeof(double) * need, TRPO_HOST_COHERENT));
         HCHK(hipHostGetDevicePointer((void **)&b->hst_dev, b->hst, 0));
         b->hst_cap = need;
     }

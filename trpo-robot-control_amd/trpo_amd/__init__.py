@@ -107,6 +107,8 @@ def lib():
     L.trpo_ctx_attach_peers_local.argtypes = [C.c_void_p, C.c_int, C.c_int, P(C.c_void_p)]
     L.trpo_ctx_surrogate.restype = C.c_int
     L.trpo_ctx_surrogate.argtypes = [C.c_void_p, _dp, C.c_int, C.c_int, _dp]
+    L.trpo_hip_runtime_path.restype = C.c_char_p
+    L.trpo_hip_runtime_path.argtypes = []
     L.trpo_ctx_comm_backend.restype = C.c_char_p
     L.trpo_ctx_comm_backend.argtypes = [C.c_void_p]
     L.trpo_ctx_fvp.restype = C.c_double
@@ -148,7 +150,22 @@ def lib():
     L.trpo_cache_clear.restype = None
     L.trpo_cache_clear.argtypes = []
     _lib = L
+    rt = runtime_path()
+    if rt and not os.path.realpath(rt).startswith(("/opt/rocm", os.path.realpath("/opt/rocm"))):
+        # torch (or another HIP user) was imported first and its bundled runtime now serves this
+        # library too: in-process multi-context peer exchanges on the slab paths gave intermittently
+        # wrong sums there (tests/test_gpu_peer.py), never on the system runtime.  Load this
+        # library before importing torch (tests/conftest.py and bench.py do).
+        import warnings
+        warnings.warn("libtrpo_mi355x.so runs on the HIP runtime %s, not the system ROCm it was built "
+                      "against; import trpo_amd and call trpo_amd.lib() before importing torch" % rt,
+                      RuntimeWarning, stacklevel=2)
     return L
+
+
+def runtime_path() -> str:
+    """Path of the libamdhip64 this library's HIP calls resolve to (trpo_hip_runtime_path)."""
+    return lib().trpo_hip_runtime_path().decode()
 
 
 MAX_BACKTRACKS = 32
