@@ -5,12 +5,17 @@ kernel (equal hidden widths 32 / 48 / 64), the generic kernel (deeper nets, wide
 random activations, sample counts that are not multiples of 16 and sigma != 1.
 
 Tolerances as the golden tests: FVP relative L2 <= 1e-5, CG / update step <= 1e-4 (fp32 FVP,
-reorthogonalised fp64 CG; tests/test_gpu_parity.py), policy gradient <= 2e-6.  One draw is held to
-a wider update bound, measured and explained: draw 23 ([4,54,26,17,5] 'lslll', generic kernel) -- the
-reference's CG on that update's right-hand side stalls at iterations 8 -> 9 (rdotr 3.97e-8 ->
-3.92e-8) and then drops 160x in its tenth step, so the returned step is the one the FVP's rounding
-decides: the fp32 FVP (~1e-7 relative) moves it 1.2e-3, while the same policy's CG on a random
-right-hand side lands 5e-7 from the reference and every other draw's update <= 6e-6
+reorthogonalised fp64 CG; tests/test_gpu_parity.py), policy gradient <= 2e-6.  Every draw also runs in
+the fp64 precision mode (tile shapes on the cooperative fp64 kernel, the rest on the generic kernel's
+fp64 instantiation): FVP <= 1e-12, update step <= 1e-4.
+One draw's fp32 update step is not asserted, measured and explained: draw 23 ([4,54,26,17,5] 'lslll',
+generic kernel) -- the reference's CG on that update's right-hand side stalls at iterations 8 -> 9
+(rdotr 3.97e-8 -> 3.92e-8) and then drops 160x in its tenth step: its own fp64 residuals have lost
+orthogonality there, so the step it returns is not the exact-arithmetic CG step.  The fp32 path's
+residual reorthogonalisation restores orthogonality and lands 1.2e-3 from it; without
+reorthogonalisation the fp32 FVP's noise leaves 3.7e-4 (tools/diag/draw23.py).  The fp64 mode runs the
+reference's plain CG (no reorthogonalisation) and reproduces the step to 1.0e-5, so for that draw it
+is the fp64 step that is held to the 1e-4 bound.  Every other draw's fp32 update is <= 6e-6
 (tools/rand_errors.py prints the table).  The draws are seeded, so a failure names a reproducible
 configuration.
 """
@@ -25,7 +30,7 @@ from trpo_amd import synth
 pytestmark = pytest.mark.gpu
 
 ACTS = "ltso"                     # linear, tanh, sigmoid, 0.1 x (the reference's four kinds)
-UPD_TOL_DRAW = {23: 2e-3}          # see the module docstring
+FP32_STALLED = {23}                # fp32 update step not asserted (module docstring); fp64 is
 
 
 def _draw(seed):
@@ -60,7 +65,6 @@ def test_random_policy_fvp_cg_update(seed):
     mean, action, adv = synth.make_rollout(layers, acts, th, obs, std, seed=500 + seed)
     ref = oracle.update(layers, acts, th, obs, mean, action, adv, std, 0.1)
     bref, _ = oracle.policy_grad(layers, acts, th, obs, mean, action, adv)
-    upd_tol = UPD_TOL_DRAW.get(seed, 1e-4)
     with trpo_amd.Context(layers, acts, th, obs, std, 0.1) as ctx:
         kname = ctx.kernel_name
         z = ctx.fvp(v)
@@ -72,6 +76,16 @@ def test_random_policy_fvp_cg_update(seed):
     assert cases.rel_l2(x, xr) <= 1e-4, what
     assert cases.rel_l2(r["b"], bref) <= 2e-6, what
     assert r["accepted"] == ref["accepted"], what
-    assert cases.rel_l2(r["x"], ref["x"]) <= upd_tol, what
+    if seed not in FP32_STALLED:
+        assert cases.rel_l2(r["x"], ref["x"]) <= 1e-4, what
+        if ref["accepted"] >= 0:
+            assert cases.rel_l2(r["theta"] - th, ref["theta"] - th) <= 1e-4, what
+    with trpo_amd.Context(layers, acts, th, obs, std, 0.1, precision="fp64") as c64:
+        z64 = c64.fvp(v)
+        c64.set_rollout(mean, action, adv)
+        r64 = c64.update()
+    assert cases.rel_l2(z64, zr) <= 1e-12, what + " fp64"
+    assert r64["accepted"] == ref["accepted"], what + " fp64"
+    assert cases.rel_l2(r64["x"], ref["x"]) <= 1e-4, what + " fp64"
     if ref["accepted"] >= 0:
-        assert cases.rel_l2(r["theta"] - th, ref["theta"] - th) <= upd_tol, what
+        assert cases.rel_l2(r64["theta"] - th, ref["theta"] - th) <= 1e-4, what + " fp64"

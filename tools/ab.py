@@ -29,18 +29,21 @@ for sname in os.environ.get("SHAPES", "arm,2x64").split(","):
         for k, val in old.items():
             if val is None: os.environ.pop(k)
             else: os.environ[k] = val
-    res = {i: {"cg": [], "k": [], "f": []} for i in range(len(mods))}
+    res = {i: {"cg": [], "k": [], "f": [], "k3": []} for i in range(len(mods))}
     xs = []
     for r in range(int(os.environ.get("ROUNDS", "5"))):
         for i, c in enumerate(ctxs):
             res[i]["cg"].append(c.time_ms(2, 20, 10, 0.0) * 1e3)
             res[i]["k"].append(c.time_ms(0, 50) * 1e3)
             res[i]["f"].append(c.time_ms(1, 50) * 1e3)
+            if sname == "arm":
+                res[i]["k3"].append(c.time_ms(3, 10, 10) * 1e3)
     for i, c in enumerate(ctxs):
         x = c.cg(b, 10, 0.0); xs.append(x)
     for i, path in enumerate(libs):
         rel = np.linalg.norm(xs[i] - xs[0]) / np.linalg.norm(xs[0])
-        print("%-5s %-40s cg10 med %.1f min %.1f us | fvp-kernel med %.2f us | fvp call med %.2f us | x vs lib0 %.1e" % (
+        print("%-5s %-40s cg10 med %.1f min %.1f us | fvp-kernel med %.2f us | fvp call med %.2f us | cg-iter kernel "
+              "med %.2f us | x vs lib0 %.1e" % (
             sname, os.path.basename(specs[i]), np.median(res[i]["cg"]), np.min(res[i]["cg"]), np.median(res[i]["k"]),
-            np.median(res[i]["f"]), rel), flush=True)
+            np.median(res[i]["f"]), np.median(res[i]["k3"]) if res[i]["k3"] else 0.0, rel), flush=True)
     for c in ctxs: c.close()

@@ -41,6 +41,9 @@
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 #define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b), (c), 0, 0, 0)
+// v_mfma_f32_4x4x1_16b_f32: 16 blocks of 4x4 with K = 1; lane l is block l / 4, supplies A_b[l % 4] and
+// B_b[l % 4], and register i of lane 4b + j accumulates A_b[i] B_b[j] (probed: tools/micro/mfma4x4.hip)
+#define MFMA4(a, b, c) __builtin_amdgcn_mfma_f32_4x4x1f32((a), (b), (c), 0, 0, 0)
 
 // Fragment-order pack layout for the 3-weight-layer fast path (offsets in floats).
 struct Pack {
@@ -459,6 +462,23 @@ __device__ __forceinline__ float act_r(int a, float y, float rx) {
     default: return rx;
     }
 }
+// fp64 twins (the generic kernel's precision mode): tanh64 (trpo_common.h) and the libm exp
+__device__ __forceinline__ double act_y(int a, double x) {
+    switch (a) {
+    case ACT_T: return tanh64(x);
+    case ACT_O: return 0.1 * x;
+    case ACT_S: return 1.0 / (1.0 + exp(-x));
+    default: return x;
+    }
+}
+__device__ __forceinline__ double act_r(int a, double y, double rx) {
+    switch (a) {
+    case ACT_T: return rx * (1.0 - y * y);
+    case ACT_O: return 0.1 * rx;
+    case ACT_S: return rx * y * (1.0 - y);
+    default: return rx;
+    }
+}
 // tanh' = 1 - y^2 as ONE explicit fma: left to the compiler, whether the product is fused
 // depends on what else uses y*y, so the recomputing (MODE 0) and cached (MODE 2) kernels could
 // round it differently -- they must agree bit for bit
@@ -685,6 +705,13 @@ __global__ void to_f32_kernel(float *dst, const double *src, int len) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e < len) dst[e] = (float)src[e];
 }
+// fp64 -> the generic path's element type (esz 4: fp32, 8: a copy)
+__global__ void to_elem_kernel(void *dst, const double *src, long len, int f64) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= len) return;
+    if (f64) reinterpret_cast<double *>(dst)[e] = src[e];
+    else reinterpret_cast<float *>(dst)[e] = (float)src[e];
+}
 
 // ---------------------------------------------------------------------------
 // Diagnostic build only (-DTRPO_STAMPS): s_memrealtime (100 MHz) stamps per block.
@@ -808,6 +835,21 @@ __device__ __forceinline__ float rowsum16(float v) {
     return v;
 }
 
+// sum of one value over the four 16-lane rows of a wave (gfx950 v_permlane32_swap, v_permlane16_swap):
+// (row 0 + row 2) + (row 1 + row 3), the same bits in every lane
+__device__ __forceinline__ float rowgroup_sum(float v) {
+    const auto h = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    const float t = __uint_as_float(h[0]) + __uint_as_float(h[1]);
+    const auto q = __builtin_amdgcn_permlane16_swap(__float_as_uint(t), __float_as_uint(t), false, false);
+    return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+}
+__device__ __forceinline__ f4 rowgroup_sum4(f4 v) {
+    f4 r;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = rowgroup_sum(v[i]);
+    return r;
+}
+
 // Transpose scratch of fvp_mlp3_kernel: scr_put writes lane (c, g)'s accumulator rows 4g + r of
 // column c (ds_write_b32), scr_get reads row c's columns 4g .. 4g + 3 (ds_read_b128).  Layout
 // (TRPO_SCR_SWZ, round 2): 16 floats per row, 16 floats of gap after every 4 rows, and the 4-float
@@ -850,7 +892,19 @@ __device__ __forceinline__ f4 scr_get(const float *scr, int row0, int c, int g) 
 // -mllvm -amdgpu-kernarg-preload-count (14 SGPRs at most besides the kernarg pointer) they arrive in
 // SGPRs at wave start, so those loads issue without waiting for a scalar load of the kernarg segment
 // (a byval aggregate is never preloaded).
-template <int T0, int T1, int T2, int T3, int ACT, int MODE, int QB = 0>
+// NO (narrow output layer, T3 == 1 and at most NO <= 4 outputs): the output layer's
+// forward / R-forward run on v_mfma_f32_4x4x1_16b_f32 -- lane (c, g) is block 4g + c / 4, column
+// c & 3: instruction s multiplies hidden neuron 4g + s of sample c by the weight row of output i in
+// register i, and a two-step permlane sum over the lane groups g completes the sum over the hidden
+// neurons, leaving outputs 0..3 of sample c in registers 0..3 of EVERY lane group (not only g = 0);
+// G2 = W2 G3 and the RGW2 / B3 contractions then run on the VALU (per-lane partials over the
+// lane's sample column, summed over the 16 columns once in the epilogue).  With 16x16x4 MFMAs the
+// 3-wide output layer took 16 of the 40 MFMAs per tile, 13/16 of their products padding.
+// NO encoding: outputs handled (NO & 7, <= 4) | 8 when RGW2 / B3 stay on the 16x16x4 contraction
+// ("lite": no per-lane partials, so no 16-column reduction in the epilogue -- the better choice when a
+// wave runs only a few tiles; the VALU partials win once the tile loop dominates, bench C4_sweep)
+constexpr int NO_MFMA_RGW2 = 8;
+template <int T0, int T1, int T2, int T3, int ACT, int MODE, int QB = 0, int NO = 0>
 __global__ void __launch_bounds__((64 * FastCfg<T0, T1, T2, T3>::WAVES))
 fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p, const double *__restrict__ k_r,
                 const double *__restrict__ k_x, const int *__restrict__ k_pslot, const void *k_q, int k_meta,
@@ -1263,6 +1317,32 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
         rFB2 = TW[C::FB2 / 4 + lane];
     }
 #define WLD(REG, EXPR) (C::REGW ? (REG) : (EXPR))
+    constexpr int NOUT = NO & 7;                            // outputs of the narrow layer (0: off)
+    static_assert(NO == 0 || (T3 == 1 && NOUT >= 1 && NOUT <= 4 && C::NT == 1), "narrow output layer");
+    constexpr int NOA = NOUT ? NOUT : 1;
+    constexpr bool NOV = NOUT && !(NO & NO_MFMA_RGW2);      // RGW2 / B3 on the VALU
+    [[maybe_unused]] f4 nFA2[T2], nVFA2[T2], w2n[T2][4];    // NO: 4x4 A operands, W2[16kt + 4g + r][0..3]
+    [[maybe_unused]] f4 nb2 = zero4, nvb2 = zero4, niv = zero4;
+    [[maybe_unused]] float acc2[T2][4][NOA], sb3n[NOA];    // NO: per-lane RGW2 / B3 partials
+    if constexpr (NO) {
+        const int lp = (c & 3) + 16 * g;                     // FA2 lane holding W2[16kt + 4g + s][c & 3]
+#pragma unroll
+        for (int kt = 0; kt < T2; ++kt) {
+            nFA2[kt] = TW[C::FA2 / 4 + kt * 64 + lp];
+            nVFA2[kt] = FV ? VW[C::VFA2 / 4 + kt * 64 + lp] : zero4;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) w2n[kt][r] = TW[C::FB2 / 4 + kt * 64 + 4 * g + r];   // FB2 lane 4g + r
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int o = 0; o < NOA; ++o) acc2[kt][r][o] = 0.0f;
+        }
+        nb2 = g == 0 ? TW[C::BI2 / 4] : zero4;               // biases enter once: row group 0 only
+        nvb2 = (FV && g == 0) ? VW[C::VB2 / 4] : zero4;
+        niv = TW[C::IV / 4];
+#pragma unroll
+        for (int o = 0; o < NOA; ++o) sb3n[o] = 0.0f;
+    }
     f4 accW0[T0][T1], accW1[T1][T2], accW2[T2][T3];
     f4 sB1[T1], sB2[T2], sB3[T3];
 #pragma unroll
@@ -1408,6 +1488,42 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
 #endif
         // ---- layer 2 (output) and G3 = act3'(Ry3 / sigma^2) ----
         f4 g3[NT][T3];
+        if constexpr (NO) {
+            // narrow: outputs 0..3 of sample c in registers 0..3 of every lane (see the kernel comment)
+            f4 a = nb2, ra = nvb2, rb = zero4;
+#pragma unroll
+            for (int kt = 0; kt < T2; ++kt)
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    if (!YC && y3_needed) a = MFMA4(nFA2[kt][s], y2[0][kt][s], a);
+                    if constexpr (FV) {
+                        ra = MFMA4(nFA2[kt][s], r2[0][kt][s], ra);
+                        rb = MFMA4(nVFA2[kt][s], y2[0][kt][s], rb);
+                    }
+                }
+            const f4 rx = FV ? rowgroup_sum4(ra + rb) : zero4;
+            f4 r3, gg, y3;
+            if constexpr (YC) {
+                y3 = y3_needed ? ycur[T1 + T2] : zero4;
+                r3 = act_r4(a3, y3, rx);
+            } else {
+                y3 = act_fwd(a3, y3_needed ? rowgroup_sum4(a) : zero4, rx, r3);
+                if (ycs && y3_needed) ycs[((long)tile * NYC + T1 + T2) * 64 + lane] = y3;
+            }
+            if constexpr (FV) {
+                gg = act_bwd(a3, y3, r3 * niv);
+            } else {
+                const int tt = min(tile, ntiles - 1);
+                const f4 dm = reinterpret_cast<const f4 *>(A.pg_d4)[(long)(tt * 16 + c) * 4];
+                const float adv = A.pg_adv[tt * 16 + c];
+                gg = act_bwd(a3, y3, (adv * dm) * reinterpret_cast<const f4 *>(A.pg_iv4)[0]);
+            }
+            g3[0][0] = live[0] ? gg : zero4;
+            if constexpr (NOV) {
+#pragma unroll
+                for (int o = 0; o < NOA; ++o) sb3n[o] += g3[0][0][o];
+            }
+        } else
 #pragma unroll
         for (int ot = 0; ot < T3; ++ot) {
             const f4 b2 = TW[C::BI2 / 4 + ot * 4 + g], vb2 = VW[C::VB2 / 4 + ot * 4 + g];
@@ -1464,13 +1580,27 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
         }
 #endif
         // ---- contraction RGW2 += Y2 . G3^T (K = 16 samples per tile) ----
+        [[maybe_unused]] f4 g3m[NT][T3];                  // G3 in the 16x16x4 layout (rows 4g + r)
+        if constexpr (NO && !NOV) {
+            g3m[0][0] = g == 0 ? g3[0][0] : zero4;
+            sB3[0] += g3m[0][0];
+        }
+        if constexpr (NOV) {
+            // per lane: hidden 16kt + 4g + r x output o of the lane's own sample column
+#pragma unroll
+            for (int kt = 0; kt < T2; ++kt)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int o = 0; o < NOA; ++o) acc2[kt][r][o] = fmaf(y2[0][kt][r], g3[0][0][o], acc2[kt][r][o]);
+        } else {
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
             float *sc = scr + t * C::SCR;
 #pragma unroll
             for (int i = 0; i < T2; ++i) scr_put(sc, 16 * i, y2[t][i], c, g);
 #pragma unroll
-            for (int i = 0; i < T3; ++i) scr_put(sc, 16 * (T2 + i), g3[t][i], c, g);
+            for (int i = 0; i < T3; ++i) scr_put(sc, 16 * (T2 + i), NO ? g3m[t][i] : g3[t][i], c, g);
         }
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
@@ -1487,6 +1617,7 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
                     for (int s = 0; s < 4; ++s) accW2[at][bt] = MFMA(ya[s], gb[bt][s], accW2[at][bt]);
             }
         }
+        }
         // ---- G2 = act2'(W2 G3) ----
         f4 g2[NT][T2];
 #pragma unroll
@@ -1494,6 +1625,13 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
             f4 a[NT];
 #pragma unroll
             for (int t = 0; t < NT; ++t) a[t] = zero4;
+            if constexpr (NO) {
+                // the fmaf chain over the outputs a 16x16x4 MFMA forms (its padded rows add zeros)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int o = 0; o < NOA; ++o) a[0][r] = fmaf(w2n[it][r][o], g3[0][0][o], a[0][r]);
+            } else
 #pragma unroll
             for (int kt = 0; kt < T3; ++kt) {
                 const f4 w = WLD(rFB2, TW[C::FB2 / 4 + (it * T3 + kt) * 64 + lane]);
@@ -1603,10 +1741,32 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
     for (int a = 0; a < T2; ++a)
 #pragma unroll
         for (int r = 0; r < 4; ++r) sB2[a][r] = rowsum16(sB2[a][r]);
+    if constexpr (NOV) {
+        // the per-lane partials summed over the 16 sample columns, then laid out as the 16x16x4
+        // contraction leaves them: RGW2 lane (c, g) register r = hidden 16kt + 4g + r x output c,
+        // B3 lane (c, g) register r = output 4g + r (row group 0 only)
+#pragma unroll
+        for (int o = 0; o < NOA; ++o) sb3n[o] = rowsum16(sb3n[o]);
+#pragma unroll
+        for (int kt = 0; kt < T2; ++kt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                float v = 0.0f;
+#pragma unroll
+                for (int o = 0; o < NOA; ++o) {
+                    const float t = rowsum16(acc2[kt][r][o]);
+                    v = c == o ? t : v;
+                }
+                accW2[kt][0][r] = v;
+            }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sB3[0][r] = (g == 0 && r < NOA) ? sb3n[r < NOA ? r : 0] : 0.0f;
+    } else {
 #pragma unroll
     for (int a = 0; a < T3; ++a)
 #pragma unroll
         for (int r = 0; r < 4; ++r) sB3[a][r] = rowsum16(sB3[a][r]);
+    }
     f4 acc[C::NACC / 4];
     {
         int k = 0;
@@ -2299,64 +2459,66 @@ fvp_coop_kernel(IterArgs A, Net net) {
 }
 
 // ---------------------------------------------------------------------------
-// Generic FVP kernel: any depth, any widths (one thread per sample, fp32).
+// Generic FVP kernel: any depth, any widths (one thread per sample; T = float, or double in the fp64
+// precision mode, which runs the reference's own arithmetic: fp64 products, tanh64).
 // Per-sample activations live in a block-private global scratch laid out
 // [row][256] so that every access is coalesced across the block.
 // ---------------------------------------------------------------------------
 constexpr int GEN_T = 256;
 
+template <typename T>
 __global__ void __launch_bounds__(GEN_T)
-fvp_generic_kernel(const float *__restrict__ obs, int n, const float *__restrict__ th, const float *__restrict__ v,
-                   const float *__restrict__ iv, float *__restrict__ scratch, int srows, float *__restrict__ slabs,
+fvp_generic_kernel(const T *__restrict__ obs, int n, const T *__restrict__ th, const T *__restrict__ v,
+                   const T *__restrict__ iv, T *__restrict__ scratch, int srows, T *__restrict__ slabs,
                    int sstride, Net net, const int *__restrict__ skip) {
     if (*skip) return;
     const int tid = threadIdx.x;
-    float *Y = scratch + (long)blockIdx.x * 3 * srows * GEN_T;
-    float *RY = Y + (long)srows * GEN_T;
-    float *RG = RY + (long)srows * GEN_T;
+    T *Y = scratch + (long)blockIdx.x * 3 * srows * GEN_T;
+    T *RY = Y + (long)srows * GEN_T;
+    T *RG = RY + (long)srows * GEN_T;
     int roff[MAXL + 1];
     roff[0] = 0;
     for (int i = 0; i < net.nl; ++i) roff[i + 1] = roff[i] + net.L[i];
-    float *slab = slabs + (long)blockIdx.x * sstride;
+    T *slab = slabs + (long)blockIdx.x * sstride;
     const int nw = net.P - net.A;
-    for (int q = tid; q < nw; q += GEN_T) slab[q] = 0.0f;
+    for (int q = tid; q < nw; q += GEN_T) slab[q] = T(0);
 
     const int npass = (n + GEN_T - 1) / GEN_T;
     for (int pass = blockIdx.x; pass < npass; pass += gridDim.x) {
         const int s = pass * GEN_T + tid;
         const bool live = s < n;
         for (int k = 0; k < net.L[0]; ++k) {
-            Y[k * GEN_T + tid] = live ? obs[(long)s * net.L[0] + k] : 0.0f;
-            RY[k * GEN_T + tid] = 0.0f;
+            Y[k * GEN_T + tid] = live ? obs[(long)s * net.L[0] + k] : T(0);
+            RY[k * GEN_T + tid] = T(0);
         }
         for (int i = 0; i + 1 < net.nl; ++i) {
             const int in = net.L[i], out = net.L[i + 1];
-            const float *W = th + net.woff[i], *B = th + net.boff[i];
-            const float *VWp = v + net.woff[i], *VB = v + net.boff[i];
+            const T *W = th + net.woff[i], *B = th + net.boff[i];
+            const T *VWp = v + net.woff[i], *VB = v + net.boff[i];
             for (int j = 0; j < out; ++j) {
-                float x = B[j], rx = VB[j];
+                T x = B[j], rx = VB[j];
                 for (int k = 0; k < in; ++k) {
-                    const float yk = Y[(roff[i] + k) * GEN_T + tid], ryk = RY[(roff[i] + k) * GEN_T + tid];
+                    const T yk = Y[(roff[i] + k) * GEN_T + tid], ryk = RY[(roff[i] + k) * GEN_T + tid];
                     x += yk * W[k * out + j];
                     rx += ryk * W[k * out + j];
                     rx += yk * VWp[k * out + j];
                 }
-                const float y = act_y(net.act[i + 1], x);
+                const T y = act_y(net.act[i + 1], x);
                 Y[(roff[i + 1] + j) * GEN_T + tid] = y;
                 RY[(roff[i + 1] + j) * GEN_T + tid] = act_r(net.act[i + 1], y, rx);
             }
         }
         const int last = net.nl - 1;
         for (int j = 0; j < net.A; ++j) {
-            const float y = Y[(roff[last] + j) * GEN_T + tid];
-            const float gg = act_r(net.act[last], y, RY[(roff[last] + j) * GEN_T + tid] * iv[j]);
-            RG[(roff[last] + j) * GEN_T + tid] = live ? gg : 0.0f;
+            const T y = Y[(roff[last] + j) * GEN_T + tid];
+            const T gg = act_r(net.act[last], y, RY[(roff[last] + j) * GEN_T + tid] * iv[j]);
+            RG[(roff[last] + j) * GEN_T + tid] = live ? gg : T(0);
         }
         for (int i = last; i >= 2; --i) {
             const int cur = net.L[i], prev = net.L[i - 1];
-            const float *W = th + net.woff[i - 1];
+            const T *W = th + net.woff[i - 1];
             for (int j = 0; j < prev; ++j) {
-                float t = 0.0f;
+                T t = T(0);
                 for (int k = 0; k < cur; ++k) t += W[j * cur + k] * RG[(roff[i] + k) * GEN_T + tid];
                 RG[(roff[i - 1] + j) * GEN_T + tid] = act_r(net.act[i - 1], Y[(roff[i - 1] + j) * GEN_T + tid], t);
             }
@@ -2368,13 +2530,13 @@ fvp_generic_kernel(const float *__restrict__ obs, int n, const float *__restrict
             while (i + 2 < net.nl && q >= net.woff[i + 1]) ++i;
             const int in = net.L[i], out = net.L[i + 1];
             const int local = q - net.woff[i];
-            float acc = 0.0f;
+            T acc = T(0);
             if (local < in * out) {
                 const int a = local / out, b = local % out;
-                const float *ya = Y + (long)(roff[i] + a) * GEN_T, *gb = RG + (long)(roff[i + 1] + b) * GEN_T;
+                const T *ya = Y + (long)(roff[i] + a) * GEN_T, *gb = RG + (long)(roff[i + 1] + b) * GEN_T;
                 for (int t = 0; t < GEN_T; ++t) acc += ya[t] * gb[t];
             } else {
-                const float *gb = RG + (long)(roff[i + 1] + local - in * out) * GEN_T;
+                const T *gb = RG + (long)(roff[i + 1] + local - in * out) * GEN_T;
                 for (int t = 0; t < GEN_T; ++t) acc += gb[t];
             }
             slab[q] += acc;
@@ -2987,10 +3149,10 @@ cg_axpy_kernel(const double *__restrict__ dots, int G, const double *__restrict_
 // ===========================================================================
 typedef void (*fast_launch_fn)(dim3, int, hipStream_t, const IterArgs &, const Net &);
 
-template <int T0, int T1, int T2, int T3, int ACT, int MODE, int QB = 0>
+template <int T0, int T1, int T2, int T3, int ACT, int MODE, int QB = 0, int NO = 0>
 static void fast_launch(dim3 g, int lds, hipStream_t st, const IterArgs &a, const Net &net) {
     const int meta = (a.Ps & 0xFFFFF) | ((a.R_in & 63) << 20) | ((a.nq & 63) << 26);
-    hipLaunchKernelGGL((fvp_mlp3_kernel<T0, T1, T2, T3, ACT, MODE, QB>), g, dim3(64 * FastCfg<T0, T1, T2, T3>::WAVES),
+    hipLaunchKernelGGL((fvp_mlp3_kernel<T0, T1, T2, T3, ACT, MODE, QB, NO>), g, dim3(64 * FastCfg<T0, T1, T2, T3>::WAVES),
                        lds, st, a.acc_in, a.p_in, a.r_in, a.x, a.pslot, (const void *)a.q, meta, a, net);
 }
 // MODE 3 kernels by the reorthogonalisation basis they load in their prologue (QB slots)
@@ -3017,38 +3179,39 @@ static int cg_E(int P) {
         if (d->f64) CG_DISPATCH_T(E, double, KERNEL, __VA_ARGS__)                     \
         else CG_DISPATCH_T(E, float, KERNEL, __VA_ARGS__)                             \
     } while (0)
-template <int T0, int T1, int T2, int T3, int ACT>
+template <int T0, int T1, int T2, int T3, int ACT, int NO = 0>
 static hipError_t fast_attr(int lds) {
-    hipError_t e = hipFuncSetAttribute((const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 0>,
+    hipError_t e = hipFuncSetAttribute((const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 0, 0, NO>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     if constexpr (FastCfg<T0, T1, T2, T3>::REGW) {
-        e = hipFuncSetAttribute((const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 2>,
+        e = hipFuncSetAttribute((const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 2, 0, NO>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return e;
-        const void *k3[4] = {(const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 3, kQB[0]>,
-                             (const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 3, kQB[1]>,
-                             (const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 3, kQB[2]>,
-                             (const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 3, kQB[3]>};
+        const void *k3[4] = {(const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 3, kQB[0], NO>,
+                             (const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 3, kQB[1], NO>,
+                             (const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 3, kQB[2], NO>,
+                             (const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 3, kQB[3], NO>};
         for (const void *k : k3) {
             e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
             if (e != hipSuccess) return e;
         }
     }
-    return hipFuncSetAttribute((const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 1>,
+    return hipFuncSetAttribute((const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 1, 0, NO>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 }
 
 // MODE 2 (forward cache) exists for the register-resident small-net shapes only
-template <int T0, int T1, int T2, int T3, int ACT, int MODE, int QB = 0>
+template <int T0, int T1, int T2, int T3, int ACT, int MODE, int QB = 0, int NO = 0>
 static constexpr fast_launch_fn yc_launch() {
-    if constexpr (FastCfg<T0, T1, T2, T3>::REGW) return fast_launch<T0, T1, T2, T3, ACT, MODE, QB>;
+    if constexpr (FastCfg<T0, T1, T2, T3>::REGW) return fast_launch<T0, T1, T2, T3, ACT, MODE, QB, NO>;
     else return nullptr;
 }
 
 struct FastEntry {
     int T[4];
     int act;                     // -1: run-time activations
+    int no;                      // narrow output layer, the kernels' NO (0: 16x16x4 output layer)
     fast_launch_fn launch;
     fast_launch_fn launch_pg;    // MODE 1: policy gradient
     fast_launch_fn launch_yc;    // MODE 2: FVP on the cached forward activations
@@ -3058,21 +3221,29 @@ struct FastEntry {
 };
 
 #define ACT_TTL (ACT_T | (ACT_T << 2) | (ACT_L << 4))
-#define FAST_ENTRY(a, b, c, d, act)                                                                               \
-    {{a, b, c, d}, act, fast_launch<a, b, c, d, act, 0>, fast_launch<a, b, c, d, act, 1>,                         \
-     yc_launch<a, b, c, d, act, 2>(),                                                                             \
-     {yc_launch<a, b, c, d, act, 3, kQB[0]>(), yc_launch<a, b, c, d, act, 3, kQB[1]>(),                           \
-      yc_launch<a, b, c, d, act, 3, kQB[2]>(), yc_launch<a, b, c, d, act, 3, kQB[3]>()}, fast_attr<a, b, c, d, act>, \
+#define FAST_ENTRY_NO(a, b, c, d, act, no)                                                                        \
+    {{a, b, c, d}, act, no, fast_launch<a, b, c, d, act, 0, 0, no>, fast_launch<a, b, c, d, act, 1, 0, no>,       \
+     yc_launch<a, b, c, d, act, 2, 0, no>(),                                                                      \
+     {yc_launch<a, b, c, d, act, 3, kQB[0], no>(), yc_launch<a, b, c, d, act, 3, kQB[1], no>(),                   \
+      yc_launch<a, b, c, d, act, 3, kQB[2], no>(), yc_launch<a, b, c, d, act, 3, kQB[3], no>()},                  \
+     fast_attr<a, b, c, d, act, no>,                                                                              \
      FastCfg<a, b, c, d>::lds_bytes(), FastCfg<a, b, c, d>::TLEN, FastCfg<a, b, c, d>::VLEN,                      \
      FastCfg<a, b, c, d>::SLAB, FastCfg<a, b, c, d>::EMAX, FastCfg<a, b, c, d>::WAVES}
+#define FAST_ENTRY(a, b, c, d, act) FAST_ENTRY_NO(a, b, c, d, act, 0)
 #define FAST_SHAPE(a, b, c, d) FAST_ENTRY(a, b, c, d, ACT_TTL), FAST_ENTRY(a, b, c, d, -1)
+// narrow output layer (<= 3 or <= 4 outputs; VALU or MFMA RGW2) of the register-resident small-net shape
+#define FAST_NO_PAIR(a, b, c, d, act, no) FAST_ENTRY_NO(a, b, c, d, act, no), FAST_ENTRY_NO(a, b, c, d, act, no | NO_MFMA_RGW2)
+#define FAST_SHAPE_NO(a, b, c, d)                                                                                 \
+    FAST_NO_PAIR(a, b, c, d, ACT_TTL, 3), FAST_NO_PAIR(a, b, c, d, -1, 3), FAST_NO_PAIR(a, b, c, d, ACT_TTL, 4),   \
+        FAST_NO_PAIR(a, b, c, d, -1, 4)
 
 static const FastEntry kFast[] = {
 #ifdef TRPO_ARM_ONLY    // experiment builds (make variant): armDOF_0-class shapes only, fast to compile
-    FAST_ENTRY(1, 1, 1, 1, ACT_TTL),
+    FAST_ENTRY(1, 1, 1, 1, ACT_TTL), FAST_NO_PAIR(1, 1, 1, 1, ACT_TTL, 3),
 #else
     FAST_SHAPE(1, 1, 1, 1), FAST_SHAPE(1, 2, 2, 1), FAST_SHAPE(1, 4, 4, 1),
     FAST_SHAPE(2, 1, 1, 1), FAST_SHAPE(2, 2, 2, 1), FAST_SHAPE(2, 4, 4, 1),
+    FAST_SHAPE_NO(1, 1, 1, 1),
 #endif
 };
 
@@ -3142,6 +3313,7 @@ struct trpo_dev {
     int Ps;                     // even row stride of replica sets and the basis: P rounded up to even
     // fast path
     const FastEntry *fast;
+    const FastEntry *fast_no[2];  // narrow-output twins of fast: [0] MFMA RGW2 (few tiles per wave), [1] VALU RGW2
     const CoopEntry *coop_e;    // cooperative kernel for wide hidden layers (else NULL)
     int coop;
     int coop_fused;             // CG step fused into the cooperative FVP kernel (MODE 2)
@@ -3170,7 +3342,7 @@ struct trpo_dev {
     size_t yc_cap;              // bytes
     int yc_on, yc_valid;
     // generic path
-    float *th32, *v32, *iv32, *obs32, *scratch;
+    void *gth, *gv, *giv, *gobs, *scratch;   // generic path: theta, direction, 1/sigma^2, observations (esz)
     int srows;
     size_t scratch_blocks;
     // common
@@ -3336,6 +3508,34 @@ static int act_code(char a) {
 
 extern "C" size_t trpo_dev_num_params(const trpo_dev *d) { return d ? (size_t)d->P : 0; }
 
+static void name_fast(trpo_dev *d) {
+    const int *T = d->fast->T;
+    const int no = d->coop ? 0 : d->fast->no;
+    snprintf(d->name, sizeof d->name, "mfma-mlp3 %dx%dx%dx%d%s%s%s%s", T[0], T[1], T[2], T[3],
+             d->fast->act >= 0 ? " ttl" : "", d->coop ? " coop" : "", d->f64 ? " fp64" : "",
+             !no ? "" : (no & NO_MFMA_RGW2) ? " no-mfma" : " no-valu");
+}
+
+// the narrow-output twin for n local samples: RGW2 on the VALU once every wave runs several tiles
+// (its 16-column epilogue reduction then amortises; measured crossover between 50k and 500k samples on
+// 256 blocks of 8 waves, TRPO_NO_VALU_MIN_TILES), else on the 16x16x4 contraction
+static void bind_fast_no(trpo_dev *d) {
+    if (!d->fast_no[0]) return;
+    const char *e = getenv("TRPO_NO_VALU_MIN_TILES");
+    const long min_tiles = e ? atol(e) : 4;
+    const long tiles_per_wave = cdiv(cdiv((long)d->n, 16), (long)d->grid * d->fast_no[0]->waves);
+    const FastEntry *f = d->fast_no[tiles_per_wave >= min_tiles ? 1 : 0];
+    if (f == d->fast) return;
+    d->fast = f;
+    d->k_fvp = f->launch;
+    d->k_pg = f->launch_pg;
+    d->k_fvp_yc = f->launch_yc;
+    d->k_cg_yc = f->launch_yc_cg[0];
+    for (int i = 0; i < 4; ++i) d->k_cg_yc_q[i] = f->launch_yc_cg[i];
+    d->yc_valid = 0;                                   // the two twins lay the y3 cache out alike, but be safe
+    name_fast(d);
+}
+
 extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, const char *ac, char *err,
                                      size_t errlen) {
 #define FAIL(...)                                      \
@@ -3391,14 +3591,14 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
     if (d->P > 32 * 1024) FAIL("NumParams=%d exceeds the 32768 supported by the device CG", d->P);
 
     // pick the kernel family
-    d->fast = NULL;
+    d->fast = d->fast_no[0] = d->fast_no[1] = NULL;
     if (nl == 4) {
         int T[4];
         for (int i = 0; i < 4; ++i) T[i] = cdiv(n.L[i], 16);
         const FastEntry *best = NULL;
         const int act = n.act[1] | (n.act[2] << 2) | (n.act[3] << 4);
         for (const FastEntry &f : kFast) {
-            bool ok = f.act < 0 || f.act == act;
+            bool ok = (f.act < 0 || f.act == act) && f.no == 0;
             for (int i = 0; i < 4; ++i) ok = ok && f.T[i] >= T[i];
             if (!ok) continue;
             int cost = f.T[0] * f.T[1] + f.T[1] * f.T[2] + f.T[2] * f.T[3];
@@ -3406,9 +3606,23 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
             if (cost < bcost || (cost == bcost && best && best->act < 0 && f.act >= 0)) best = &f;
         }
         d->fast = best;
+        // the narrow output layer's twins of that kernel (TRPO_NARROW_OUT, default on) where the
+        // outputs fit: <= 3 -> the 3-output kernels, 4 -> the 4-output ones; set_obs picks one by N
+        const char *eno = getenv("TRPO_NARROW_OUT");
+        const int want = (!best || (eno && atoi(eno) == 0)) ? 0 : n.L[3] <= 3 ? 3 : n.L[3] <= 4 ? 4 : 0;
+        d->fast_no[0] = d->fast_no[1] = NULL;
+        if (want)
+            for (const FastEntry &f : kFast) {
+                bool same = f.act == best->act;
+                for (int i = 0; i < 4; ++i) same = same && f.T[i] == best->T[i];
+                if (same && f.no == (want | NO_MFMA_RGW2)) d->fast_no[0] = &f;
+                if (same && f.no == want) d->fast_no[1] = &f;
+            }
+        if (!d->fast_no[0] || !d->fast_no[1]) d->fast_no[0] = d->fast_no[1] = NULL;
+        if (d->fast_no[0]) d->fast = d->fast_no[0];
     }
     const char *force = getenv("TRPO_FORCE_GENERIC");
-    if (force && atoi(force)) d->fast = NULL;
+    if (force && atoi(force)) d->fast = d->fast_no[0] = d->fast_no[1] = NULL;
     {
         // precision mode: "fp64" runs the FVP in fp64 (v_mfma_f64_16x16x4_f64) -- the reference's
         // own precision -- through the cooperative kernel, which covers every tile-kernel shape
@@ -3416,7 +3630,6 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
         d->f64 = ep && (strcmp(ep, "fp64") == 0 || strcmp(ep, "64") == 0 || strcmp(ep, "double") == 0);
         if (ep && !d->f64 && strcmp(ep, "fp32") != 0 && strcmp(ep, "32") != 0 && strcmp(ep, "float") != 0)
             FAIL("TRPO_PRECISION=%s: expected fp32 or fp64", ep);
-        if (d->f64 && !d->fast) FAIL("TRPO_PRECISION=fp64 needs a 3-layer network with widths <= 64");
         d->esz = d->f64 ? sizeof(double) : sizeof(float);
     }
 
@@ -3451,8 +3664,12 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
     {
         const char *el = getenv("TRPO_CG_LAST");
         d->no_cg_last = el && atoi(el) == 0;
+        // residual reorthogonalisation counters the fp32 FVP's direction-dependent noise; the
+        // fp64 mode has none to counter and runs the reference's plain CG: where the reference's own
+        // fp64 CG loses orthogonality (random-shape draw 23: a stalled solve), reorthogonalising would
+        // move the step 1.2e-3 AWAY from the reference (1.0e-5 without; tools/diag/draw23.py)
         const char *eo = getenv("TRPO_CG_REORTH");
-        d->reorth = !(eo && atoi(eo) == 0);
+        d->reorth = eo ? atoi(eo) != 0 : !d->f64;
     }
     DMALLOC(d->pacc, sizeof(double) * 2 * d->R * d->Ps);
     d->Rc = d->R;
@@ -3493,6 +3710,8 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
         hipLaunchKernelGGL(build_maps_kernel, dim3(cdiv(len, 256)), dim3(256), 0, d->stream, n, pk, d->tmap, d->vmap,
                            d->f64);
         if (d->fast->attr(d->fast->lds) != hipSuccess) FAIL("hipFuncSetAttribute(LDS=%d) failed", d->fast->lds);
+        if (d->fast_no[1] && d->fast_no[1]->attr(d->fast_no[1]->lds) != hipSuccess)
+            FAIL("hipFuncSetAttribute(LDS=%d) failed", d->fast_no[1]->lds);
         d->k_fvp = d->fast->launch;
         d->k_pg = d->fast->launch_pg;
         d->k_lds = d->fast->lds;
@@ -3551,20 +3770,20 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
             }
             d->yc_on = d->k_fvp_yc && d->k_cg_yc && !(ey && atoi(ey) == 0);
         }
-        snprintf(d->name, sizeof d->name, "mfma-mlp3 %dx%dx%dx%d%s%s%s", T[0], T[1], T[2], T[3],
-                 d->fast->act >= 0 ? " ttl" : "", d->coop ? " coop" : "", d->f64 ? " fp64" : "");
+        if (d->coop) d->fast_no[0] = d->fast_no[1] = NULL;
+        name_fast(d);
     } else {
-        DMALLOC(d->th32, sizeof(float) * d->P);
-        DMALLOC(d->v32, sizeof(float) * d->P);
-        DMALLOC(d->iv32, sizeof(float) * n.A);
+        d->esz = d->f64 ? sizeof(double) : sizeof(float);
+        DMALLOC(d->gth, d->esz * d->P);
+        DMALLOC(d->gv, d->esz * d->P);
+        DMALLOC(d->giv, d->esz * n.A);
         int rows = 0;
         for (int i = 0; i < n.nl; ++i) rows += n.L[i];
         d->srows = rows;
         d->slab = cdiv(d->P, RS_POS) * RS_POS;           // row stride of the block partials
         DMALLOC(d->imap, sizeof(int) * d->slab);
         hipLaunchKernelGGL(iota_kernel, dim3(cdiv(d->slab, 256)), dim3(256), 0, d->stream, d->imap, d->slab, d->nw);
-        snprintf(d->name, sizeof d->name, "generic");
-        d->esz = sizeof(float);
+        snprintf(d->name, sizeof d->name, "generic%s", d->f64 ? " fp64" : "");
     }
     if (hipStreamSynchronize(d->stream) != hipSuccess) FAIL("initialisation kernels failed");
     d->damping = 0.1;
@@ -3587,7 +3806,7 @@ extern "C" void trpo_dev_destroy(trpo_dev *d) {
     if (d->comm) ncclCommDestroy(d->comm);
     trpo_peer_destroy(d->peer);
     trpo_update_state_free(d->upd);
-    void *ptrs[] = {d->zbuf, d->dotsbuf, d->obs64, d->pg_d, d->pg_adv, d->pg_iv, d->st, d->pbuf[0], d->pbuf[1], d->rbuf[0], d->rbuf[1], d->accbuf, d->pacc, d->imap, d->tpack, d->vpack, d->tmap, d->vmap, d->pslot, d->islot, d->obs4, d->yc, d->th32, d->v32, d->iv32, d->obs32, d->scratch,
+    void *ptrs[] = {d->zbuf, d->dotsbuf, d->obs64, d->pg_d, d->pg_adv, d->pg_iv, d->st, d->pbuf[0], d->pbuf[1], d->rbuf[0], d->rbuf[1], d->accbuf, d->pacc, d->imap, d->tpack, d->vpack, d->tmap, d->vmap, d->pslot, d->islot, d->obs4, d->yc, d->gth, d->gv, d->giv, d->gobs, d->scratch,
                     d->theta64, d->std64, d->r, d->zacc, d->slabs, d->ctl, d->hist, d->tscr, d->qbuf, d->qzero, d->zred, d->ptmp, d->pn};
     for (void *p : ptrs)
         if (p) hipFree(p);
@@ -3625,7 +3844,8 @@ extern "C" int trpo_dev_set_theta(trpo_dev *d, const double *theta) {
         hipLaunchKernelGGL(gather_pack_kernel, dim3(cdiv(d->pack.iv, 256)), dim3(256), 0, d->stream, d->tpack,
                            d->theta64, d->tmap, d->pack.iv, d->f64);
     } else {
-        hipLaunchKernelGGL(to_f32_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, d->th32, d->theta64, d->P);
+        hipLaunchKernelGGL(to_elem_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, d->gth, d->theta64,
+                           (long)d->P, d->f64);
     }
     HCHK(hipGetLastError());
     HCHK(hipStreamSynchronize(d->stream));
@@ -3643,8 +3863,8 @@ extern "C" int trpo_dev_set_std(trpo_dev *d, const double *stdv) {
         hipLaunchKernelGGL(set_invvar_kernel, dim3(1), dim3(cdiv(len, 64) * 64), 0, d->stream,
                            (void *)((char *)d->tpack + d->esz * d->pack.iv), d->std64, d->net.A, len, d->f64);
     } else {
-        hipLaunchKernelGGL(set_invvar_kernel, dim3(cdiv(d->net.A, 256)), dim3(256), 0, d->stream, (void *)d->iv32,
-                           d->std64, d->net.A, d->net.A, 0);
+        hipLaunchKernelGGL(set_invvar_kernel, dim3(cdiv(d->net.A, 256)), dim3(256), 0, d->stream, d->giv,
+                           d->std64, d->net.A, d->net.A, d->f64);
     }
     HCHK(hipGetLastError());
     HCHK(hipStreamSynchronize(d->stream));
@@ -3696,6 +3916,7 @@ extern "C" int trpo_dev_set_obs(trpo_dev *d, const double *obs, size_t n) {
     d->n = n;
     d->grid = choose_grid(d);
     choose_reduction(d);
+    bind_fast_no(d);
     if (d->fast) {
         const size_t npad = (size_t)cdiv((long)n, 16) * 16 + 16;
         const int ld = 16 * d->pack.T[0];
@@ -3721,15 +3942,15 @@ extern "C" int trpo_dev_set_obs(trpo_dev *d, const double *obs, size_t n) {
         }
     } else {
         if ((size_t)n * L0 > d->npad_cap) {
-            if (d->obs32) hipFree(d->obs32);
-            HCHK(hipMalloc((void **)&d->obs32, sizeof(float) * (n * L0 + 1)));
+            if (d->gobs) hipFree(d->gobs);
+            HCHK(hipMalloc((void **)&d->gobs, d->esz * (n * L0 + 1)));
             d->npad_cap = n * L0;
         }
-        if (n) hipLaunchKernelGGL(to_f32_kernel, dim3(cdiv((long)n * L0, 256)), dim3(256), 0, d->stream, d->obs32,
-                                  tmp, (int)(n * L0));
+        if (n) hipLaunchKernelGGL(to_elem_kernel, dim3(cdiv((long)n * L0, 256)), dim3(256), 0, d->stream, d->gobs,
+                                  tmp, (long)n * L0, d->f64);
         if ((size_t)d->grid > d->scratch_blocks) {
             if (d->scratch) hipFree(d->scratch);
-            HCHK(hipMalloc((void **)&d->scratch, sizeof(float) * 3 * (size_t)d->srows * GEN_T * d->grid));
+            HCHK(hipMalloc((void **)&d->scratch, d->esz * 3 * (size_t)d->srows * GEN_T * d->grid));
             d->scratch_blocks = d->grid;
         }
     }
@@ -4085,6 +4306,20 @@ static double *launch_fvp_plain(trpo_dev *d, IterArgs &a, bool sink = false) {
     return acc;
 }
 
+// the generic kernel on the context's element type (d->gv already holds the direction)
+static void launch_generic(trpo_dev *d, const int *skip) {
+    if (d->f64)
+        hipLaunchKernelGGL(fvp_generic_kernel<double>, dim3(d->grid), dim3(GEN_T), 0, d->stream,
+                           (const double *)d->gobs, (int)d->n, (const double *)d->gth, (const double *)d->gv,
+                           (const double *)d->giv, (double *)d->scratch, d->srows, (double *)d->slabs, d->slab, d->net,
+                           skip);
+    else
+        hipLaunchKernelGGL(fvp_generic_kernel<float>, dim3(d->grid), dim3(GEN_T), 0, d->stream,
+                           (const float *)d->gobs, (int)d->n, (const float *)d->gth, (const float *)d->gv,
+                           (const float *)d->giv, (float *)d->scratch, d->srows, (float *)d->slabs, d->slab, d->net,
+                           skip);
+}
+
 // enqueue: partial sums of F*src into d->zacc (global over ranks)
 static int enqueue_fvp_core(trpo_dev *d, const double *src, const int *skip) {
     const Net &n = d->net;
@@ -4095,9 +4330,9 @@ static int enqueue_fvp_core(trpo_dev *d, const double *src, const int *skip) {
         else d->k_fvp(dim3(d->grid), d->k_lds, d->stream, a, n);
         HCHK(hipGetLastError());
     } else {
-        hipLaunchKernelGGL(to_f32_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, d->v32, src, d->P);
-        hipLaunchKernelGGL(fvp_generic_kernel, dim3(d->grid), dim3(GEN_T), 0, d->stream, d->obs32, (int)d->n,
-                           d->th32, d->v32, d->iv32, d->scratch, d->srows, (float *)d->slabs, d->slab, n, skip);
+        hipLaunchKernelGGL(to_elem_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, d->gv, src, (long)d->P,
+                           d->f64);
+        launch_generic(d, skip);
         HCHK(hipGetLastError());
     }
     launch_reduce(d, skip);
@@ -4174,9 +4409,7 @@ extern "C" int trpo_dev_fvp_kernel(trpo_dev *d) {
         a.v_nat = d->vec[TRPO_VEC_V];                  // the same launch as the FVP call's
         launch_fvp_plain(d, a, true);                  // no epilogue follows: accumulate into the sink
     } else {
-        hipLaunchKernelGGL(fvp_generic_kernel, dim3(d->grid), dim3(GEN_T), 0, d->stream, d->obs32, (int)d->n,
-                           d->th32, d->v32, d->iv32, d->scratch, d->srows, (float *)d->slabs, d->slab, d->net,
-                           &d->ctl->zero);
+        launch_generic(d, &d->ctl->zero);
     }
     HCHK(hipGetLastError());
     return 0;
