@@ -5,6 +5,7 @@ v_mfma_f32_4x4x1_16b_f32 and G2 = W2 G3 on the VALU; its two twins differ in the
 contraction -- on the 16x16x4 MFMA ("no-mfma", few tiles per wave) or as per-lane VALU partials
 ("no-valu", many tiles per wave) -- and set_obs picks one by tiles per wave
 (TRPO_NO_VALU_MIN_TILES, default 4).  TRPO_NARROW_OUT=0 keeps the 16x16x4 output layer.
+Also the cooperative kernel's narrow output layer (wide hidden layers: no4 coop).
 Checked: both twins against the oracle (FVP, CG, policy gradient, full update) for 1..4 outputs and
 every output activation, the forward cache bit for bit against recomputing for both twins, agreement
 with the 16x16x4 output layer to fp32 rounding, the per-N choice, and that a context re-binds its twin
@@ -114,3 +115,42 @@ def test_twin_follows_n_and_rebinds(monkeypatch):
     zr, _ = oracle.fvp(L, "lttl", th, big, std, v)
     assert cases.rel_l2(z_big, zr) <= FVP_TOL
     assert np.all(np.isfinite(x_big))
+
+
+@pytest.mark.parametrize("L,acts", [([15, 64, 64, 3], "lttl"), ([20, 32, 32, 4], "lstl"), ([30, 48, 48, 2], "ltol"),
+                                    ([15, 64, 64, 3], "ltts")])
+def test_cooperative_kernel_narrow_output(L, acts, monkeypatch):
+    """The cooperative kernel's narrow output layer ("no4 coop", fp32, <= 4 outputs): FVP / CG / update
+    against the oracle, the forward cache bit for bit against recomputing, and the 16x16x4 output layer
+    (TRPO_NARROW_OUT=0) to fp32 rounding."""
+    n = 3001
+    th, obs, std, v, b = _problem(L, acts, n, seed=11)
+    zr, _ = oracle.fvp(L, acts, th, obs, std, v)
+    xr = oracle.cg(L, acts, th, obs, std, b, 10, 0.0)["x"]
+    mean, action, adv = synth.make_rollout(L, acts, th, obs, std)
+    ref = oracle.update(L, acts, th, obs, mean, action, adv, std, 0.1)
+
+    def run():
+        with trpo_amd.Context(L, acts, th, obs, std, 0.1) as ctx:
+            name = ctx.kernel_name
+            z1, z2 = ctx.fvp(v), ctx.fvp(v)
+            x = ctx.cg(b, 10, 0.0)
+            ctx.set_rollout(mean, action, adv)
+            return name, z1, z2, x, ctx.update()
+
+    name, z1, z2, x, r = run()
+    assert name.endswith("no4 coop"), name
+    np.testing.assert_array_equal(z1, z2)
+    assert cases.rel_l2(z1, zr) <= FVP_TOL
+    assert cases.rel_l2(x, xr) <= CG_TOL
+    assert r["accepted"] == ref["accepted"]
+    assert cases.rel_l2(r["x"], ref["x"]) <= CG_TOL
+    monkeypatch.setenv("TRPO_YCACHE", "0")
+    _, z0, _, x0, _ = run()
+    np.testing.assert_array_equal(z0, z1)
+    np.testing.assert_array_equal(x0, x)
+    monkeypatch.setenv("TRPO_NARROW_OUT", "0")
+    name16, z16, _, x16, _ = run()
+    assert "no4" not in name16
+    assert cases.rel_l2(z16, z1) <= 1e-6
+    assert cases.rel_l2(x16, x) <= 1e-5

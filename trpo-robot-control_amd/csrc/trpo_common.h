@@ -38,11 +38,12 @@ struct Net {
     } while (0)
 
 // Pinned host staging buffers that the host writes and kernels read (uploads), or kernels write and
-// the host reads (results through the mapped pointer), are allocated COHERENT.  hipHostMallocDefault
-// is non-coherent under HIP_HOST_COHERENT=0 (the default): the GPU may keep its lines in an XCD's L2,
-// and a kernel launched behind another kernel on the same queue acquires at agent scope, which does
-// not drop them -- so a host memcpy into the buffer between two calls could be read stale by the next
-// upload's copy kernel (seen as an intermittently wrong FVP direction on a few 128-B lines).
+// the host reads (results through the mapped pointer), are allocated COHERENT (hipHostMallocDefault is
+// non-coherent under HIP_HOST_COHERENT=0, the default: the GPU may cache its lines).  They are only
+// ever accessed by kernels through the mapped pointer and by the host -- never by hipMemcpyAsync: a
+// hipMemcpyAsync to / from such a buffer, with kernels reading the device side right after, gave
+// intermittently stale device data (the host-group all-reduce, tools/diag/shard_race.py: 6 of 10
+// sharded 2x64 solves diverged between ranks; 0 of 10 with copy kernels).
 #define TRPO_HOST_COHERENT (hipHostMallocMapped | hipHostMallocCoherent)
 
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }

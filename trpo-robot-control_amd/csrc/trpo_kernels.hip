@@ -916,7 +916,10 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
     static_assert(!YC || C::NT == 1, "forward cache with one tile in flight");
     // the cache only for the register-resident small nets: on the wide shapes its extra registers
     // push the kernel into scratch spills (and those runs were not bitwise reproducible)
-    static_assert(!YC || C::REGW, "forward cache only for the small-net kernels");
+#ifndef TRPO_YC_ALL
+#define TRPO_YC_ALL 0   // diagnostic build: the forward cache for every tile shape
+#endif
+    static_assert(!YC || C::REGW || TRPO_YC_ALL, "forward cache only for the small-net kernels");
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ double sh64[(5 + QB) * 4 * C::WAVES];      // 5 + QB DPP block sums, 4 rows per wave
     // streaming basis dots of a MODE 0 update: the tile scratch, unused until the tile loop's barrier
@@ -1298,7 +1301,7 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
     const int a2 = ACT >= 0 ? ((ACT >> 2) & 3) : net.act[2];
     const int a3 = ACT >= 0 ? ((ACT >> 4) & 3) : net.act[3];
     const bool y3_needed = act_needs_y(a3);
-    f4 *ycs = (MODE == 0 && C::REGW) ? reinterpret_cast<f4 *>(A.yc) : nullptr;   // cache writer (MODE 0)
+    f4 *ycs = (MODE == 0 && (C::REGW || TRPO_YC_ALL)) ? reinterpret_cast<f4 *>(A.yc) : nullptr;   // cache writer
     const f4 *TW = reinterpret_cast<const f4 *>(tw);
     const f4 *VW = reinterpret_cast<const f4 *>(vw);
 
@@ -2035,12 +2038,18 @@ __device__ __forceinline__ T coop_vgather(const Net &net, const double *src, int
     return m >= 0 ? (T)v : (T)0;
 }
 
-template <typename T, int T0, int TH, int ACT, int MODE>
+// NO (fp32 only): the narrow output layer of fvp_mlp3_kernel (<= 4 outputs): each wave's share of the
+// output layer's forward / R-forward on v_mfma_f32_4x4x1_16b_f32 (A operands from FA2 / VFA2 lane
+// (c & 3) + 16g), summed over its lane groups by two permlane steps and over the group's waves through
+// LDS as before; G2 = W2 G3 for the wave's row tile as a VALU fmaf chain; RGW2 and B3 stay on the
+// 16x16x4 contraction (G3 back in rows 4g + r).
+template <typename T, int T0, int TH, int ACT, int MODE, int NO = 0>
 __global__ void __launch_bounds__((CoopCfg<T, T0, TH>::THREADS))
 fvp_coop_kernel(IterArgs A, Net net) {
     using Q = CoopCfg<T, T0, TH>;
     using C = FastCfg<T0, TH, TH, 1>;                      // pack offsets (same fragment packs)
     using V = typename PT<T>::V;
+    static_assert(NO == 0 || (sizeof(T) == 4 && NO <= 4), "narrow output layer: fp32, <= 4 outputs");
     // MODE 3 / 4: MODE 0 / 2 on the forward-activation cache (fp32; output activation without y):
     // a wave's y1, y2 row tiles come from the cache a MODE 0 launch wrote, the forward MFMAs are skipped
     constexpr bool FV = MODE != 1, UPD = MODE == 2 || MODE == 4, YC = MODE == 3 || MODE == 4;
@@ -2085,10 +2094,18 @@ fvp_coop_kernel(IterArgs A, Net net) {
         fa1[kt] = TP[C::FA1 / 4 + (w * T1 + kt) * 64 + lane];
         fb1[kt] = TP[C::FB1 / 4 + (w * T2 + kt) * 64 + lane];
     }
-    const V fa2 = TP[C::FA2 / 4 + w * 64 + lane];
-    const V fb2 = TP[C::FB2 / 4 + w * 64 + lane];
+    // narrow output: the output layer's A operands from lane l2 = (c & 3) + 16g, its per-output vectors
+    // (bias, 1/sigma^2, ...) for outputs 0..3 in every lane group (g2 = 0)
+    const int l2 = NO ? (c & 3) + 16 * g : lane, g2 = NO ? 0 : g;
+    const V fa2 = TP[C::FA2 / 4 + w * 64 + l2];
+    const V fb2 = NO ? zero4 : TP[C::FB2 / 4 + w * 64 + lane];
+    [[maybe_unused]] V w2n[4];                             // NO: W2[16w + 4g + r][0..3] (FB2 lane 4g + r)
+    if constexpr (NO) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) w2n[r] = TP[C::FB2 / 4 + w * 64 + 4 * g + r];
+    }
     const V b0w = dvec<T>(TPs + C::BI0 + 16 * w, g), b1w = dvec<T>(TPs + C::BI1 + 16 * w, g);
-    const V b2 = dvec<T>(TPs + C::BI2, g), iv = dvec<T>(TPs + C::IV, g);
+    const V b2 = dvec<T>(TPs + C::BI2, g2), iv = dvec<T>(TPs + C::IV, g2);
     V vfa2, vb0w, vb1w, vb2;
     if constexpr (UPD) {
         // ---- CG step j-1 -> j; z = F p_{j-1} arrives reduced (un-normalised) in acc_in ----
@@ -2183,10 +2200,10 @@ fvp_coop_kernel(IterArgs A, Net net) {
             for (int s = 0; s < 4; ++s) vfa1[kt][s] = vget(C::VFA1 + ((w * T1 + kt) * 64 + lane) * 4 + s);
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-            vfa2[s] = vget(C::VFA2 + (w * 64 + lane) * 4 + s);
+            vfa2[s] = vget(C::VFA2 + (w * 64 + l2) * 4 + s);
             vb0w[s] = vget(C::VB0 + 16 * w + PT<T>::neu(g, s));
             vb1w[s] = vget(C::VB1 + 16 * w + PT<T>::neu(g, s));
-            vb2[s] = vget(C::VB2 + PT<T>::neu(g, s));
+            vb2[s] = vget(C::VB2 + PT<T>::neu(g2, s));
         }
         __syncthreads();                                   // LDS goes back to the tile exchanges
     } else if (FV && A.v_nat) {                            // plain FVP of a natural-order direction
@@ -2201,20 +2218,20 @@ fvp_coop_kernel(IterArgs A, Net net) {
             for (int s = 0; s < 4; ++s) vfa1[kt][s] = vget(C::VFA1 + ((w * T1 + kt) * 64 + lane) * 4 + s);
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-            vfa2[s] = vget(C::VFA2 + (w * 64 + lane) * 4 + s);
+            vfa2[s] = vget(C::VFA2 + (w * 64 + l2) * 4 + s);
             vb0w[s] = vget(C::VB0 + 16 * w + PT<T>::neu(g, s));
             vb1w[s] = vget(C::VB1 + 16 * w + PT<T>::neu(g, s));
-            vb2[s] = vget(C::VB2 + PT<T>::neu(g, s));
+            vb2[s] = vget(C::VB2 + PT<T>::neu(g2, s));
         }
     } else {
 #pragma unroll
         for (int kt = 0; kt < T0; ++kt) vfa0[kt] = FV ? VP[C::VFA0 / 4 + (w * T0 + kt) * 64 + lane] : zero4;
 #pragma unroll
         for (int kt = 0; kt < T1; ++kt) vfa1[kt] = FV ? VP[C::VFA1 / 4 + (w * T1 + kt) * 64 + lane] : zero4;
-        vfa2 = FV ? VP[C::VFA2 / 4 + w * 64 + lane] : zero4;
+        vfa2 = FV ? VP[C::VFA2 / 4 + w * 64 + l2] : zero4;
         vb0w = FV ? dvec<T>(VPs + C::VB0 + 16 * w, g) : zero4;
         vb1w = FV ? dvec<T>(VPs + C::VB1 + 16 * w, g) : zero4;
-        vb2 = FV ? dvec<T>(VPs + C::VB2, g) : zero4;
+        vb2 = FV ? dvec<T>(VPs + C::VB2, g2) : zero4;
     }
 
     const int a1 = ACT >= 0 ? (ACT & 3) : net.act[1];
@@ -2318,11 +2335,24 @@ fvp_coop_kernel(IterArgs A, Net net) {
         V a3p = zero4, r3p = zero4, r3q = zero4;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-            if (!YC && y3_needed) a3p = PT<T>::mfma(fa2[s], y2w[s], a3p);   // YC: y3 never needed
-            if constexpr (FV) {
-                r3p = PT<T>::mfma(fa2[s], r2w[s], r3p);
-                r3q = PT<T>::mfma(vfa2[s], y2w[s], r3q);
+            if constexpr (NO) {
+                if (!YC && y3_needed) a3p = MFMA4(fa2[s], y2w[s], a3p);
+                if constexpr (FV) {
+                    r3p = MFMA4(fa2[s], r2w[s], r3p);
+                    r3q = MFMA4(vfa2[s], y2w[s], r3q);
+                }
+            } else {
+                if (!YC && y3_needed) a3p = PT<T>::mfma(fa2[s], y2w[s], a3p);   // YC: y3 never needed
+                if constexpr (FV) {
+                    r3p = PT<T>::mfma(fa2[s], r2w[s], r3p);
+                    r3q = PT<T>::mfma(vfa2[s], y2w[s], r3q);
+                }
             }
+        }
+        if constexpr (NO) {                                // the wave's 16 hidden neurons: sum the lane groups
+            if (!YC && y3_needed) a3p = rowgroup_sum4(a3p);
+            r3p = FV ? rowgroup_sum4(r3p + r3q) : zero4;
+            r3q = zero4;
         }
         V x3 = b2, rx3 = vb2;
         if constexpr (Q::GW > 1) {
@@ -2343,16 +2373,18 @@ fvp_coop_kernel(IterArgs A, Net net) {
         if constexpr (FV) {
             g3 = actv_bwd<T>(a3, y3, r3 * iv);
         } else {
-            const V dm = dvec<T>(reinterpret_cast<const T *>(A.pg_d4) + (long)(tc * 16 + c) * 16, g);
+            const V dm = dvec<T>(reinterpret_cast<const T *>(A.pg_d4) + (long)(tc * 16 + c) * 16, g2);
             const T adv = reinterpret_cast<const T *>(A.pg_adv)[tc * 16 + c];
-            g3 = actv_bwd<T>(a3, y3, (adv * dm) * dvec<T>(reinterpret_cast<const T *>(A.pg_iv4), g));
+            g3 = actv_bwd<T>(a3, y3, (adv * dm) * dvec<T>(reinterpret_cast<const T *>(A.pg_iv4), g2));
         }
         g3 = live ? g3 : zero4;
-        if (w == 0) sB3 += g3;
+        // NO: every lane group holds outputs 0..3; the contractions below want rows 4g + r
+        const V g3m = (NO && g != 0) ? zero4 : g3;
+        if (w == 0) sB3 += g3m;
 
         // ---- RGW2 tile (w, 0) += Y2_w . G3^T ----
         scr_put_t<T>(scr, 0, y2w, c, g);
-        scr_put_t<T>(scr, 16, g3, c, g);
+        scr_put_t<T>(scr, 16, g3m, c, g);
         {
             const V ya = scr_get_t<T>(scr, 0, c, g), gg = scr_get_t<T>(scr, 16, c, g);
 #pragma unroll
@@ -2360,8 +2392,16 @@ fvp_coop_kernel(IterArgs A, Net net) {
         }
         // ---- G2 row tile w = act2'(W2 G3) ----
         V t = zero4;
+        if constexpr (NO) {
+            // the fmaf chain over the outputs a 16x16x4 MFMA forms (its padded rows added zeros)
 #pragma unroll
-        for (int s = 0; s < 4; ++s) t = PT<T>::mfma(fb2[s], g3[s], t);
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int o = 0; o < NO; ++o) t[r] = fmaf(w2n[r][o], g3[o], t[r]);
+        } else {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) t = PT<T>::mfma(fb2[s], g3[s], t);
+        }
         const V g2w = actv_bwd<T>(a2, y2w, t);
         sB2 += g2w;
         V g2[T2];
@@ -3184,7 +3224,7 @@ static hipError_t fast_attr(int lds) {
     hipError_t e = hipFuncSetAttribute((const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 0, 0, NO>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
-    if constexpr (FastCfg<T0, T1, T2, T3>::REGW) {
+    if constexpr (FastCfg<T0, T1, T2, T3>::REGW || TRPO_YC_ALL) {
         e = hipFuncSetAttribute((const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 2, 0, NO>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return e;
@@ -3204,7 +3244,7 @@ static hipError_t fast_attr(int lds) {
 // MODE 2 (forward cache) exists for the register-resident small-net shapes only
 template <int T0, int T1, int T2, int T3, int ACT, int MODE, int QB = 0, int NO = 0>
 static constexpr fast_launch_fn yc_launch() {
-    if constexpr (FastCfg<T0, T1, T2, T3>::REGW) return fast_launch<T0, T1, T2, T3, ACT, MODE, QB, NO>;
+    if constexpr (FastCfg<T0, T1, T2, T3>::REGW || TRPO_YC_ALL) return fast_launch<T0, T1, T2, T3, ACT, MODE, QB, NO>;
     else return nullptr;
 }
 
@@ -3240,6 +3280,8 @@ struct FastEntry {
 static const FastEntry kFast[] = {
 #ifdef TRPO_ARM_ONLY    // experiment builds (make variant): armDOF_0-class shapes only, fast to compile
     FAST_ENTRY(1, 1, 1, 1, ACT_TTL), FAST_NO_PAIR(1, 1, 1, 1, ACT_TTL, 3),
+#elif defined(TRPO_DIAG_1441)   // diagnostic build: the 2x64 one-wave-per-tile shape only (with TRPO_COOP=0)
+    FAST_ENTRY(1, 4, 4, 1, ACT_TTL),
 #else
     FAST_SHAPE(1, 1, 1, 1), FAST_SHAPE(1, 2, 2, 1), FAST_SHAPE(1, 4, 4, 1),
     FAST_SHAPE(2, 1, 1, 1), FAST_SHAPE(2, 2, 2, 1), FAST_SHAPE(2, 4, 4, 1),
@@ -3247,62 +3289,63 @@ static const FastEntry kFast[] = {
 #endif
 };
 
-// cooperative kernels (T1 == T2 == TH, T3 == 1); element type T: fp32 or the fp64 precision mode
-template <typename T, int T0, int TH, int ACT, int MODE>
+// cooperative kernels (T1 == T2 == TH, T3 == 1); element type T: fp32 or the fp64 precision mode;
+// NO: the narrow output layer (fp32, <= 4 outputs)
+template <typename T, int T0, int TH, int ACT, int MODE, int NO = 0>
 static void coop_launch(dim3 g, int lds, hipStream_t st, const IterArgs &a, const Net &net) {
-    hipLaunchKernelGGL((fvp_coop_kernel<T, T0, TH, ACT, MODE>), g, dim3(CoopCfg<T, T0, TH>::THREADS), lds, st, a,
-                       net);
+    hipLaunchKernelGGL((fvp_coop_kernel<T, T0, TH, ACT, MODE, NO>), g, dim3(CoopCfg<T, T0, TH>::THREADS), lds, st,
+                       a, net);
 }
 template <typename T, int T0, int TH>
 struct CoopYC {
     static constexpr bool ok = sizeof(T) == 4 ? !(T0 == 2 && TH == 4) : (TH > 1 || TRPO_F64_TH1_WAVES <= 4);
 };
-template <typename T, int T0, int TH, int ACT>
+template <typename T, int T0, int TH, int ACT, int NO = 0>
 static hipError_t coop_attr(int lds) {
-    hipError_t e = hipFuncSetAttribute((const void *)fvp_coop_kernel<T, T0, TH, ACT, 0>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    if (e != hipSuccess) return e;
-    e = hipFuncSetAttribute((const void *)fvp_coop_kernel<T, T0, TH, ACT, 1>,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    if (e != hipSuccess) return e;
+    const void *k[5] = {(const void *)fvp_coop_kernel<T, T0, TH, ACT, 0, NO>,
+                        (const void *)fvp_coop_kernel<T, T0, TH, ACT, 1, NO>,
+                        (const void *)fvp_coop_kernel<T, T0, TH, ACT, 2, NO>, nullptr, nullptr};
     if constexpr (CoopYC<T, T0, TH>::ok) {
-        e = hipFuncSetAttribute((const void *)fvp_coop_kernel<T, T0, TH, ACT, 3>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        if (e != hipSuccess) return e;
-        e = hipFuncSetAttribute((const void *)fvp_coop_kernel<T, T0, TH, ACT, 4>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        k[3] = (const void *)fvp_coop_kernel<T, T0, TH, ACT, 3, NO>;
+        k[4] = (const void *)fvp_coop_kernel<T, T0, TH, ACT, 4, NO>;
+    }
+    for (const void *f : k) {
+        if (!f) continue;
+        const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return e;
     }
-    return hipFuncSetAttribute((const void *)fvp_coop_kernel<T, T0, TH, ACT, 2>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    return hipSuccess;
 }
 // MODE 3 / 4 (forward cache): not where the cache registers push the kernel into scratch spills
 // (fp32 T0 = 2, TH = 4; fp64 TH = 1, whose 8-wave blocks cap a wave at 256 VGPRs)
-template <typename T, int T0, int TH, int ACT, int MODE>
+template <typename T, int T0, int TH, int ACT, int MODE, int NO = 0>
 static constexpr fast_launch_fn coop_yc_launch() {
-    if constexpr (CoopYC<T, T0, TH>::ok) return coop_launch<T, T0, TH, ACT, MODE>;
+    if constexpr (CoopYC<T, T0, TH>::ok) return coop_launch<T, T0, TH, ACT, MODE, NO>;
     else return nullptr;
 }
 struct CoopEntry {
-    int f64, T0, TH, act;
+    int f64, T0, TH, act, no;
     fast_launch_fn launch, launch_pg, launch_cg;   // MODE 0 FVP, 1 policy gradient, 2 CG iteration
     fast_launch_fn launch_yc, launch_cg_yc;        // MODE 3 / 4: 0 / 2 on the forward cache (fp32)
     hipError_t (*attr)(int);
     int lds, slab, ng, threads, main_bytes;
 };
-#define COOP_ENTRY(T, t0, th, act)                                                                                \
-    {sizeof(T) == 8, t0, th, act, coop_launch<T, t0, th, act, 0>, coop_launch<T, t0, th, act, 1>,                \
-     coop_launch<T, t0, th, act, 2>, coop_yc_launch<T, t0, th, act, 3>(), coop_yc_launch<T, t0, th, act, 4>(),    \
-     coop_attr<T, t0, th, act>, CoopCfg<T, t0, th>::LDS_BYTES,                                                    \
+#define COOP_ENTRY_NO(T, t0, th, act, no)                                                                         \
+    {sizeof(T) == 8, t0, th, act, no, coop_launch<T, t0, th, act, 0, no>, coop_launch<T, t0, th, act, 1, no>,     \
+     coop_launch<T, t0, th, act, 2, no>, coop_yc_launch<T, t0, th, act, 3, no>(),                                \
+     coop_yc_launch<T, t0, th, act, 4, no>(), coop_attr<T, t0, th, act, no>, CoopCfg<T, t0, th>::LDS_BYTES,      \
      CoopCfg<T, t0, th>::SLAB, CoopCfg<T, t0, th>::NG, CoopCfg<T, t0, th>::THREADS, CoopCfg<T, t0, th>::MAIN_BYTES}
+#define COOP_ENTRY(T, t0, th, act) COOP_ENTRY_NO(T, t0, th, act, 0)
 #define COOP_SHAPE(T, t0, th) COOP_ENTRY(T, t0, th, ACT_TTL), COOP_ENTRY(T, t0, th, -1)
+#define COOP_SHAPE_NO(t0, th) COOP_ENTRY_NO(float, t0, th, ACT_TTL, 4), COOP_ENTRY_NO(float, t0, th, -1, 4)
 static const CoopEntry kCoop[] = {
-#ifdef TRPO_ARM_ONLY
+#if defined(TRPO_ARM_ONLY) || defined(TRPO_DIAG_1441)
     COOP_ENTRY(double, 1, 1, ACT_TTL)};
 #else
     COOP_SHAPE(float, 1, 2),  COOP_SHAPE(float, 1, 4),  COOP_SHAPE(float, 2, 2),  COOP_SHAPE(float, 2, 4),
     COOP_SHAPE(double, 1, 1), COOP_SHAPE(double, 1, 2), COOP_SHAPE(double, 1, 4), COOP_SHAPE(double, 2, 1),
-    COOP_SHAPE(double, 2, 2), COOP_SHAPE(double, 2, 4)};
+    COOP_SHAPE(double, 2, 2), COOP_SHAPE(double, 2, 4),
+    COOP_SHAPE_NO(1, 2),      COOP_SHAPE_NO(1, 4),      COOP_SHAPE_NO(2, 2),      COOP_SHAPE_NO(2, 4)};
 #endif
 
 struct trpo_dev {
@@ -3391,7 +3434,7 @@ struct trpo_dev {
     ncclComm_t comm;
     // in-process host-staged group (trpo_dev_set_group): the same sharded code path without RCCL
     trpo_hgroup *group;
-    double *gbuf;               // pinned host staging for the group exchange
+    double *gbuf, *gbuf_dev;    // pinned (coherent, mapped) host staging for the group exchange
     size_t gbuf_cap;
     // peer-window exchange over xGMI (trpo_peer.hip): when peer_on, every collective goes through it
     // and the CG graph's per-FVP all-reduce becomes one exchange kernel into zred
@@ -3457,6 +3500,7 @@ extern "C" void trpo_hgroup_destroy(trpo_hgroup *g) {
 
 // in-place sum of buf[count] (device, on d's stream) over the group; every rank must call it with
 // the same count, in the same order as the others (the library's fixed launch sequences do)
+__global__ void vcopy64_kernel(const double *__restrict__ src, double *__restrict__ dst, int n);
 static int hgroup_allreduce(trpo_dev *d, double *buf, size_t count) {
     trpo_hgroup *g = d->group;
     // a local failure before the exchange still takes part in both barriers (a rank that returned
@@ -3467,10 +3511,16 @@ static int hgroup_allreduce(trpo_dev *d, double *buf, size_t count) {
         if (d->gbuf) hipHostFree(d->gbuf);
         d->gbuf = NULL;
         d->gbuf_cap = 0;
-        ok = hipHostMalloc((void **)&d->gbuf, sizeof(double) * count, TRPO_HOST_COHERENT) == hipSuccess;
+        ok = hipHostMalloc((void **)&d->gbuf, sizeof(double) * count, TRPO_HOST_COHERENT) == hipSuccess &&
+             hipHostGetDevicePointer((void **)&d->gbuf_dev, d->gbuf, 0) == hipSuccess;
         if (ok) d->gbuf_cap = count;
     }
-    ok = ok && hipMemcpyAsync(d->gbuf, buf, sizeof(double) * count, hipMemcpyDeviceToHost, d->stream) == hipSuccess;
+    // copies by KERNEL through the mapped buffer, not hipMemcpyAsync: a host-to-device hipMemcpyAsync
+    // into buf followed by kernels reading buf gave intermittently stale reads (ranks diverging in
+    // whole 512-element cg_axpy slices, 6 of 10 sharded 2x64 solves; tools/diag/shard_race.py)
+    if (ok) hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv((long)count, 256)), dim3(256), 0, d->stream,
+                               (const double *)buf, d->gbuf_dev, (int)count);
+    ok = ok && hipGetLastError() == hipSuccess;
     ok = ok && hipStreamSynchronize(d->stream) == hipSuccess;
     g->slot[d->rank] = ok ? d->gbuf : NULL;
     g->count[d->rank] = ok ? count : (size_t)-1;
@@ -3489,7 +3539,9 @@ static int hgroup_allreduce(trpo_dev *d, double *buf, size_t count) {
     if (!sum) return -4;
     memcpy(d->gbuf, sum, sizeof(double) * count);
     free(sum);
-    HCHK(hipMemcpyAsync(buf, d->gbuf, sizeof(double) * count, hipMemcpyHostToDevice, d->stream));
+    hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv((long)count, 256)), dim3(256), 0, d->stream,
+                       (const double *)d->gbuf_dev, buf, (int)count);
+    HCHK(hipGetLastError());
     HCHK(hipStreamSynchronize(d->stream));
     return 0;
 }
@@ -3512,8 +3564,8 @@ static void name_fast(trpo_dev *d) {
     const int *T = d->fast->T;
     const int no = d->coop ? 0 : d->fast->no;
     snprintf(d->name, sizeof d->name, "mfma-mlp3 %dx%dx%dx%d%s%s%s%s", T[0], T[1], T[2], T[3],
-             d->fast->act >= 0 ? " ttl" : "", d->coop ? " coop" : "", d->f64 ? " fp64" : "",
-             !no ? "" : (no & NO_MFMA_RGW2) ? " no-mfma" : " no-valu");
+             d->fast->act >= 0 ? " ttl" : "", d->coop ? (d->coop_e->no ? " no4 coop" : " coop") : "",
+             d->f64 ? " fp64" : "", !no ? "" : (no & NO_MFMA_RGW2) ? " no-mfma" : " no-valu");
 }
 
 // the narrow-output twin for n local samples: RGW2 on the VALU once every wave runs several tiles
@@ -3721,9 +3773,15 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
         d->coop_e = NULL;
         d->coop = 0;
         const char *ec = getenv("TRPO_COOP");
+        const char *eno_coop = getenv("TRPO_NARROW_OUT");
         if ((d->f64 || !(ec && atoi(ec) == 0)) && T[1] == T[2] && T[3] == 1)
             for (const CoopEntry &e : kCoop)
-                if (e.f64 == d->f64 && e.T0 == T[0] && e.TH == T[1] && e.act == d->fast->act) d->coop_e = &e;
+                if (e.f64 == d->f64 && e.T0 == T[0] && e.TH == T[1] && e.act == d->fast->act && e.no == 0)
+                    d->coop_e = &e;
+        // its narrow-output twin (fp32, <= 4 outputs; TRPO_NARROW_OUT=0 keeps the 16x16x4 output layer)
+        if (d->coop_e && !d->f64 && n.L[3] <= 4 && !(eno_coop && atoi(eno_coop) == 0))
+            for (const CoopEntry &e : kCoop)
+                if (!e.f64 && e.T0 == T[0] && e.TH == T[1] && e.act == d->fast->act && e.no == 4) d->coop_e = &e;
         if (d->f64 && !d->coop_e) FAIL("internal: no fp64 kernel for tile shape %dx%dx%dx%d", T[0], T[1], T[2], T[3]);
         if (d->coop_e) {
             if (d->coop_e->attr(d->coop_e->lds) != hipSuccess)
@@ -4437,9 +4495,7 @@ static int allreduce(trpo_dev *d, double *buf, size_t count) {
     if (d->peer_on) {
         // in place through the staging vector (the exchange kernel's output must not alias its input)
         if (count > trpo_peer_slot(d->peer)) return -1;
-        // a copy KERNEL, not hipMemcpyAsync: under the HIP runtime torch bundles (ROCm 7.0) a
-        // device-to-device hipMemcpyAsync behind the slab reduce intermittently handed the exchange
-        // stale lines of buf (tests/test_gpu_peer.py::test_peer_fvp_and_update_slab_paths)
+        // a copy kernel (stream-ordered like the exchange that follows)
         hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv((long)count, 256)), dim3(256), 0, d->stream, (const double *)buf,
                            d->ptmp, (int)count);
         HCHK(hipGetLastError());
