@@ -466,6 +466,13 @@ def sweep(device, dist, steps=10, comm="rccl"):
     return out
 
 
+def latest_traffic_json():
+    """profiles/rNN_cgiter_traffic.json of the highest round present (None if there is none)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_cgiter_traffic.json")))
+    return files[-1] if files else None
+
+
 def main():
     args = parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -506,11 +513,13 @@ def main():
     achieved_tflops = flops / (k3 * 1e-3) / 1e12
     hbm_bound = bytes_alg / (PEAK_HBM_GBS * 1e9) >= flops / (PEAK_FP32_TFLOPS * 1e12)
 
-    traffic = None
-    tpath = os.environ.get("TRPO_TRAFFIC_JSON", os.path.join(ROOT, "profiles", "r02_cgiter_traffic.json"))
-    if os.path.exists(tpath) and dist.world == 1:
-        # HBM bytes per launch of this kernel at this workload, from the committed rocprofv3 PMC passes
+    traffic, tsrc = None, None
+    tpath = os.environ.get("TRPO_TRAFFIC_JSON") or latest_traffic_json()
+    if tpath and os.path.exists(tpath) and dist.world == 1:
+        # HBM bytes per launch of this kernel at this workload, from the newest committed rocprofv3 PMC
+        # passes (tools/profile_round.sh: FETCH_SIZE x2 + WRITE_SIZE, separate passes)
         traffic = json.load(open(tpath))["traffic_bytes"]
+        tsrc = os.path.relpath(tpath, ROOT)
 
     result = {
         "metric": "FVP samples/sec + 10-iter CG wall time, armDOF_0 policy",
@@ -539,7 +548,7 @@ def main():
                      "peak": PEAK_HBM_GBS if hbm_bound else PEAK_FP32_TFLOPS,
                      "unit": "GB/s" if hbm_bound else "TFLOP/s",
                      "frac": achieved_gbs / PEAK_HBM_GBS if hbm_bound else achieved_tflops / PEAK_FP32_TFLOPS,
-                     "traffic": traffic,
+                     "traffic": traffic, "traffic_source": tsrc,
                      "kernel": "fvp_mlp3_kernel MODE 3 (CG-iteration kernel: fp64 CG step + cached-forward FVP)",
                      "kernel_ms": k3, "flops_per_launch": flops, "alg_bytes_per_launch": bytes_alg,
                      "fp32_tflops": achieved_tflops, "fp32_frac": achieved_tflops / PEAK_FP32_TFLOPS,
