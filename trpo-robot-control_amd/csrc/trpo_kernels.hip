@@ -752,6 +752,9 @@ constexpr int SCR_LD3 = TRPO_SCR_LD3;  // fvp_mlp3_kernel's transpose scratch (T
 #ifndef TRPO_SKIPW
 #define TRPO_SKIPW 1                    // element-less waves skip the CG-state loads (pair layout)
 #endif
+#ifndef TRPO_DIAG_NOLOAD
+#define TRPO_DIAG_NOLOAD 0              // diagnostic builds only: every tile reuses the first tile's inputs
+#endif
 #ifndef TRPO_ISLOT_TABLE
 #define TRPO_ISLOT_TABLE 1              // epilogue slot positions from a table (not islot_at)
 #endif
@@ -859,6 +862,18 @@ __device__ __forceinline__ f4 rowgroup_sum4(f4 v) {
 // ds_read_b128 groups ({0-3,12-15,20-27} and the three others) cover every bank exactly once.  The
 // round-1 row stride of 20 floats left 3 two-way conflicts per read group (42 % of the kernel's LDS
 // cycles were conflict cycles).  Same footprint: 20 floats per row.
+// the tile loop's streamed inputs (observations, forward cache)
+#ifndef TRPO_NT_STREAM
+#define TRPO_NT_STREAM 0
+#endif
+__device__ __forceinline__ f4 stream_ld(const f4 *p) {
+#if TRPO_NT_STREAM
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+
 __device__ __forceinline__ int scr_off(int row, int chunk) {
 #if TRPO_SCR_SWZ
     const int q = (row >> 2) & 3;
@@ -1391,16 +1406,16 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
                 for (int kt = 0; kt < T0; ++kt) x0[t][kt] = obs4[(long)(tc * 16 + c) * (4 * T0) + kt * 4 + g];
             }
         }
-        {   // unconditional (clamped) prefetch of the next trip's first tile
+        if constexpr (!TRPO_DIAG_NOLOAD) {   // unconditional (clamped) prefetch of the next trip's first tile
             const int tn = min(tile + NT * nwaves, ntiles - 1);
 #pragma unroll
-            for (int kt = 0; kt < T0; ++kt) xn[kt] = obs4[(long)(tn * 16 + c) * (4 * T0) + kt * 4 + g];
+            for (int kt = 0; kt < T0; ++kt) xn[kt] = stream_ld(obs4 + (long)(tn * 16 + c) * (4 * T0) + kt * 4 + g);
             if constexpr (YC) {
 #pragma unroll
-                for (int k = 0; k < T1 + T2; ++k) yn[k] = yc4[((long)tn * NYC + k) * 64 + lane];
+                for (int k = 0; k < T1 + T2; ++k) yn[k] = stream_ld(yc4 + ((long)tn * NYC + k) * 64 + lane);
                 if (y3_needed)
 #pragma unroll
-                    for (int k = T1 + T2; k < NYC; ++k) yn[k] = yc4[((long)tn * NYC + k) * 64 + lane];
+                    for (int k = T1 + T2; k < NYC; ++k) yn[k] = stream_ld(yc4 + ((long)tn * NYC + k) * 64 + lane);
             }
 #if TRPO_PF_PIN
             // keep the prefetch at the top of the trip: left to itself the scheduler sinks it to
