@@ -3132,7 +3132,16 @@ cg_axpy_kernel(const double *__restrict__ dots, int G, const double *__restrict_
     const CgSt sin = *st_in;
     const double cth = ctl->resth;
     const int cmax = ctl->maxiter;
-    if (*skip) return;                                    // grid-uniform
+    // grid-uniform stop test on the state this step starts from: the value ctl->done held when the
+    // launch began (cg_init_kernel / the previous step set it by this formula).  Not *skip: block 0
+    // of THIS launch rewrites ctl->done at its end, and a block that starts after that (a GPU shared
+    // with other processes) would skip its slice of the final x update.  A stopped step carries the
+    // state forward (st_out = st_in) so that the next launch's test sees it too.
+    (void)skip;
+    if (sin.rdotr < cth || sin.iter >= cmax) {
+        if (blockIdx.x == 0 && tid == 0) *st_out = sin;
+        return;
+    }
     if (lane == 0) {
 #pragma unroll
         for (int i = 0; i < NI; ++i)
