@@ -518,7 +518,7 @@ __device__ __forceinline__ f4 act_bwd(int a, f4 y, f4 g) {
     if (a == ACT_O) return 0.1f * g;
     return g;
 }
-__device__ __forceinline__ bool act_needs_y(int a) { return a == ACT_T || a == ACT_S; }
+__host__ __device__ constexpr inline bool act_needs_y(int a) { return a == ACT_T || a == ACT_S; }
 // R{y} of four rows from R{x} and the (cached) forward value y
 __device__ __forceinline__ f4 act_r4(int a, f4 y, f4 rx) {
     if (a == ACT_T) return rx * dtanh4(y);
@@ -754,7 +754,7 @@ constexpr int SCR_LD3 = TRPO_SCR_LD3;  // fvp_mlp3_kernel's transpose scratch (T
 #endif
 #ifndef TRPO_DIAG_NOLOAD
 #define TRPO_DIAG_NOLOAD 0              // diagnostic builds only: every tile reuses the first tile's inputs
-#endif
+#endif                                  // (1: all of them, 2: the observations only, 3: the cached y only)
 #ifndef TRPO_ISLOT_TABLE
 #define TRPO_ISLOT_TABLE 1              // epilogue slot positions from a table (not islot_at)
 #endif
@@ -976,10 +976,12 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
     // a load guarded by a run-time condition makes hipcc branch around it and drain vmcnt,
     // which serialises the round trips (cdna_hip_programming.md §5 trap (c)).
     f4 st[PER];
+    // the wave's tile index is wave-uniform: kept in an SGPR (readfirstlane), the tile loop's
+    // bookkeeping, bound test and input addresses are scalar work, not VALU
 #if TRPO_TILE_ILV
-    int tile = wave * gridDim.x + blockIdx.x;
+    int tile = __builtin_amdgcn_readfirstlane(wave * gridDim.x + blockIdx.x);
 #else
-    int tile = blockIdx.x * C::WAVES + wave;
+    int tile = __builtin_amdgcn_readfirstlane(blockIdx.x * C::WAVES + wave);
 #endif
     f4 xn[T0];
     [[maybe_unused]] f4 yn[YC ? NYC : 1];
@@ -1384,46 +1386,9 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
 
     // NT independent tiles per loop trip (ILP: the scheduler interleaves their MFMA chains)
     constexpr int NT = C::NT;
-    for (; tile < ntiles; tile += NT * nwaves) {
-        // input tiles: lane holds features 16kt+4g..+3 of its sample (D-layout rows)
-        f4 x0[NT][T0];
-        [[maybe_unused]] f4 ycur[YC ? NYC : 1];
-        if constexpr (YC) {
-#pragma unroll
-            for (int k = 0; k < NYC; ++k) ycur[k] = yn[k];
-        }
-        bool live[NT];
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const int tt = tile + t * nwaves;
-            live[t] = tt * 16 + c < n;
-            if (t == 0) {
-#pragma unroll
-                for (int kt = 0; kt < T0; ++kt) x0[0][kt] = xn[kt];
-            } else {
-                const int tc = min(tt, ntiles - 1);
-#pragma unroll
-                for (int kt = 0; kt < T0; ++kt) x0[t][kt] = obs4[(long)(tc * 16 + c) * (4 * T0) + kt * 4 + g];
-            }
-        }
-        if constexpr (!TRPO_DIAG_NOLOAD) {   // unconditional (clamped) prefetch of the next trip's first tile
-            const int tn = min(tile + NT * nwaves, ntiles - 1);
-#pragma unroll
-            for (int kt = 0; kt < T0; ++kt) xn[kt] = stream_ld(obs4 + (long)(tn * 16 + c) * (4 * T0) + kt * 4 + g);
-            if constexpr (YC) {
-#pragma unroll
-                for (int k = 0; k < T1 + T2; ++k) yn[k] = stream_ld(yc4 + ((long)tn * NYC + k) * 64 + lane);
-                if (y3_needed)
-#pragma unroll
-                    for (int k = T1 + T2; k < NYC; ++k) yn[k] = stream_ld(yc4 + ((long)tn * NYC + k) * 64 + lane);
-            }
-#if TRPO_PF_PIN
-            // keep the prefetch at the top of the trip: left to itself the scheduler sinks it to
-            // the loop latch, where the x0 = xn copy then waits out a full memory round trip
-            __builtin_amdgcn_sched_barrier(0);
-#endif
-        }
-
+    // one tile (NT tiles) of work: inputs x0, the cached activations ycur, live columns
+    auto tile_step = [&](const int tile, const f4 (&x0)[NT][T0], const f4 (&ycur)[YC ? NYC : 1],
+                         const bool (&live)[NT]) __attribute__((always_inline)) {
         // ---- layer 0: x1 = W0^T x0 + b0 ; Rx1 = VW0^T x0 + vb0 (Ry0 = 0) ----
         f4 y1[NT][T1], r1[NT][T1];
 #pragma unroll
@@ -1746,6 +1711,50 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
         }
         first_tile = false;
 #endif
+    };
+    for (; tile < ntiles; tile += NT * nwaves) {
+        // input tiles: lane holds features 16kt+4g..+3 of its sample (D-layout rows)
+        f4 x0[NT][T0];
+        [[maybe_unused]] f4 ycur[YC ? NYC : 1];
+        if constexpr (YC) {
+#pragma unroll
+            for (int k = 0; k < NYC; ++k) ycur[k] = yn[k];
+        }
+        bool live[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int tt = tile + t * nwaves;
+            live[t] = tt * 16 + c < n;
+            if (t == 0) {
+#pragma unroll
+                for (int kt = 0; kt < T0; ++kt) x0[0][kt] = xn[kt];
+            } else {
+                const int tc = min(tt, ntiles - 1);
+#pragma unroll
+                for (int kt = 0; kt < T0; ++kt) x0[t][kt] = obs4[(long)(tc * 16 + c) * (4 * T0) + kt * 4 + g];
+            }
+        }
+        if constexpr (TRPO_DIAG_NOLOAD != 1) {   // unconditional (clamped) prefetch of the next trip's first tile
+            const int tn = min(tile + NT * nwaves, ntiles - 1);
+            if constexpr (TRPO_DIAG_NOLOAD != 2) {
+#pragma unroll
+                for (int kt = 0; kt < T0; ++kt) xn[kt] = stream_ld(obs4 + (long)(tn * 16 + c) * (4 * T0) + kt * 4 + g);
+            }
+            if constexpr (YC && TRPO_DIAG_NOLOAD != 3) {
+#pragma unroll
+                for (int k = 0; k < T1 + T2; ++k) yn[k] = stream_ld(yc4 + ((long)tn * NYC + k) * 64 + lane);
+                if (y3_needed)
+#pragma unroll
+                    for (int k = T1 + T2; k < NYC; ++k) yn[k] = stream_ld(yc4 + ((long)tn * NYC + k) * 64 + lane);
+            }
+#if TRPO_PF_PIN
+            // keep the prefetch at the top of the trip: left to itself the scheduler sinks it to
+            // the loop latch, where the x0 = xn copy then waits out a full memory round trip
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+        }
+
+        tile_step(tile, x0, ycur, live);
     }
 
     STAMP(4);
