@@ -752,6 +752,12 @@ constexpr int SCR_LD3 = TRPO_SCR_LD3;  // fvp_mlp3_kernel's transpose scratch (T
 #ifndef TRPO_SKIPW
 #define TRPO_SKIPW 1                    // element-less waves skip the CG-state loads (pair layout)
 #endif
+#ifndef TRPO_BUF_PF
+#define TRPO_BUF_PF 1                   // the tile loop's prefetch as buffer loads (scalar tile addressing)
+#endif
+#ifndef TRPO_RGS4_T
+#define TRPO_RGS4_T 1                   // rowgroup_sum4 as a transposed reduction (same bits, half the swaps)
+#endif
 #ifndef TRPO_DIAG_NOLOAD
 #define TRPO_DIAG_NOLOAD 0              // diagnostic builds only: every tile reuses the first tile's inputs
 #endif                                  // (1: all of them, 2: the observations only, 3: the cached y only)
@@ -846,11 +852,33 @@ __device__ __forceinline__ float rowgroup_sum(float v) {
     const auto q = __builtin_amdgcn_permlane16_swap(__float_as_uint(t), __float_as_uint(t), false, false);
     return __uint_as_float(q[0]) + __uint_as_float(q[1]);
 }
+// rowgroup_sum of four values at once, transposed: the half-wave swap pairs values 0/1 and 2/3 and the
+// row swap pairs the two results, so one swap + one add serves two values (row g of t then holds value
+// {0, 2, 1, 3}[g] as (row 0 + row 2) + (row 1 + row 3) -- rowgroup_sum's association, the same bits);
+// three more swaps broadcast the four totals back to every row.  12 instructions instead of ~24.
 __device__ __forceinline__ f4 rowgroup_sum4(f4 v) {
+#if TRPO_RGS4_T
+    const auto p01 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[0]), __float_as_uint(v[1]), false, false);
+    const auto p23 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[2]), __float_as_uint(v[3]), false, false);
+    const float s01 = __uint_as_float(p01[0]) + __uint_as_float(p01[1]);   // rows: v0, v0, v1, v1 (half sums)
+    const float s23 = __uint_as_float(p23[0]) + __uint_as_float(p23[1]);   // rows: v2, v2, v3, v3
+    const auto q = __builtin_amdgcn_permlane16_swap(__float_as_uint(s01), __float_as_uint(s23), false, false);
+    const float t = __uint_as_float(q[0]) + __uint_as_float(q[1]);         // rows: v0, v2, v1, v3
+    const auto h = __builtin_amdgcn_permlane32_swap(__float_as_uint(t), __float_as_uint(t), false, false);
+    const auto b02 = __builtin_amdgcn_permlane16_swap(h[0], h[0], false, false);   // rows 0, 1 of t
+    const auto b13 = __builtin_amdgcn_permlane16_swap(h[1], h[1], false, false);   // rows 2, 3 of t
+    f4 r;
+    r[0] = __uint_as_float(b02[0]);
+    r[1] = __uint_as_float(b13[0]);
+    r[2] = __uint_as_float(b02[1]);
+    r[3] = __uint_as_float(b13[1]);
+    return r;
+#else
     f4 r;
 #pragma unroll
     for (int i = 0; i < 4; ++i) r[i] = rowgroup_sum(v[i]);
     return r;
+#endif
 }
 
 // Transpose scratch of fvp_mlp3_kernel: scr_put writes lane (c, g)'s accumulator rows 4g + r of
@@ -1386,6 +1414,7 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
 
     // NT independent tiles per loop trip (ILP: the scheduler interleaves their MFMA chains)
     constexpr int NT = C::NT;
+    [[maybe_unused]] const int pf_xoff = (c * (4 * T0) + g) * 16, pf_yoff = lane * 16;   // prefetch lane offsets (bytes)
     // one tile (NT tiles) of work: inputs x0, the cached activations ycur, live columns
     auto tile_step = [&](const int tile, const f4 (&x0)[NT][T0], const f4 (&ycur)[YC ? NYC : 1],
                          const bool (&live)[NT]) __attribute__((always_inline)) {
@@ -1736,6 +1765,28 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
         }
         if constexpr (TRPO_DIAG_NOLOAD != 1) {   // unconditional (clamped) prefetch of the next trip's first tile
             const int tn = min(tile + NT * nwaves, ntiles - 1);
+#if TRPO_BUF_PF
+            // buffer loads off per-trip descriptors of the tile's records: the wave-uniform part of the
+            // address is SALU work, the lane offsets loop-invariant (no per-trip VALU address arithmetic)
+            if constexpr (TRPO_DIAG_NOLOAD != 2) {
+                const auto rx = __builtin_amdgcn_make_buffer_rsrc((void *)(obs4 + (long)tn * (16 * 4 * T0)), 0,
+                                                                  16 * 64 * T0, 0x00020000);
+#pragma unroll
+                for (int kt = 0; kt < T0; ++kt)
+                    xn[kt] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rx, pf_xoff + kt * 64, 0, 0));
+            }
+            if constexpr (YC && TRPO_DIAG_NOLOAD != 3) {
+                const auto ry = __builtin_amdgcn_make_buffer_rsrc((void *)(yc4 + (long)tn * (NYC * 64)), 0, NYC * 1024,
+                                                                  0x00020000);
+#pragma unroll
+                for (int k = 0; k < T1 + T2; ++k)
+                    yn[k] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ry, pf_yoff + k * 1024, 0, 0));
+                if (y3_needed)
+#pragma unroll
+                    for (int k = T1 + T2; k < NYC; ++k)
+                        yn[k] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ry, pf_yoff + k * 1024, 0, 0));
+            }
+#else
             if constexpr (TRPO_DIAG_NOLOAD != 2) {
 #pragma unroll
                 for (int kt = 0; kt < T0; ++kt) xn[kt] = stream_ld(obs4 + (long)(tn * 16 + c) * (4 * T0) + kt * 4 + g);
@@ -1747,6 +1798,7 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
 #pragma unroll
                     for (int k = T1 + T2; k < NYC; ++k) yn[k] = stream_ld(yc4 + ((long)tn * NYC + k) * 64 + lane);
             }
+#endif
 #if TRPO_PF_PIN
             // keep the prefetch at the top of the trip: left to itself the scheduler sinks it to
             // the loop latch, where the x0 = xn copy then waits out a full memory round trip
