@@ -46,3 +46,27 @@ def test_repeated_solves_bitwise():
         xs = [ctx.cg(b, 10, 0.0) for _ in range(3)] + [ctx.cg(b * 1e-3, 10, 1e-9), ctx.cg(b, 10, 0.0)]
     for x in (xs[1], xs[2], xs[4]):
         np.testing.assert_array_equal(x, xs[0])
+
+
+def test_small_net_solves_after_early_stop_bitwise():
+    """armDOF_0 (one-wave-per-tile kernels, fp64 atomic targets): the next solve's first atomic target is
+    zeroed by the last step even when the solve has stopped early -- solves after early stops and after
+    short solves give the bits of a fresh context's solve."""
+    L = [15, 16, 16, 3]
+    th, obs, std, b = _problem(L, 50000, 13)
+    with trpo_amd.Context(L, "lttl", th, obs, std, 0.1) as ref:
+        x_ref = ref.cg(b, 10, 0.0)
+        x2_ref = ref.cg(b, 2, 0.0)
+    with trpo_amd.Context(L, "lttl", th, obs, std, 0.1) as ctx:
+        x_stop = ctx.cg(b, 10, 1e30)            # stops at iteration 0
+        x_early = ctx.cg(b * 1e-3, 10, 1e-9)     # stops after a few iterations
+        x_full = ctx.cg(b, 10, 0.0)
+        x_two = ctx.cg(b, 2, 0.0)
+        x_one = ctx.cg(b, 1, 0.0)
+        x_again = ctx.cg(b, 10, 0.0)
+    assert np.all(x_stop == 0.0)
+    assert np.all(np.isfinite(x_early))
+    np.testing.assert_array_equal(x_full, x_ref)
+    np.testing.assert_array_equal(x_two, x2_ref)
+    assert np.all(np.isfinite(x_one))
+    np.testing.assert_array_equal(x_again, x_ref)
