@@ -151,17 +151,41 @@ def make_ctx(L, n_total, dist, device, precision=None, comm="rccl"):
     lo, hi = shard_range(n_total, dist.rank, dist.world)
     obs = synth.make_obs(hi - lo, L[0], start=lo)
     ctx = trpo_amd.Context(L, "lttl", theta, obs, np.ones(L[-1]), DAMPING, device=device, precision=precision)
-    if dist.world > 1 and comm == "peer":
-        handles = dist.allgather_bytes(ctx.peer_handle())
-        ctx.attach_peers(dist.rank, dist.world, handles)
-    elif dist.world > 1:
-        uid = dist.bcast_bytes(trpo_amd.unique_id() if dist.rank == 0 else None)
-        ctx.attach_comm(dist.rank, dist.world, uid)
-    if dist.world > 1:
-        info = ctx.comm_info()
-        if info["world"] != dist.world:
-            raise SystemExit("RCCL communicator has %d ranks, expected %d" % (info["world"], dist.world))
+    try:
+        if dist.world > 1 and comm == "peer":
+            handles = dist.allgather_bytes(ctx.peer_handle())
+            ctx.attach_peers(dist.rank, dist.world, handles)
+        elif dist.world > 1:
+            uid = dist.bcast_bytes(trpo_amd.unique_id() if dist.rank == 0 else None)
+            ctx.attach_comm(dist.rank, dist.world, uid)
+        if dist.world > 1:
+            info = ctx.comm_info()
+            if info["world"] != dist.world:
+                raise RuntimeError("%s communicator has %d ranks, expected %d" % (comm, info["world"], dist.world))
+    except BaseException:
+        ctx.close()
+        raise
     return ctx, theta, obs
+
+
+def make_ctx_agreed(L, n_total, dist, device, comm):
+    """The headline context at N > 1: attach `comm`; if it fails on ANY rank (the ranks agree over gloo),
+    every rank drops its context and attaches the other backend instead, so the scaling run still
+    measures the sharded solve.  Returns (ctx, theta, obs, backend used, fallback record or None)."""
+    tried = []
+    for c in (comm, "rccl" if comm == "peer" else "peer"):
+        ctx, err = None, None
+        try:
+            ctx, theta, obs = make_ctx(L, n_total, dist, device, comm=c)
+        except Exception as e:                  # noqa: BLE001 -- agreed below, every rank moves on together
+            err = "%s: %s" % (type(e).__name__, e)
+        if dist.max(0.0 if err is None else 1.0) == 0.0:
+            return ctx, theta, obs, c, ({"requested": comm, "failed": tried} if tried else None)
+        if ctx is not None:
+            ctx.close()
+        tried.append({"comm": c, "rank": dist.rank, "error": err or "another rank failed to attach"})
+        print("bench.py: rank %d: %s attach failed (%s)" % (dist.rank, c, tried[-1]["error"]), file=sys.stderr)
+    raise SystemExit("bench.py: neither collective attached: %s" % tried)
 
 
 def time_steps(ctx, dist, steps, warmup, b):
@@ -489,12 +513,20 @@ def main():
     if world != args.gpus:                       # before any rendezvous or device use
         print("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world), file=sys.stderr)
         sys.exit(2)
+    # stdout carries exactly one line (rank 0's JSON): what RCCL, gloo and the runtimes print to fd 1
+    # (RCCL's version banner, gloo's connection notice) goes to stderr from here on
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     import trpo_amd
     trpo_amd.lib()                               # the system ROCm runtime before torch's (Dist)
     dist = Dist()
     device = int(os.environ.get("TRPO_BENCH_DEVICE", dist.local_rank))   # override: testing only
 
-    ctx, theta, obs_local = make_ctx(ARM, N_TOTAL, dist, device, comm=args.comm)
+    if dist.world > 1:
+        ctx, theta, obs_local, args.comm, fallback = make_ctx_agreed(ARM, N_TOTAL, dist, device, args.comm)
+    else:
+        (ctx, theta, obs_local), fallback = make_ctx(ARM, N_TOTAL, dist, device), None
     comm = ctx.comm_info()
     P = num_params(ARM)
     b = synth.make_b(P)
@@ -545,7 +577,8 @@ def main():
                                   % (dist.world, "RCCL" if args.comm == "rccl" else "peer-window"),
                    "cg_scalars": "fp64", "fvp_kernel": ctx.kernel_name, "geometry": ctx.geometry},
         "comm": {"backend": comm["backend"], "ranks": comm["world"],
-                 "replicas_per_fvp": comm["replicas"], "hip_runtime": trpo_amd.runtime_path()},
+                 "replicas_per_fvp": comm["replicas"], "hip_runtime": trpo_amd.runtime_path(),
+                 "fallback": fallback},
         "cg_wall_ms": ms_per_step,
         "roofline": {"bound": "hbm" if hbm_bound else "mfma",
                      "achieved": achieved_gbs if hbm_bound else achieved_tflops,
@@ -580,8 +613,10 @@ def main():
         result["parity"] = {"cg_step_relL2_vs_cpu": rel, "tolerance": 1e-4}
     ctx.close()
     dist.close()
-    if dist.rank == 0:
-        print(json.dumps(result), flush=True)
+    sys.stdout.flush()
+    with os.fdopen(json_fd, "w") as out:
+        if dist.rank == 0:
+            out.write(json.dumps(result) + "\n")
 
 
 if __name__ == "__main__":

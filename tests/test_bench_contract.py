@@ -35,3 +35,62 @@ def test_rank_count_mismatch_exits_nonzero():
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 2
     assert "WORLD_SIZE=3" in r.stderr
+
+
+class _FakeDist:
+    """Two ranks seen from rank 0; `peer_fails` = backends whose attach fails on the OTHER rank."""
+
+    def __init__(self, peer_fails=()):
+        self.world, self.rank, self.peer_fails, self.current = 2, 0, set(peer_fails), None
+
+    def max(self, x):
+        return max(x, 1.0 if self.current in self.peer_fails else 0.0)
+
+
+class _FakeCtx:
+    def __init__(self, comm):
+        self.comm, self.closed = comm, False
+
+    def close(self):
+        self.closed = True
+
+
+def _agreed(monkeypatch, local_fails=(), peer_fails=(), comm="rccl"):
+    b = _bench()
+    dist = _FakeDist(peer_fails)
+    made = []
+
+    def fake_make_ctx(L, n, d, device, comm="rccl"):
+        dist.current = comm
+        if comm in local_fails:
+            raise RuntimeError("attach_%s failed (-4)" % comm)
+        made.append(_FakeCtx(comm))
+        return made[-1], "theta", "obs"
+
+    monkeypatch.setattr(b, "make_ctx", fake_make_ctx)
+    return b, dist, made, b.make_ctx_agreed(b.ARM, b.N_TOTAL, dist, 0, comm)
+
+
+def test_headline_collective_agreed_no_fallback(monkeypatch):
+    _, _, made, (ctx, _, _, used, fb) = _agreed(monkeypatch)
+    assert used == "rccl" and fb is None and ctx is made[0] and not ctx.closed
+
+
+def test_headline_falls_back_when_this_rank_fails(monkeypatch):
+    """RCCL refusing to attach (e.g. two ranks on one device) moves every rank to the peer exchange."""
+    _, _, made, (ctx, _, _, used, fb) = _agreed(monkeypatch, local_fails={"rccl"})
+    assert used == "peer" and ctx.comm == "peer"
+    assert fb["requested"] == "rccl" and "attach_rccl failed" in fb["failed"][0]["error"]
+
+
+def test_headline_falls_back_when_another_rank_fails(monkeypatch):
+    """This rank attached but another did not: its context is closed and it moves on with the others."""
+    _, _, made, (ctx, _, _, used, fb) = _agreed(monkeypatch, peer_fails={"rccl"})
+    assert used == "peer" and made[0].closed and not ctx.closed
+    assert fb["failed"][0]["error"] == "another rank failed to attach"
+
+
+def test_headline_exits_when_no_collective_attaches(monkeypatch):
+    import pytest
+    with pytest.raises(SystemExit):
+        _agreed(monkeypatch, local_fails={"rccl", "peer"})
