@@ -6,7 +6,8 @@ and the fp64 oracle is far too slow.  Size-independent properties only:
     un-normalised weight block over all N equals the sum of the blocks of two contexts holding the
     halves of the same seeded sample stream -- (z - lambda v) N = (z1 - lambda v) N1 + (z2 - lambda v) N2
     -- which checks the full-size cross-block accumulation against independent smaller launches
-    (fp32 per-sample math, different block partition: relative 1e-5);
+    (fp32 block partials added in fp64, different block partition: measured 3.5e-9 at both sizes,
+    tools/diag/large_n_decomposition.py; bound 1e-7);
   * the CG step's true residual against the recurrence's reported one (src/TRPO_CG.c:56).
 """
 import numpy as np
@@ -53,7 +54,7 @@ def test_fvp_properties_and_shard_decomposition(n):
     nw = P - A
     full = (zu[:nw] - LAM * u[:nw]) * n
     parts = (z1[:nw] - LAM * u[:nw]) * n1 + (z2[:nw] - LAM * u[:nw]) * (n - n1)
-    assert _rel(full, parts) <= 1e-5
+    assert _rel(full, parts) <= 1e-7
 
 
 def test_cg_residual_matches_reported_4m():
