@@ -1,4 +1,4 @@
-"""MI355X: the armDOF_0 FVP and CG at the C4 sweep's batch sizes (N = 500k and 4M), where
+"""MI355X: the armDOF_0 FVP and CG at the C4 sweep's batch sizes (and the 2x64 cooperative FVP) (N = 500k and 4M), where
 the throughput-regime kernel variants run (the narrow-output twin picked by tiles per wave, §5.1b)
 and the fp64 oracle is far too slow.  Size-independent properties only:
   * linearity, symmetry, positivity and the exact log-std block, as tests/test_gpu_properties.py at 50k;
@@ -6,7 +6,8 @@ and the fp64 oracle is far too slow.  Size-independent properties only:
     un-normalised weight block over all N equals the sum of the blocks of two contexts holding the
     halves of the same seeded sample stream -- (z - lambda v) N = (z1 - lambda v) N1 + (z2 - lambda v) N2
     -- which checks the full-size cross-block accumulation against independent smaller launches
-    (fp32 block partials added in fp64, different block partition: measured 3.5e-9 at both sizes,
+    (fp32 block partials added in fp64, different block partition: measured 3.5e-9 for armDOF_0 at 500k
+    and 4M, 3.4e-9 / 6.8e-9 for the 2x64 cooperative slab path at 50k / 500k,
     tools/diag/large_n_decomposition.py; bound 1e-7);
   * the CG step's true residual against the recurrence's reported one (src/TRPO_CG.c:56).
 """
@@ -24,32 +25,37 @@ STD = np.array([0.8, 1.0, 1.3])
 SIZES = [500_000, 4_000_000]
 
 
-def _ctx(n, start=0):
-    return trpo_amd.Context(ARM, "lttl", synth.make_theta(ARM), synth.make_obs(n, ARM[0], start=start), STD, LAM)
+def _ctx(n, start=0, layers=ARM):
+    return trpo_amd.Context(layers, "lttl", synth.make_theta(layers), synth.make_obs(n, layers[0], start=start), STD,
+                            LAM)
 
 
 def _rel(a, b):
     return float(np.linalg.norm(a - b) / np.linalg.norm(b))
 
 
-@pytest.mark.parametrize("n", SIZES)
-def test_fvp_properties_and_shard_decomposition(n):
-    P = synth.num_params(ARM)
+W64 = [15, 64, 64, 3]
+CASES = [(ARM, n) for n in SIZES] + [(W64, 50_000), (W64, 500_000)]   # + the cooperative slab path (2x64)
+
+
+@pytest.mark.parametrize("layers,n", CASES, ids=["%s-%d" % ("x".join(map(str, l)), n) for l, n in CASES])
+def test_fvp_properties_and_shard_decomposition(layers, n):
+    P = synth.num_params(layers)
     rng = np.random.default_rng(23)
     u, w = rng.standard_normal(P), rng.standard_normal(P)
     a, b = -0.6, 1.3
-    with _ctx(n) as ctx:
+    with _ctx(n, layers=layers) as ctx:
         zu, zw, zc = ctx.fvp(u), ctx.fvp(w), ctx.fvp(a * u + b * w)
     assert _rel(zc, a * zu + b * zw) <= 1e-5
     assert abs(u @ zw - w @ zu) <= 1e-5 * abs(u @ zw)
     for v, z in ((u, zu), (w, zw)):
         assert v @ z >= LAM * (v @ v)
-    A = ARM[-1]
+    A = layers[-1]
     np.testing.assert_array_equal(zu[-A:], 2.0 * u[-A:] + LAM * u[-A:])
     n1 = n // 2 + 37                                   # uneven halves, not tile multiples
-    with _ctx(n1) as c1:
+    with _ctx(n1, layers=layers) as c1:
         z1 = c1.fvp(u)
-    with _ctx(n - n1, start=n1) as c2:
+    with _ctx(n - n1, start=n1, layers=layers) as c2:
         z2 = c2.fvp(u)
     nw = P - A
     full = (zu[:nw] - LAM * u[:nw]) * n
