@@ -105,8 +105,11 @@ class Dist:
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
         if self.world > 1:
+            import datetime
             import torch.distributed as dist
-            dist.init_process_group("gloo")
+            # every rendezvous / agreement is bounded: a rank that dies makes the others raise, not hang
+            dist.init_process_group("gloo", timeout=datetime.timedelta(
+                seconds=int(os.environ.get("TRPO_GLOO_TIMEOUT_S", "600"))))
             self.dist = dist
 
     def barrier(self):
@@ -142,7 +145,8 @@ class Dist:
 
 def make_ctx(L, n_total, dist, device, precision=None, comm="rccl"):
     """This rank's context: all weights, its contiguous shard of the seeded observation stream.
-    comm: "rccl" (RCCL communicator) or "peer" (the peer-window exchange over xGMI, csrc/trpo_peer.hip)."""
+    comm: "rccl" (RCCL communicator) or "peer" (the peer-window exchange over xGMI, csrc/trpo_peer.hip).
+    For the secondary configs; the headline context is built by make_ctx_agreed."""
     import numpy as np
     import trpo_amd
     from trpo_amd import synth
@@ -157,7 +161,7 @@ def make_ctx(L, n_total, dist, device, precision=None, comm="rccl"):
             ctx.attach_peers(dist.rank, dist.world, handles)
         elif dist.world > 1:
             uid = dist.bcast_bytes(trpo_amd.unique_id() if dist.rank == 0 else None)
-            ctx.attach_comm(dist.rank, dist.world, uid)
+            ctx.attach_comm(dist.rank, dist.world, uid, COMM_TIMEOUT_MS)
         if dist.world > 1:
             info = ctx.comm_info()
             if info["world"] != dist.world:
@@ -168,89 +172,212 @@ def make_ctx(L, n_total, dist, device, precision=None, comm="rccl"):
     return ctx, theta, obs
 
 
-def make_ctx_agreed(L, n_total, dist, device, comm):
-    """The headline context at N > 1: attach `comm`; if it fails on ANY rank (the ranks agree over gloo),
-    every rank drops its context and attaches the other backend instead, so the scaling run still
-    measures the sharded solve.  Returns (ctx, theta, obs, backend used, fallback record or None)."""
-    tried = []
-    for c in (comm, "rccl" if comm == "peer" else "peer"):
-        ctx, err = None, None
+COMM_TIMEOUT_MS = int(os.environ.get("TRPO_BENCH_COMM_TIMEOUT_MS", "60000"))   # RCCL init, self-check, solve
+STAGES = ("context", "bootstrap", "attach", "verify", "solve", "hash")
+
+
+class StageFault(RuntimeError):
+    pass
+
+
+def _fault(stage, rank, attempt):
+    """TRPO_BENCH_FAULT=<stage>:<rank>[:<attempt>] (testing): make `stage` fail on `rank` in attempt
+    `attempt` (default 0) of the headline's collective setup.  Stages: STAGES, plus comm-verify /
+    comm-hang, which arm the LIBRARY's self-check fault (TRPO_COMM_FAULT) for that attempt."""
+    spec = os.environ.get("TRPO_BENCH_FAULT", "")
+    if not spec:
+        return False
+    f = spec.split(":")
+    return f[0] == stage and int(f[1]) == rank and (int(f[2]) if len(f) > 2 else 0) == attempt
+
+
+def x_digest(x):
+    import hashlib
+    import numpy as np
+    return hashlib.sha256(np.ascontiguousarray(x, np.float64).tobytes()).hexdigest()[:16]
+
+
+def make_ctx_agreed(L, n_total, dist, device, comm, b, plan=None):
+    """The headline context at N > 1, set up stage by stage with the ranks agreeing (over gloo) after
+    EVERY stage, so a failure on one rank alone never leaves the others in a mismatched collective:
+      context   create this rank's context (its shard)
+      bootstrap the RCCL unique id on rank 0 (then broadcast) / this rank's peer window handle (then
+                all-gathered)
+      attach    RCCL init bounded by COMM_TIMEOUT_MS / the peer attach (its 3-s exchange bound)
+      verify    the library's self-check: one eager all-reduce of a rank-dependent vector, completion
+                bounded, the exact sum checked bit for bit (trpo_ctx_comm_verify)
+      solve     one graph-replayed sharded 10-iteration CG solve, completion bounded (trpo_ctx_wait)
+      hash      x from every rank: identical bits (sha256 all-gathered)
+    On a failure anywhere every rank aborts its collective (ncclCommAbort / the peer error flag), closes
+    its context and moves to the next backend of `plan` (default: the requested one, the other, the
+    requested one again); SystemExit when none passes.
+    Returns (ctx, theta, obs, backend, record) -- record = {"verify": ..., "fallback": [...] or None}."""
+    import numpy as np
+    import trpo_amd
+    from trpo_amd import synth
+    from trpo_amd.dist import shard_range
+    other = "rccl" if comm == "peer" else "peer"
+    failed = []
+    for attempt, c in enumerate(plan or (comm, other, comm)):
+        ctx, stage, err, attached, digest = None, None, None, False, None
+        lib_fault = None
+        for kind in ("comm-verify", "comm-hang"):
+            if _fault(kind, dist.rank, attempt):
+                lib_fault = "%s:%d" % (kind.split("-")[1], dist.rank)
+        saved = os.environ.pop("TRPO_COMM_FAULT", None)
+        if lib_fault:
+            os.environ["TRPO_COMM_FAULT"] = lib_fault
+        t0 = time.perf_counter()
         try:
-            ctx, theta, obs = make_ctx(L, n_total, dist, device, comm=c)
-        except Exception as e:                  # noqa: BLE001 -- agreed below, every rank moves on together
-            err = "%s: %s" % (type(e).__name__, e)
-        if dist.max(0.0 if err is None else 1.0) == 0.0:
-            return ctx, theta, obs, c, ({"requested": comm, "failed": tried} if tried else None)
-        if ctx is not None:
-            ctx.close()
-        tried.append({"comm": c, "rank": dist.rank, "error": err or "another rank failed to attach"})
-        print("bench.py: rank %d: %s attach failed (%s)" % (dist.rank, c, tried[-1]["error"]), file=sys.stderr)
-    raise SystemExit("bench.py: neither collective attached: %s" % tried)
+            for stage in STAGES:
+                try:
+                    if _fault(stage, dist.rank, attempt):
+                        raise StageFault("injected fault (TRPO_BENCH_FAULT)")
+                    if stage == "context":
+                        theta = synth.make_theta(L)
+                        lo, hi = shard_range(n_total, dist.rank, dist.world)
+                        obs = synth.make_obs(hi - lo, L[0], start=lo)
+                        ctx = trpo_amd.Context(L, "lttl", theta, obs, np.ones(L[-1]), DAMPING, device=device)
+                    elif stage == "bootstrap":
+                        boot = ctx.peer_handle() if c == "peer" else (trpo_amd.unique_id() if dist.rank == 0 else None)
+                    elif stage == "attach":
+                        if c == "peer":
+                            ctx.attach_peers(dist.rank, dist.world, boot)
+                        else:
+                            ctx.attach_comm(dist.rank, dist.world, boot, COMM_TIMEOUT_MS)
+                        attached = True
+                        info = ctx.comm_info()
+                        if info["world"] != dist.world:
+                            raise RuntimeError("%s communicator has %d ranks, expected %d"
+                                               % (c, info["world"], dist.world))
+                    elif stage == "verify":
+                        ctx.comm_verify(COMM_TIMEOUT_MS)
+                    elif stage == "solve":
+                        ctx.upload_b(b)
+                        ctx.enqueue_cg(CG_ITERS, 0.0)
+                        ctx.wait(COMM_TIMEOUT_MS)
+                        digest = x_digest(ctx.download_x())
+                except Exception as e:          # noqa: BLE001 -- agreed below, every rank moves on together
+                    err = "%s: %s" % (type(e).__name__, e)
+                # agreement after the stage; the collective parts of bootstrap / hash run only if all agree
+                if dist.max(0.0 if err is None else 1.0) != 0.0:
+                    raise StageFault(err or "another rank failed at stage %s" % stage)
+                if stage == "bootstrap":
+                    boot = dist.allgather_bytes(boot) if c == "peer" else dist.bcast_bytes(boot)
+                elif stage == "hash":
+                    digests = dist.allgather_bytes(digest.encode())
+                    if len(set(digests)) != 1 or _fault("hash-mismatch", dist.rank, attempt):
+                        err = "x differs across ranks: %s" % sorted(set(d.decode() for d in digests))
+                    if dist.max(0.0 if err is None else 1.0) != 0.0:
+                        raise StageFault(err or "another rank saw differing x")
+            record = {"verify": {"stages": list(STAGES), "eager_allreduce_exact": True, "x_sha256_16": digest,
+                                 "x_identical_on_all_ranks": True, "attempt": attempt,
+                                 "setup_s": time.perf_counter() - t0},
+                      "fallback": ({"requested": comm, "failed": failed} if failed else None)}
+            return ctx, theta, obs, c, record
+        except StageFault as e:
+            if ctx is not None:
+                if attached:
+                    ctx.comm_abort()
+                ctx.close()
+            failed.append({"attempt": attempt, "comm": c, "stage": stage, "rank": dist.rank, "error": str(e)})
+            print("bench.py: rank %d: %s failed at stage %s (%s)" % (dist.rank, c, stage, e), file=sys.stderr)
+        finally:
+            os.environ.pop("TRPO_COMM_FAULT", None)
+            if saved is not None:
+                os.environ["TRPO_COMM_FAULT"] = saved
+    raise SystemExit("bench.py: no collective passed setup and self-check: %s" % failed)
 
 
 def time_steps(ctx, dist, steps, warmup, b):
+    """K timed solves after W warm-up ones, bracketed by barrier + completion on both sides; the wait
+    is bounded at N > 1 (trpo_ctx_wait spins on the stream, so it costs what a synchronize costs)."""
+    wait = ctx.synchronize if dist.world == 1 else (lambda: ctx.wait(COMM_TIMEOUT_MS))
     ctx.upload_b(b)
     for _ in range(warmup):
         ctx.enqueue_cg(CG_ITERS, 0.0)
-    ctx.synchronize()
+    wait()
     dist.barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
         ctx.enqueue_cg(CG_ITERS, 0.0)
-    ctx.synchronize()
+    wait()
     t1 = time.perf_counter()
     dist.barrier()
     return dist.max(t1 - t0)
+
+
+def _cpu_model():
+    try:
+        return [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if "model name" in l][0]
+    except Exception:
+        return None
+
+
+CPU_FLAGS = "gcc -O3 -march=x86-64-v3 -fopenmp (Makefile.cpuonly flags, portable -march)"
+
+
+def _ref_run(mode, mf, df, nn, vec, extra, threads):
+    """oracle/_ref/ref_driver_fast: the reference's own TRPO_FVP.c / TRPO_CG.c / TRPO_Update.c."""
+    import oracle
+    cmd = [oracle.REF_DRIVER_FAST, mode, mf, df, str(nn), ",".join(map(str, ARM)), "lttl", str(DAMPING), vec]
+    cmd += extra + [str(threads)]
+    p = subprocess.run(cmd, capture_output=True, text=True)
+    if p.returncode != 0:
+        raise RuntimeError("%s failed: %s" % (mode, p.stderr[-400:]))
+    return json.loads(p.stderr.strip().splitlines()[-1])
+
+
+def cpu_reference_cg(theta, obs_all, b):
+    """The reference's CG (src/TRPO_CG.c) on all of obs_all, one host core: (headline record, x_ref).
+    Falls back to the clean-room port where the reference build is absent (kind "port")."""
+    import numpy as np
+    import oracle
+    from trpo_amd import synth
+    n = obs_all.shape[0]
+    if not os.path.exists(oracle.REF_DRIVER_FAST):
+        r = oracle.cg(ARM, "lttl", theta, obs_all, np.ones(ARM[-1]), b, CG_ITERS, 0.0, DAMPING, threads=1)
+        head = dict(value=CG_ITERS * n / r["seconds"], unit="FVP samples/s", cores=1, kind="port",
+                    sample="one 10-iteration CG solve, armDOF_0, N=%d, ResidualTh=0, clean-room port, 1 thread" % n,
+                    compute_s=r["seconds"], cpu_model=_cpu_model())
+        return head, r["x"]
+    with tempfile.TemporaryDirectory() as tmp:
+        mf, df, bf, xf = (os.path.join(tmp, f) for f in ("m.txt", "d.txt", "b.txt", "x.txt"))
+        synth.write_model_file(mf, theta)
+        synth.write_data_file(df, obs_all, np.ones(ARM[-1]))
+        synth.write_vector_file(bf, b)
+        t1 = _ref_run("cg", mf, df, n, bf, [str(CG_ITERS), "0", xf], 1)
+        x_ref = np.loadtxt(xf)
+    head = dict(value=CG_ITERS * n / t1["compute_s"], unit="FVP samples/s", cores=1, kind="reference",
+                sample="one 10-iteration CG solve (the reference's CG, src/TRPO_CG.c), armDOF_0, N=%d, "
+                       "ResidualTh=0, NumThreads=1; compute seconds as CG returns them (file parsing excluded)" % n,
+                compute_s=t1["compute_s"], wall_s_incl_file_parse=t1["wall_s"], build=CPU_FLAGS,
+                cpu_model=_cpu_model())
+    return head, x_ref
 
 
 def cpu_rows(theta, obs_all, b, threads_all):
     """The reference itself (oracle/_ref/ref_driver_fast: src/TRPO_FVP.c + TRPO_CG.c compiled with the
     Makefile.cpuonly flags, -march=x86-64-v3) on this host: returns (headline, rows, x_ref)."""
     import numpy as np
-    import oracle
     from trpo_amd import synth
     n = obs_all.shape[0]
-    flags = "gcc -O3 -march=x86-64-v3 -fopenmp (Makefile.cpuonly flags, portable -march)"
-    try:
-        cpu_model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if "model name" in l][0]
-    except Exception:
-        cpu_model = None
+    head, x_ref = cpu_reference_cg(theta, obs_all, b)
     rows = []
-    if not os.path.exists(oracle.REF_DRIVER_FAST):
-        r = oracle.cg(ARM, "lttl", theta, obs_all, np.ones(ARM[-1]), b, CG_ITERS, 0.0, DAMPING, threads=1)
-        head = dict(value=CG_ITERS * n / r["seconds"], unit="FVP samples/s", cores=1, kind="port",
-                    sample="one 10-iteration CG solve, armDOF_0, N=%d, ResidualTh=0, clean-room port, 1 thread" % n,
-                    compute_s=r["seconds"], cpu_model=cpu_model)
-        return head, rows, r["x"]
-
-    def run(mode, mf, df, nn, vec, extra, threads):
-        cmd = [oracle.REF_DRIVER_FAST, mode, mf, df, str(nn), ",".join(map(str, ARM)), "lttl", str(DAMPING), vec]
-        cmd += extra + [str(threads)]
-        p = subprocess.run(cmd, capture_output=True, text=True)
-        if p.returncode != 0:
-            raise RuntimeError("%s failed: %s" % (mode, p.stderr[-400:]))
-        return json.loads(p.stderr.strip().splitlines()[-1])
-
+    if head["kind"] != "reference":
+        return head, rows, x_ref
+    rows.append(dict(config="C3 CG10 armDOF_0 N=%d" % n, threads=1, compute_s=head["compute_s"],
+                     fvp_samples_per_s=head["value"]))
     with tempfile.TemporaryDirectory() as tmp:
-        mf, df, bf, xf = (os.path.join(tmp, f) for f in ("m.txt", "d.txt", "b.txt", "x.txt"))
+        mf, bf = os.path.join(tmp, "m.txt"), os.path.join(tmp, "b.txt")
         synth.write_model_file(mf, theta)
-        synth.write_data_file(df, obs_all, np.ones(ARM[-1]))
         synth.write_vector_file(bf, b)
-        t1 = run("cg", mf, df, n, bf, [str(CG_ITERS), "0", xf], 1)
-        x_ref = np.loadtxt(xf)
-        head = dict(value=CG_ITERS * n / t1["compute_s"], unit="FVP samples/s", cores=1, kind="reference",
-                    sample="one 10-iteration CG solve (the reference's CG, src/TRPO_CG.c), armDOF_0, N=%d, "
-                           "ResidualTh=0, NumThreads=1; compute seconds as CG returns them (file parsing excluded)"
-                           % n,
-                    compute_s=t1["compute_s"], wall_s_incl_file_parse=t1["wall_s"], build=flags, cpu_model=cpu_model)
-        rows.append(dict(config="C3 CG10 armDOF_0 N=%d" % n, threads=1, compute_s=t1["compute_s"],
-                         fvp_samples_per_s=CG_ITERS * n / t1["compute_s"]))
         # all host cores: the reference's per-neuron OpenMP fork/join anti-scales (SURVEY §3.3), so a
         # bounded sample -- the first 5 000 samples, one 10-iteration solve -- keeps this row to seconds
         ns = min(n, 5000)
         df5 = os.path.join(tmp, "d5.txt")
         synth.write_data_file(df5, obs_all[:ns], np.ones(ARM[-1]))
-        ta = run("time", mf, df5, ns, bf, [str(CG_ITERS), "0"], threads_all)
+        ta = _ref_run("time", mf, df5, ns, bf, [str(CG_ITERS), "0"], threads_all)
         rows.append(dict(config="C3 CG10 armDOF_0 N=%d (bounded sample of the N=%d workload)" % (ns, n),
                          threads=threads_all, compute_s=ta["compute_s"],
                          fvp_samples_per_s=CG_ITERS * ns / ta["compute_s"]))
@@ -262,8 +389,8 @@ def cpu_rows(theta, obs_all, b, threads_all):
         synth.write_vector_file(vf, np.loadtxt(os.path.join(g, "ArmTestFVP.txt"))[:, 0])
         synth.write_vector_file(bf2, np.loadtxt(os.path.join(g, "ArmTestCG.txt"))[:, 0])
         for th in (1, threads_all):
-            tf = run("fvp", mfix, dfix, 3150, vf, [of], th)
-            tc = run("time", mfix, dfix, 3150, bf2, ["10", "1e-10"], th)
+            tf = _ref_run("fvp", mfix, dfix, 3150, vf, [of], th)
+            tc = _ref_run("time", mfix, dfix, 3150, bf2, ["10", "1e-10"], th)
             rows.append(dict(config="C1 fixture FVPFast N=3150", threads=th, compute_s=tf["compute_s"],
                              fvp_samples_per_s=3150 / tf["compute_s"]))
             rows.append(dict(config="C1 fixture CG(10, 1e-10) N=3150 (8 FVPs)", threads=th,
@@ -415,23 +542,18 @@ def extras_multi(device, dist, b, x_rccl, comm="rccl"):
     res, ctx = None, None
     other = "rccl" if comm == "peer" else "peer"
     try:
-        ctx, _, _ = make_ctx(ARM, N_TOTAL, dist, device, comm=other)
-        ok = 1.0
-    except Exception as e:                      # noqa: BLE001 -- recorded, every rank skips together
-        res = {"error": "%s: %s" % (type(e).__name__, e)}
-        ok = 0.0
-    if dist.max(1.0 - ok) == 0.0:               # all ranks attached
+        ctx, _, _, _, rec = make_ctx_agreed(ARM, N_TOTAL, dist, device, other, b, plan=(other,))
+    except SystemExit as e:                     # recorded; every rank skips together (agreed inside)
+        res = {"error": str(e)}
+    if ctx is not None:
         try:
             t = time_steps(ctx, dist, 50, 5, b)
             x = ctx.download_x()
             res = {"ms_per_step": 1e3 * t / 50, "fvp_samples_per_s": CG_ITERS * N_TOTAL / (t / 50),
-                   "backend": ctx.comm_backend, "n_gpus": dist.world,
+                   "backend": ctx.comm_backend, "n_gpus": dist.world, "verify": rec["verify"],
                    "x_relL2_vs_headline": float(np.linalg.norm(x - x_rccl) / np.linalg.norm(x_rccl))}
         except Exception as e:                  # noqa: BLE001
             res = {"error": "%s: %s" % (type(e).__name__, e)}
-    elif res is None:
-        res = {"error": "another rank failed to attach"}
-    if ctx is not None:
         ctx.close()
     out["C4_%s_exchange" % other] = res
     try:
@@ -523,13 +645,13 @@ def main():
     dist = Dist()
     device = int(os.environ.get("TRPO_BENCH_DEVICE", dist.local_rank))   # override: testing only
 
-    if dist.world > 1:
-        ctx, theta, obs_local, args.comm, fallback = make_ctx_agreed(ARM, N_TOTAL, dist, device, args.comm)
-    else:
-        (ctx, theta, obs_local), fallback = make_ctx(ARM, N_TOTAL, dist, device), None
-    comm = ctx.comm_info()
     P = num_params(ARM)
     b = synth.make_b(P)
+    if dist.world > 1:
+        ctx, theta, obs_local, args.comm, setup = make_ctx_agreed(ARM, N_TOTAL, dist, device, args.comm, b)
+    else:
+        (ctx, theta, obs_local), setup = make_ctx(ARM, N_TOTAL, dist, device), {"verify": None, "fallback": None}
+    comm = ctx.comm_info()
 
     t = time_steps(ctx, dist, args.steps, args.warmup, b)
     ms_per_step = 1e3 * t / args.steps
@@ -578,7 +700,7 @@ def main():
                    "cg_scalars": "fp64", "fvp_kernel": ctx.kernel_name, "geometry": ctx.geometry},
         "comm": {"backend": comm["backend"], "ranks": comm["world"],
                  "replicas_per_fvp": comm["replicas"], "hip_runtime": trpo_amd.runtime_path(),
-                 "fallback": fallback},
+                 "verify": setup["verify"], "fallback": setup["fallback"]},
         "cg_wall_ms": ms_per_step,
         "roofline": {"bound": "hbm" if hbm_bound else "mfma",
                      "achieved": achieved_gbs if hbm_bound else achieved_tflops,
@@ -611,6 +733,17 @@ def main():
         result["cpu_baseline"] = head
         rel = float(np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref))
         result["parity"] = {"cg_step_relL2_vs_cpu": rel, "tolerance": 1e-4}
+    elif dist.world > 1 and not args.no_cpu_baseline:
+        # the sharded solve's step against the reference's CG over the WHOLE batch (rank 0 regenerates
+        # the seeded 50k observations; the other ranks wait at the closing barrier)
+        if dist.rank == 0:
+            obs_all = synth.make_obs(N_TOTAL, ARM[0])
+            _, x_ref = cpu_reference_cg(theta, obs_all, b)
+            rel = float(np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref))
+            result["parity"] = {"cg_step_relL2_vs_cpu": rel, "tolerance": 1e-4,
+                                "what": "x of the %d-rank sharded solve vs the reference CG on all %d samples"
+                                        % (dist.world, N_TOTAL)}
+        dist.barrier()
     ctx.close()
     dist.close()
     sys.stdout.flush()

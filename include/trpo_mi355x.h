@@ -119,8 +119,10 @@ enum {
     TRPO_E_INVALID = -1,   /* bad shape, activation, NULL pointer */
     TRPO_E_DEVICE = -2,    /* no usable MI355X / HIP error */
     TRPO_E_NOMEM = -3,
-    TRPO_E_COMM = -4,      /* RCCL failure */
-    TRPO_E_IO = -5
+    TRPO_E_COMM = -4,      /* collective failure (RCCL, peer exchange timed out, aborted) */
+    TRPO_E_IO = -5,
+    TRPO_E_TIMEOUT = -6,   /* a bounded wait expired (RCCL init, self-check, trpo_ctx_wait) */
+    TRPO_E_VERIFY = -7     /* the collective's self-check summed wrong */
 };
 
 /* Create a context on HIP device `device` (-1: current / $TRPO_DEVICE / 0).
@@ -145,6 +147,10 @@ size_t trpo_ctx_num_params(const trpo_ctx *ctx);
  * on rank 0, broadcast by the caller. */
 int trpo_comm_unique_id(void *unique_id_128);
 int trpo_ctx_attach_comm(trpo_ctx *ctx, int rank, int world, const void *unique_id_128);
+/* The same with RCCL's initialisation bounded: ncclCommInitRank runs in a helper thread and the call
+ * returns TRPO_E_TIMEOUT when it has not completed after timeout_ms (<= 0: $TRPO_COMM_TIMEOUT_MS,
+ * default 120 000) -- e.g. a rank that never calls in; the plain attach uses that default too. */
+int trpo_ctx_attach_comm_timeout(trpo_ctx *ctx, int rank, int world, const void *unique_id_128, long timeout_ms);
 
 /* In-process sharding without RCCL: `world` contexts of ONE process, each driven by its own
  * thread (any devices, the same one included), attach to a host group and run the sharded code
@@ -177,7 +183,20 @@ int trpo_ctx_comm_info(const trpo_ctx *ctx, int *rank, int *world, int *replicas
 int trpo_ctx_peer_handle(trpo_ctx *ctx, void *handle_64);
 int trpo_ctx_attach_peers(trpo_ctx *ctx, int rank, int world, const void *handles);
 int trpo_ctx_attach_peers_local(trpo_ctx *ctx, int rank, int world, trpo_ctx *const *all);
-/* "rccl", "peer-xgmi (...)", "host-group" or "none" */
+/* Self-check of the attached collective (any backend), called by ALL ranks together before it carries
+ * results: one eager all-reduce, as long as the per-FVP message, of a rank-dependent test vector whose
+ * exact sum is known; completion awaited at most timeout_ms (<= 0: the default above), every element
+ * compared bit for bit.  0, TRPO_E_TIMEOUT (call trpo_ctx_comm_abort), TRPO_E_VERIFY or TRPO_E_COMM.
+ * No reference counterpart: the reference's CG (src/TRPO_CG.c:45-104) is single-process. */
+int trpo_ctx_comm_verify(trpo_ctx *ctx, long timeout_ms);
+/* Wait for the context's enqueued work (e.g. trpo_ctx_enqueue_cg) at most timeout_ms: 0,
+ * TRPO_E_TIMEOUT, or the collective's error. */
+int trpo_ctx_wait(trpo_ctx *ctx, long timeout_ms);
+/* Give up on the collective: ncclCommAbort (kernels blocked in it exit) or the peer exchange's error
+ * flag, the stream drained (bounded); every later result call fails with TRPO_E_COMM.  Destroy the
+ * context afterwards. */
+int trpo_ctx_comm_abort(trpo_ctx *ctx);
+/* "rccl", "peer-xgmi (...)", "host-group", "aborted" or "none" */
 const char *trpo_ctx_comm_backend(const trpo_ctx *ctx);
 /* Path of the HIP runtime (libamdhip64) this library's calls resolved to.  The library is built and
  * validated against the system ROCm (/opt/rocm); a process that loads another copy with the same
@@ -256,6 +275,20 @@ int trpo_ctx_launch_geometry(const trpo_ctx *ctx, int *blocks, int *threads, int
 const char *trpo_last_error(void);
 /* Drop every cached file-based context (FVPFast/FVP/CG cache). */
 void trpo_cache_clear(void);
+
+/* ------------------------------------------------------------------------- */
+/* Part 3: the reference's text formats, as the Part-1 entry points read them */
+/* ------------------------------------------------------------------------- */
+/* Up to `want` doubles from whitespace-separated text with fscanf("%lf") semantics (stops at the end
+ * or at the first token that is not a number); returns how many were parsed. */
+size_t trpo_text_parse_doubles(const char *txt, double *out, size_t want);
+/* Model file (src/TRPO_FVP.c:670-699): theta[P] (W, B per layer, then the LogStd line, which the
+ * reference reads as Std); entries the file lacks are 0.  0, or -1 if it cannot be opened. */
+int trpo_text_load_model(const char *path, size_t P, double *theta);
+/* Data file (src/TRPO_FVP.c:731-762, src/TRPO_Update.c:228-249): the first n rows of
+ * Mean[A] Std[A] Obs[O] Action[A] Adv; stdv = the LAST row's Std; mean / action / adv may be NULL. */
+int trpo_text_load_data(const char *path, size_t O, size_t A, size_t n, double *obs, double *stdv, double *mean,
+                        double *action, double *adv);
 
 #ifdef __cplusplus
 }

@@ -172,7 +172,25 @@ def test_unchanged_reference_header_caller_links(tmp_path):
 
 def test_library_runs_on_the_system_rocm_runtime():
     """conftest.py loads libtrpo_mi355x.so before anything imports torch, so its HIP calls resolve to
-    the system ROCm's libamdhip64 (the one it is built against), not torch's bundled copy."""
+    the libamdhip64 it is built and rpath-linked against (lib/build_info.json), not torch's bundled copy."""
     import trpo_amd
     rt = trpo_amd.runtime_path()
-    assert os.path.realpath(rt).startswith(os.path.realpath("/opt/rocm")), rt
+    assert trpo_amd.built_runtime_dir() is not None
+    assert trpo_amd.runtime_is_built_one(), (rt, trpo_amd.built_runtime_dir())
+
+
+def test_runtime_dir_compares_whole_components():
+    """/opt/rocm_other is not /opt/rocm (the old check was a string prefix)."""
+    assert trpo_amd._same_dir("/opt/rocm/lib", "/opt/rocm/lib/")
+    assert not trpo_amd._same_dir("/opt/rocm_other/lib", "/opt/rocm/lib")
+    assert not trpo_amd._same_dir("/opt/rocm/lib/x", "/opt/rocm/lib")
+
+
+def test_library_exports_exactly_the_abi():
+    """the dynamic symbol table is the header's functions (C linkage) plus the seven
+    C++-linkage twins of TRPO.h -- no kernel stubs, no trpo_dev_* / trpo_peer_* internals."""
+    out = subprocess.run(["nm", "-D", "--defined-only", trpo_amd.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    got = sorted(line.split()[-1] for line in out.splitlines() if line.strip())
+    want = sorted(set(trpo_amd.header_symbols()) | set(MANGLED.values()))
+    assert got == want, (sorted(set(got) - set(want))[:20], sorted(set(want) - set(got)))

@@ -38,59 +38,194 @@ def test_rank_count_mismatch_exits_nonzero():
 
 
 class _FakeDist:
-    """Two ranks seen from rank 0; `peer_fails` = backends whose attach fails on the OTHER rank."""
+    """Two ranks seen from rank 0.  `other_fails` = {(attempt, stage)}: the OTHER rank reports a failure
+    at that stage of that attempt (the agreement after the stage then fails on every rank)."""
 
-    def __init__(self, peer_fails=()):
-        self.world, self.rank, self.peer_fails, self.current = 2, 0, set(peer_fails), None
+    def __init__(self, other_fails=()):
+        self.world, self.rank, self.other_fails = 2, 0, set(other_fails)
+        self.attempt, self.stage_i = -1, 0
+        self.calls = []
 
     def max(self, x):
-        return max(x, 1.0 if self.current in self.peer_fails else 0.0)
+        import bench_mod
+        st = bench_mod.STAGES[min(self.stage_i, len(bench_mod.STAGES) - 1)]
+        self.stage_i += 1
+        self.calls.append(st)
+        return max(x, 1.0 if (self.attempt, st) in self.other_fails else 0.0)
+
+    def allgather_bytes(self, b):
+        return [b, b]
+
+    def bcast_bytes(self, b):
+        return b if b is not None else b"uid"
 
 
 class _FakeCtx:
-    def __init__(self, comm):
-        self.comm, self.closed = comm, False
+    made = []
+
+    def __init__(self, *a, **k):
+        self.closed, self.aborted, self.backend, self.attach_kw = False, False, None, None
+        _FakeCtx.made.append(self)
+
+    def peer_handle(self):
+        return b"h" * 64
+
+    def attach_peers(self, rank, world, handles):
+        self.backend = "peer"
+
+    def attach_comm(self, rank, world, uid, timeout_ms=0):
+        self.backend, self.attach_kw = "rccl", timeout_ms
+
+    def comm_info(self):
+        return dict(rank=0, world=2, replicas=2, backend=self.backend)
+
+    def comm_verify(self, timeout_ms=0):
+        pass
+
+    def upload_b(self, b):
+        pass
+
+    def enqueue_cg(self, *a):
+        pass
+
+    def wait(self, timeout_ms=0):
+        pass
+
+    def download_x(self):
+        import numpy as np
+        return np.arange(582, dtype=np.float64)
+
+    def comm_abort(self):
+        self.aborted = True
 
     def close(self):
         self.closed = True
 
 
-def _agreed(monkeypatch, local_fails=(), peer_fails=(), comm="rccl"):
+def _agreed(monkeypatch, other_fails=(), comm="rccl", fault=None, local_fails=None):
+    """Run make_ctx_agreed with fake contexts; local_fails = {(attempt, stage)} raised on THIS rank."""
+    import numpy as np
+    import trpo_amd
+    from trpo_amd import synth  # noqa: F401 -- the real seeded synthesis
     b = _bench()
-    dist = _FakeDist(peer_fails)
-    made = []
+    sys.modules["bench_mod"] = b
+    dist = _FakeDist(other_fails)
+    _FakeCtx.made = []
+    local_fails = set(local_fails or ())
 
-    def fake_make_ctx(L, n, d, device, comm="rccl"):
-        dist.current = comm
-        if comm in local_fails:
-            raise RuntimeError("attach_%s failed (-4)" % comm)
-        made.append(_FakeCtx(comm))
-        return made[-1], "theta", "obs"
+    class Ctx(_FakeCtx):
+        def __init__(self, *a, **k):
+            super().__init__(*a, **k)
+            if (dist.attempt, "context") in local_fails:
+                raise trpo_amd.TRPOError("trpo_ctx_create failed")
 
-    monkeypatch.setattr(b, "make_ctx", fake_make_ctx)
-    return b, dist, made, b.make_ctx_agreed(b.ARM, b.N_TOTAL, dist, 0, comm)
+        def attach_comm(self, *a):
+            if (dist.attempt, "attach") in local_fails:
+                raise trpo_amd.TRPOError("attach_comm failed (-4)")
+            super().attach_comm(*a)
+
+        def attach_peers(self, *a):
+            if (dist.attempt, "attach") in local_fails:
+                raise trpo_amd.TRPOError("attach_peers failed (-4)")
+            super().attach_peers(*a)
+
+        def comm_verify(self, timeout_ms=0):
+            if (dist.attempt, "verify") in local_fails:
+                raise trpo_amd.TRPOError("comm_verify failed (-7)")
+            super().comm_verify(timeout_ms)
+
+    monkeypatch.setattr(trpo_amd, "Context", Ctx)
+    monkeypatch.setattr(trpo_amd, "unique_id", lambda: b"u" * 128)
+    orig = b.make_ctx_agreed.__globals__["_fault"]
+
+    def fault_hook(stage, rank, attempt):
+        if stage == "context":               # first check of every attempt: track the attempt number
+            dist.attempt, dist.stage_i = attempt, 0
+        return orig(stage, rank, attempt)
+
+    monkeypatch.setitem(b.make_ctx_agreed.__globals__, "_fault", fault_hook)
+    if fault:
+        monkeypatch.setenv("TRPO_BENCH_FAULT", fault)
+    else:
+        monkeypatch.delenv("TRPO_BENCH_FAULT", raising=False)
+    out = b.make_ctx_agreed([15, 16, 16, 3], 64, dist, 0, comm, np.ones(582))
+    return b, dist, _FakeCtx.made, out
 
 
 def test_headline_collective_agreed_no_fallback(monkeypatch):
-    _, _, made, (ctx, _, _, used, fb) = _agreed(monkeypatch)
-    assert used == "rccl" and fb is None and ctx is made[0] and not ctx.closed
+    _, dist, made, (ctx, _, _, used, rec) = _agreed(monkeypatch)
+    assert used == "rccl" and rec["fallback"] is None and ctx is made[0] and not ctx.closed
+    v = rec["verify"]
+    assert v["eager_allreduce_exact"] and v["x_identical_on_all_ranks"] and len(v["x_sha256_16"]) == 16
+    # one agreement per stage, plus the x-hash comparison
+    assert dist.calls == ["context", "bootstrap", "attach", "verify", "solve", "hash", "hash"]
 
 
-def test_headline_falls_back_when_this_rank_fails(monkeypatch):
+def test_headline_falls_back_when_this_rank_fails_attach(monkeypatch):
     """RCCL refusing to attach (e.g. two ranks on one device) moves every rank to the peer exchange."""
-    _, _, made, (ctx, _, _, used, fb) = _agreed(monkeypatch, local_fails={"rccl"})
-    assert used == "peer" and ctx.comm == "peer"
-    assert fb["requested"] == "rccl" and "attach_rccl failed" in fb["failed"][0]["error"]
+    _, _, made, (ctx, _, _, used, rec) = _agreed(monkeypatch, local_fails={(0, "attach")})
+    assert used == "peer" and ctx.backend == "peer" and made[0].closed and not made[0].aborted
+    fb = rec["fallback"]
+    assert fb["requested"] == "rccl" and fb["failed"][0]["stage"] == "attach"
+    assert "attach_comm failed" in fb["failed"][0]["error"]
 
 
 def test_headline_falls_back_when_another_rank_fails(monkeypatch):
-    """This rank attached but another did not: its context is closed and it moves on with the others."""
-    _, _, made, (ctx, _, _, used, fb) = _agreed(monkeypatch, peer_fails={"rccl"})
+    """This rank attached but another did not: its collective is aborted, its context closed, and it
+    moves on with the others."""
+    _, _, made, (ctx, _, _, used, rec) = _agreed(monkeypatch, other_fails={(0, "attach")})
     assert used == "peer" and made[0].closed and not ctx.closed
-    assert fb["failed"][0]["error"] == "another rank failed to attach"
+    assert made[0].aborted                    # it had attached: abort before close
+    assert rec["fallback"]["failed"][0]["error"] == "another rank failed at stage attach"
 
 
-def test_headline_exits_when_no_collective_attaches(monkeypatch):
+def test_one_sided_failure_at_every_stage_is_agreed(monkeypatch):
+    """a failure on ONE rank at any stage makes every rank leave together."""
+    b = _bench()
+    for st in b.STAGES:
+        _, _, made, (ctx, _, _, used, rec) = _agreed(monkeypatch, other_fails={(0, st)})
+        assert used == "peer", st
+        assert rec["fallback"]["failed"][0]["stage"] == st
+        assert made[0].closed
+
+
+def test_verify_failure_aborts_and_retries(monkeypatch):
+    """A failed self-check (wrong sum or time-out) aborts the collective on every rank; with both
+    backends failing once the third attempt (the requested one again) carries the headline."""
+    _, _, made, (ctx, _, _, used, rec) = _agreed(monkeypatch, local_fails={(0, "verify"), (1, "attach")})
+    assert used == "rccl" and len(made) == 3
+    assert made[0].aborted and made[0].closed and made[1].closed and not ctx.closed
+    assert [f["stage"] for f in rec["fallback"]["failed"]] == ["verify", "attach"]
+    assert rec["verify"]["attempt"] == 2
+
+
+def test_fault_injection_env(monkeypatch):
+    """TRPO_BENCH_FAULT=<stage>:<rank>[:<attempt>] (the knob the 2-rank GPU test uses)."""
+    _, _, made, (ctx, _, _, used, rec) = _agreed(monkeypatch, fault="solve:0")
+    assert used == "peer" and made[0].aborted
+    assert rec["fallback"]["failed"][0]["stage"] == "solve"
+    assert "injected" in rec["fallback"]["failed"][0]["error"]
+    _, _, made, (ctx, _, _, used, rec) = _agreed(monkeypatch, fault="hash-mismatch:0")
+    assert used == "peer" and rec["fallback"]["failed"][0]["stage"] == "hash"
+
+
+def test_library_fault_is_armed_for_one_attempt_only(monkeypatch):
+    """comm-verify:R sets TRPO_COMM_FAULT=verify:R (read by the library's self-check) during attempt 0
+    only, and leaves the environment as it was afterwards."""
+    import os
+    seen = []
+    b = _bench()
+
+    def spy(*a, **k):
+        seen.append(os.environ.get("TRPO_COMM_FAULT"))
+
+    monkeypatch.setattr(_FakeCtx, "comm_verify", lambda self, t=0: spy())
+    _agreed(monkeypatch, fault="comm-verify:0")
+    assert seen == ["verify:0"]
+    assert "TRPO_COMM_FAULT" not in os.environ
+
+
+def test_headline_exits_when_no_collective_passes(monkeypatch):
     import pytest
     with pytest.raises(SystemExit):
-        _agreed(monkeypatch, local_fails={"rccl", "peer"})
+        _agreed(monkeypatch, local_fails={(0, "attach"), (1, "attach"), (2, "attach")})

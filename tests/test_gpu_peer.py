@@ -200,6 +200,18 @@ def test_peer_fvp_and_update_slab_paths(kind):
     assert cases.rel_l2(res[0][1]["x"], ref["x"]) <= 1e-4
 
 
+def test_peer_slab_paths_torch_runtime_first():
+    """the same slab-path exchange in a process that imported torch FIRST (its bundled
+    HIP runtime then serves the library).  The fence-free hand-off gave rank-equal wrong sums there; the
+    hand-off's system-scope release / acquire (csrc/trpo_peer.hip) must make it pass, twice over."""
+    env = dict(os.environ)
+    env.pop("TRPO_PEER_FENCE", None)
+    r = subprocess.run([sys.executable, os.path.join(HERE, "peer_torch_first.py"), "2"], capture_output=True,
+                       text=True, timeout=240, env=env)
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    assert r.stdout.count("ok ") == 4, r.stdout
+
+
 def test_peer_missing_rank_times_out():
     """Only rank 0 of a world of 2 attaches: its exchange (the shard-size all-reduce of the attach)
     waits 3 s for rank 1, then gives up with an error -- the GPU is released, nothing hangs."""

@@ -113,6 +113,7 @@ int trpo_peer_allreduce(trpo_peer *p, hipStream_t st, const double *in, int R, i
                         const int *done);
 int trpo_peer_error(const trpo_peer *p);
 size_t trpo_peer_slot(const trpo_peer *p);
-int trpo_peer_uncached(const trpo_peer *p);
+int trpo_peer_fenced(const trpo_peer *p);
+void trpo_peer_set_error(trpo_peer *p);
 
 #endif

@@ -29,7 +29,12 @@ int trpo_dev_set_obs(trpo_dev *d, const double *obs, size_t n);
 int trpo_dev_set_damping(trpo_dev *d, double damping);
 
 int trpo_dev_comm_unique_id(void *id128);
-int trpo_dev_set_comm(trpo_dev *d, int rank, int world, const void *id128);
+/* RCCL init bounded by timeout_ms (<= 0: $TRPO_COMM_TIMEOUT_MS or 120 s); -6 on time-out */
+int trpo_dev_set_comm(trpo_dev *d, int rank, int world, const void *id128, long timeout_ms);
+/* bounded self-check / wait / abort of the attached collective (trpo_kernels.hip) */
+int trpo_dev_comm_verify(trpo_dev *d, long timeout_ms, long *bad);
+int trpo_dev_wait(trpo_dev *d, long timeout_ms);
+int trpo_dev_comm_abort(trpo_dev *d);
 /* in-process host-staged group of `world` contexts (one thread each): the sharded code path
  * without RCCL, for tests (trpo_kernels.hip) */
 typedef struct trpo_hgroup trpo_hgroup;

@@ -155,9 +155,29 @@ int trpo_comm_unique_id(void *id) {
     return trpo_dev_comm_unique_id(id);
 }
 int trpo_ctx_attach_comm(trpo_ctx *c, int rank, int world, const void *id) {
-    if (!c || (world > 1 && !id)) return TRPO_E_INVALID;
-    return trpo_dev_set_comm(c->dev, rank, world, id);
+    return trpo_ctx_attach_comm_timeout(c, rank, world, id, 0);
 }
+int trpo_ctx_attach_comm_timeout(trpo_ctx *c, int rank, int world, const void *id, long timeout_ms) {
+    if (!c || (world > 1 && !id)) return TRPO_E_INVALID;
+    const int rc = trpo_dev_set_comm(c->dev, rank, world, id, timeout_ms);
+    if (rc == TRPO_E_TIMEOUT) set_err("RCCL init (rank %d of %d) did not complete within its time limit", rank, world);
+    return rc;
+}
+int trpo_ctx_comm_verify(trpo_ctx *c, long timeout_ms) {
+    if (!c) return TRPO_E_INVALID;
+    long bad = 0;
+    const int rc = trpo_dev_comm_verify(c->dev, timeout_ms, &bad);
+    if (rc == TRPO_E_VERIFY) set_err("collective self-check: %ld elements of the test all-reduce differ from the exact sum", bad);
+    else if (rc == TRPO_E_TIMEOUT) set_err("collective self-check: the test all-reduce did not complete in time");
+    return rc;
+}
+int trpo_ctx_wait(trpo_ctx *c, long timeout_ms) {
+    if (!c) return TRPO_E_INVALID;
+    const int rc = trpo_dev_wait(c->dev, timeout_ms);
+    if (rc == TRPO_E_TIMEOUT) set_err("the context's stream did not complete in time");
+    return rc;
+}
+int trpo_ctx_comm_abort(trpo_ctx *c) { return c ? trpo_dev_comm_abort(c->dev) : TRPO_E_INVALID; }
 
 trpo_group *trpo_group_create(int world) { return (trpo_group *)trpo_hgroup_create(world); }
 void trpo_group_destroy(trpo_group *g) { trpo_hgroup_destroy((trpo_hgroup *)g); }

@@ -34,6 +34,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "trpo_common.h"
 #include "trpo_dev.h"
@@ -3529,6 +3530,7 @@ struct trpo_dev {
     double *ptmp;               // [slot] staging of an in-place all-reduce
     double *pn;                 // [PEER_WMAX] the shard sizes exchanged at attach
     int rank, world;
+    int comm_aborted;           // trpo_dev_comm_abort ran: every later result call reports -4
     int no_cg_last;             // TRPO_CG_LAST=0: the last step on cg_update_kernel (A/B)
     char name[64];
 };
@@ -4234,25 +4236,113 @@ extern "C" int trpo_dev_comm_info(const trpo_dev *d, int *rank, int *world, int 
     return 0;
 }
 
-extern "C" int trpo_dev_set_comm(trpo_dev *d, int rank, int world, const void *id128) {
-    if (!d || world < 1 || rank < 0 || rank >= world) return -1;
+// Bounded RCCL initialisation.  ncclCommInitRank blocks until every rank of the unique id has joined;
+// a rank that never arrives (crashed, or failed before the call) would hold the others forever.  The
+// call therefore runs in a helper thread and the caller waits at most timeout_ms: on time-out the
+// attach fails (-6) and the helper is abandoned -- if its init completes later, it aborts the
+// communicator itself.  The communicator stays a BLOCKING one, so the data path (eager and
+// graph-captured ncclAllReduce) is exactly that of an ordinary ncclCommInitRank.
+extern "C" int trpo_dev_comm_error(const trpo_dev *d);
+static int ensure_hst(trpo_dev *d, size_t count, bool host_writes);
+__global__ void vcopy64_kernel(const double *__restrict__ src, double *__restrict__ dst, int n);
+
+struct CommInitJob {
+    pthread_mutex_t mu;
+    int device, world, rank;
+    ncclUniqueId id;
+    ncclComm_t comm;
+    ncclResult_t res;
+    int done, abandoned;
+};
+
+static void *comm_init_thread(void *arg) {
+    CommInitJob *j = (CommInitJob *)arg;
+    ncclComm_t c = NULL;
+    ncclResult_t r = hipSetDevice(j->device) == hipSuccess ? ncclCommInitRank(&c, j->world, j->id, j->rank)
+                                                             : ncclUnhandledCudaError;
+    pthread_mutex_lock(&j->mu);
+    j->comm = c;
+    j->res = r;
+    j->done = 1;
+    const int abandoned = j->abandoned;
+    pthread_mutex_unlock(&j->mu);
+    if (abandoned) {
+        if (r == ncclSuccess && c) ncclCommAbort(c);
+        pthread_mutex_destroy(&j->mu);
+        free(j);
+    }
+    return NULL;
+}
+
+static double mono_ms(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return 1e3 * (double)ts.tv_sec + 1e-6 * (double)ts.tv_nsec;
+}
+
+static long comm_timeout_ms(long given) {
+    if (given > 0) return given;
+    const char *e = getenv("TRPO_COMM_TIMEOUT_MS");
+    return e && atol(e) > 0 ? atol(e) : 120000;
+}
+
+static int comm_init_bounded(trpo_dev *d, int rank, int world, const void *id128, long timeout_ms) {
+    CommInitJob *j = (CommInitJob *)calloc(1, sizeof(CommInitJob));
+    if (!j) return -3;
+    pthread_mutex_init(&j->mu, NULL);
+    j->device = d->device;
+    j->world = world;
+    j->rank = rank;
+    memcpy(&j->id, id128, sizeof(j->id));
+    pthread_t th;
+    if (pthread_create(&th, NULL, comm_init_thread, j) != 0) {
+        pthread_mutex_destroy(&j->mu);
+        free(j);
+        return -3;
+    }
+    pthread_detach(th);
+    const double t_end = mono_ms() + (double)timeout_ms;
+    for (;;) {
+        pthread_mutex_lock(&j->mu);
+        const int done = j->done;
+        if (!done && mono_ms() > t_end) j->abandoned = 1;       // the helper frees the job
+        const int abandoned = j->abandoned;
+        pthread_mutex_unlock(&j->mu);
+        if (done) break;
+        if (abandoned) {
+            fprintf(stderr, "[trpo_mi355x] ncclCommInitRank(rank %d of %d, device %d): no completion within %ld ms\n",
+                    rank, world, d->device, timeout_ms);
+            return -6;
+        }
+        struct timespec ts = {0, 1000000};
+        nanosleep(&ts, NULL);
+    }
+    const ncclResult_t nr = j->res;
+    ncclComm_t c = j->comm;
+    pthread_mutex_destroy(&j->mu);
+    free(j);
+    if (nr != ncclSuccess) {
+        fprintf(stderr, "[trpo_mi355x] ncclCommInitRank(rank %d of %d, device %d): %s\n", rank, world, d->device,
+                ncclGetErrorString(nr));
+        return -4;
+    }
+    d->comm = c;
+    return 0;
+}
+
+extern "C" int trpo_dev_set_comm(trpo_dev *d, int rank, int world, const void *id128, long timeout_ms) {
+    if (!d || world < 1 || rank < 0 || rank >= world || (world > 1 && !id128)) return -1;
     HCHK(hipSetDevice(d->device));
     d->group = NULL;
     d->peer_on = 0;
+    d->comm_aborted = 0;
     if (d->comm) {
         ncclCommDestroy(d->comm);
         d->comm = NULL;
     }
     if (world > 1) {
-        ncclUniqueId id;
-        memcpy(&id, id128, sizeof(id));
-        const ncclResult_t nr = ncclCommInitRank(&d->comm, world, id, rank);
-        if (nr != ncclSuccess) {
-            fprintf(stderr, "[trpo_mi355x] ncclCommInitRank(rank %d of %d, device %d): %s\n", rank, world, d->device,
-                    ncclGetErrorString(nr));
-            d->comm = NULL;
-            return -4;
-        }
+        const int rc = comm_init_bounded(d, rank, world, id128, comm_timeout_ms(timeout_ms));
+        if (rc) return rc;
     }
     d->rank = rank;
     d->world = world;
@@ -4261,6 +4351,101 @@ extern "C" int trpo_dev_set_comm(trpo_dev *d, int rank, int world, const void *i
         d->cg_exec = NULL;
     }
     return refresh_n_total(d);
+}
+
+// Wait for everything enqueued on the context's stream, at most timeout_ms (<= 0: the default of
+// TRPO_COMM_TIMEOUT_MS / 120 s): 0 when it completed (or the collective's error), -6 on time-out.
+// spin: poll without sleeping (a timed region); otherwise 50 us between polls.
+static int wait_stream(trpo_dev *d, long timeout_ms, bool spin) {
+    const double t_end = mono_ms() + (double)comm_timeout_ms(timeout_ms);
+    for (;;) {
+        const hipError_t e = hipStreamQuery(d->stream);
+        if (e == hipSuccess) return 0;
+        if (e != hipErrorNotReady) {
+            fprintf(stderr, "[trpo_mi355x] HIP error %s while waiting for the stream\n", hipGetErrorString(e));
+            return -2;
+        }
+        if (mono_ms() > t_end) return -6;
+        if (!spin) {
+            struct timespec ts = {0, 50000};
+            nanosleep(&ts, NULL);
+        }
+    }
+}
+
+extern "C" int trpo_dev_wait(trpo_dev *d, long timeout_ms) {
+    if (!d) return -1;
+    HCHK(hipSetDevice(d->device));
+    const int rc = wait_stream(d, timeout_ms, true);
+    return rc ? rc : trpo_dev_comm_error(d);
+}
+
+// Give up on the attached collective: RCCL's abort (its kernels, eager or inside a captured graph, see
+// the abort flag and exit), or the peer exchange's error word (later exchanges skip their waits); the
+// CG graph holding the old collective is dropped, the stream drained (bounded), and every later result
+// call of this context reports -4.  The context is then only good for trpo_ctx_destroy.
+extern "C" int trpo_dev_comm_abort(trpo_dev *d) {
+    if (!d) return -1;
+    hipSetDevice(d->device);
+    if (d->comm) {
+        ncclCommAbort(d->comm);
+        d->comm = NULL;
+    }
+    if (d->peer) trpo_peer_set_error(d->peer);
+    d->comm_aborted = 1;
+    const int rc = wait_stream(d, 10000, false);
+    if (d->cg_exec) {
+        hipGraphExecDestroy(d->cg_exec);
+        d->cg_exec = NULL;
+    }
+    return rc;
+}
+
+// Self-check of the attached collective before it carries results: ONE eager all-reduce, through the
+// same allreduce() every FVP uses, of a vector as long as the per-FVP message (Rc x Ps replica values
+// in the atomic mode, the reduced vector otherwise).  Rank r contributes 2^r (1 + i mod 251) at
+// element i, so the sum is (2^world - 1)(1 + i mod 251) exactly, and a lost, doubled or misplaced
+// contribution changes it.  The wait is bounded (timeout_ms); every element is compared bit for bit.
+// Returns 0, -6 (no completion: the caller aborts), -7 (wrong sum; *bad = mismatching elements) or the
+// collective's error.  TRPO_COMM_FAULT=verify:R / hang:R (testing) makes rank R contribute a wrong
+// value / skip the all-reduce.
+static int comm_fault(const trpo_dev *d, const char *kind) {
+    const char *e = getenv("TRPO_COMM_FAULT");
+    const size_t k = strlen(kind);
+    return e && !strncmp(e, kind, k) && e[k] == ':' && atoi(e + k + 1) == d->rank;
+}
+
+extern "C" int trpo_dev_comm_verify(trpo_dev *d, long timeout_ms, long *bad) {
+    if (bad) *bad = 0;
+    if (!d) return -1;
+    if (d->comm_aborted) return -4;
+    if (!has_collective(d)) return 0;
+    HCHK(hipSetDevice(d->device));
+    const size_t count = d->atomic ? (size_t)d->Rc * d->Ps : (size_t)d->nw;
+    // a buffer that exists already (no allocation while another rank's exchange may be waiting):
+    // the atomic sink set (never consumed) or the slab-path reduced vector (rewritten by every FVP)
+    double *buf = d->atomic ? d->pacc + (long)d->R * d->Ps : d->zacc;
+    if (ensure_hst(d, count, true)) return -2;
+    for (size_t i = 0; i < count; ++i) d->hst[i] = ldexp((double)(1 + i % 251), d->rank);
+    if (comm_fault(d, "verify")) d->hst[0] += 1.0;
+    hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv((long)count, 256)), dim3(256), 0, d->stream,
+                       (const double *)d->hst_dev, buf, (int)count);
+    HCHK(hipGetLastError());
+    int rc = comm_fault(d, "hang") ? 0 : allreduce(d, buf, count);
+    if (rc) return rc;
+    hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv((long)count, 256)), dim3(256), 0, d->stream, (const double *)buf,
+                       d->hst_dev, (int)count);
+    HCHK(hipGetLastError());
+    rc = wait_stream(d, timeout_ms, false);
+    d->hst_pending = 0;
+    if (rc) return rc;
+    rc = trpo_dev_comm_error(d);
+    if (rc) return rc;
+    const double f = ldexp(1.0, d->world) - 1.0;
+    long nbad = 0;
+    for (size_t i = 0; i < count; ++i) nbad += d->hst[i] != f * (double)(1 + i % 251);
+    if (bad) *bad = nbad;
+    return nbad ? -7 : 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -4319,8 +4504,9 @@ extern "C" int trpo_dev_set_peers(trpo_dev *d, int rank, int world, const void *
     return rn ? rn : trpo_dev_comm_error(d);
 }
 
-// -4 after a peer exchange whose wait timed out (a rank missing); 0 otherwise
+// -4 after a peer exchange whose wait timed out (a rank missing) or an abort; 0 otherwise
 extern "C" int trpo_dev_comm_error(const trpo_dev *d) {
+    if (d && d->comm_aborted) return -4;
     return d && d->peer_on && trpo_peer_error(d->peer) ? -4 : 0;
 }
 
@@ -4332,7 +4518,8 @@ extern "C" const char *trpo_hip_runtime_path(void) {
 
 extern "C" const char *trpo_dev_comm_backend(const trpo_dev *d) {
     if (!d) return "";
-    if (d->peer_on) return trpo_peer_uncached(d->peer) ? "peer-xgmi (uncached window)" : "peer-xgmi (fine-grained window)";
+    if (d->comm_aborted) return "aborted";
+    if (d->peer_on) return trpo_peer_fenced(d->peer) ? "peer-xgmi (uncached window, fenced hand-off)" : "peer-xgmi (uncached window)";
     if (d->comm) return "rccl";
     if (d->group) return "host-group";
     return "none";

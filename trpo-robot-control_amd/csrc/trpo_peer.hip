@@ -24,6 +24,18 @@
 // which read that set) has completed.
 // A poll that does not see its flag within 3 s sets an error word (pinned host memory) instead of
 // spinning forever; later exchanges then skip the wait (results invalid, but the GPU is released).
+//
+// Memory ordering (round 4).  The window is allocated uncached, and every exchanged byte is stored and
+// loaded at system scope, so on the system ROCm no cache can hold a stale line of it.  That property
+// is the allocator's, not the kernel's: under another HIP runtime (a PyTorch wheel's bundled
+// libamdhip64 loaded first) the in-process slab-path exchange returned rank-equal wrong sums -- the
+// signature of a reader's L2 still holding the lines of exchange e - 2 (the same set, read by the same
+// workgroup index on the same XCD on every rank).  So the hand-off also carries the ordering itself
+// (fence = 1, the default): the signalling lane issues a system-scope release after the barrier that
+// follows every storing wave's vmcnt(0) wait (its own asm vmcnt(0) behind it, the compiler-hazard
+// form of MI355X_MICROARCH.md), and the polling wave issues a system-scope acquire (L1 and L2
+// invalidate) after its poll matched, waits for it, and releases the workgroup's other waves by the
+// barrier.  TRPO_PEER_FENCE=0 restores the fence-free form for A/B.
 #include <hip/hip_runtime.h>
 
 #include <stdlib.h>
@@ -44,8 +56,8 @@ struct trpo_peer {
     unsigned long long *cnt;         // [PEER_WMAX] per-workgroup exchange counters
     int *err_h, *err_d;              // pinned host error word and its device view
     int rank, world;
-    int uncached;                    // always 1: hipDeviceMallocUncached (creation fails without it)
     int connected;                   // windows carry the exchange numbering: one connect per window
+    int fence;                       // release / acquire around the flag hand-off (TRPO_PEER_FENCE, default 1)
 };
 
 static size_t win_doubles(size_t S) { return 2 * (size_t)PEER_WMAX * S + (size_t)PEER_WMAX * FLAG_STRIDE; }
@@ -64,7 +76,8 @@ __device__ __forceinline__ double ld_sys(const double *p) {
 
 __global__ void __launch_bounds__(PEER_T)
 peer_exchange_kernel(const double *__restrict__ in, int R, int Rstride, int count, double *const *wins, int rank,
-                     int world, int S, double *__restrict__ out, unsigned long long *cnt, int *err, const int *done) {
+                     int world, int S, double *__restrict__ out, unsigned long long *cnt, int *err, const int *done,
+                     int fence) {
     if (done && *done) return;                     // converged CG: every rank skips the same exchanges
     const int t = blockIdx.x, tid = threadIdx.x;
     const unsigned long long e = cnt[t] + 1;
@@ -76,18 +89,20 @@ peer_exchange_kernel(const double *__restrict__ in, int R, int Rstride, int coun
         for (int k = 1; k < R; ++k) v += in[(long)k * Rstride + i];
         st_sys(dst + i, v);
     }
-    // 3: every storing wave drained, a workgroup barrier, then the flag.  No release fence: every
-    // exchanged byte is stored and loaded at system scope (sc0 sc1) in uncached memory, so no cache
-    // holds a line to write back or invalidate -- the drained stores are in HBM before the flag
-    // store is issued (MI355X_MICROARCH.md, inter-workgroup hand-off: sc1 stores drained by every
-    // storing wave, one lane signalling behind a barrier, sc1 loads after the poll and a barrier)
+    // 3: every storing wave drained, a workgroup barrier, then (fence) one system-scope release and its
+    // own drain, then the flag
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
+        if (fence) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         gu64 *flag = (gu64 *)(size_t)(wins[t] + 2 * (size_t)PEER_WMAX * S);
         __hip_atomic_store(flag + (size_t)rank * FLAG_STRIDE, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    // 4: every rank's flag in the own window
+    // 4: every rank's flag in the own window (relaxed polls), then (fence) one system-scope acquire by the
+    // polling wave, drained before the barrier releases the other waves
     const double *own = wins[rank];
     if (tid < world) {
         gu64 *f = (gu64 *)(size_t)(own + 2 * (size_t)PEER_WMAX * S) + (size_t)tid * FLAG_STRIDE;
@@ -102,9 +117,12 @@ peer_exchange_kernel(const double *__restrict__ in, int R, int Rstride, int coun
             }
         }
     }
+    if (fence && tid < 64) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __syncthreads();
-    // 5: slice t of the elements (system-scope loads of uncached memory: no acquire fence needed),
-    // summed over the slots in rank order
+    // 5: slice t of the elements (system-scope loads), summed over the slots in rank order
     const int per = (count + world - 1) / world, lo = t * per, hi = min(count, lo + per);
     const double *src = own + (size_t)set * PEER_WMAX * S;
     for (int i = lo + tid; i < hi; i += PEER_T) {
@@ -138,9 +156,10 @@ trpo_peer *trpo_peer_create(int device, size_t S) {
         return NULL;
     }
     const size_t bytes = sizeof(double) * win_doubles(p->S);
-    // uncached or nothing: the fence-free hand-off below is only argued for an uncached window (a
-    // fine-grained fallback would need release / acquire fences around the flag), so no fallback
-    p->uncached = 1;
+    // uncached: remote writes land in HBM and no L2 line of the window is kept (the hand-off's own
+    // release / acquire make it correct on any window; see the header comment)
+    const char *ef = getenv("TRPO_PEER_FENCE");
+    p->fence = !(ef && atoi(ef) == 0);
     if (hipExtMallocWithFlags((void **)&p->win, bytes, hipDeviceMallocUncached) != hipSuccess) {
         (void)hipGetLastError();
         p->win = NULL;
@@ -229,11 +248,15 @@ int trpo_peer_allreduce(trpo_peer *p, hipStream_t st, const double *in, int R, i
     if (!p || count < 0 || (size_t)count > p->S || R < 1 || in == out) return -1;
     if (count == 0) return 0;
     hipLaunchKernelGGL(peer_exchange_kernel, dim3(p->world), dim3(PEER_T), 0, st, in, R, Rstride, count, p->dwins,
-                       p->rank, p->world, (int)p->S, out, p->cnt, p->err_d, done);
+                       p->rank, p->world, (int)p->S, out, p->cnt, p->err_d, done, p->fence);
     HCHK(hipGetLastError());
     return 0;
 }
 
 int trpo_peer_error(const trpo_peer *p) { return p && p->err_h ? __atomic_load_n(p->err_h, __ATOMIC_ACQUIRE) : 0; }
 size_t trpo_peer_slot(const trpo_peer *p) { return p ? p->S : 0; }
-int trpo_peer_uncached(const trpo_peer *p) { return p ? p->uncached : 0; }
+int trpo_peer_fenced(const trpo_peer *p) { return p ? p->fence : 0; }
+// abandon the exchange (trpo_dev_comm_abort): later exchanges skip their waits and report the error
+void trpo_peer_set_error(trpo_peer *p) {
+    if (p && p->err_h) __atomic_store_n(p->err_h, 1, __ATOMIC_RELEASE);
+}

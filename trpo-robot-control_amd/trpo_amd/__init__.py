@@ -91,6 +91,14 @@ def lib():
     L.trpo_comm_unique_id.argtypes = [C.c_char_p]
     L.trpo_ctx_attach_comm.restype = C.c_int
     L.trpo_ctx_attach_comm.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_char_p]
+    L.trpo_ctx_attach_comm_timeout.restype = C.c_int
+    L.trpo_ctx_attach_comm_timeout.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_char_p, C.c_long]
+    L.trpo_ctx_comm_verify.restype = C.c_int
+    L.trpo_ctx_comm_verify.argtypes = [C.c_void_p, C.c_long]
+    L.trpo_ctx_wait.restype = C.c_int
+    L.trpo_ctx_wait.argtypes = [C.c_void_p, C.c_long]
+    L.trpo_ctx_comm_abort.restype = C.c_int
+    L.trpo_ctx_comm_abort.argtypes = [C.c_void_p]
     L.trpo_group_create.restype = C.c_void_p
     L.trpo_group_create.argtypes = [C.c_int]
     L.trpo_group_destroy.restype = None
@@ -151,16 +159,37 @@ def lib():
     L.trpo_cache_clear.argtypes = []
     _lib = L
     rt = runtime_path()
-    if rt and not os.path.realpath(rt).startswith(("/opt/rocm", os.path.realpath("/opt/rocm"))):
+    expect = built_runtime_dir()
+    if rt and expect and not _same_dir(os.path.dirname(os.path.realpath(rt)), expect):
         # torch (or another HIP user) was imported first and its bundled runtime now serves this
-        # library too: in-process multi-context peer exchanges on the slab paths gave intermittently
-        # wrong sums there (tests/test_gpu_peer.py), never on the system runtime.  Load this
-        # library before importing torch (tests/conftest.py and bench.py do).
+        # library too.  Load this library before importing torch (tests/conftest.py and bench.py do).
         import warnings
-        warnings.warn("libtrpo_mi355x.so runs on the HIP runtime %s, not the system ROCm it was built "
-                      "against; import trpo_amd and call trpo_amd.lib() before importing torch" % rt,
+        warnings.warn("libtrpo_mi355x.so runs on the HIP runtime %s, not the one it was built and linked "
+                      "against (%s); import trpo_amd and call trpo_amd.lib() before importing torch" % (rt, expect),
                       RuntimeWarning, stacklevel=2)
     return L
+
+
+def built_runtime_dir():
+    """Directory of the libamdhip64 the library was linked and rpath'ed against (lib/build_info.json,
+    written by the Makefile from its ROCM), resolved; None if unknown."""
+    import json
+    try:
+        with open(os.path.join(os.path.dirname(LIB_PATH), "build_info.json")) as f:
+            return os.path.realpath(json.load(f)["hip_runtime_dir"])
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def _same_dir(a: str, b: str) -> bool:
+    """Whole-path-component comparison of two resolved directories."""
+    return os.path.normpath(os.path.realpath(a)).split(os.sep) == os.path.normpath(os.path.realpath(b)).split(os.sep)
+
+
+def runtime_is_built_one() -> bool:
+    """True when this process's HIP calls resolve to the runtime the library was built against."""
+    expect = built_runtime_dir()
+    return expect is None or _same_dir(os.path.dirname(os.path.realpath(runtime_path())), expect)
 
 
 def runtime_path() -> str:
@@ -400,8 +429,30 @@ class Context:
     def set_damping(self, d):
         self._chk(lib().trpo_ctx_set_damping(self._h, d), "set_damping")
 
-    def attach_comm(self, rank: int, world: int, unique_id: bytes):
-        self._chk(lib().trpo_ctx_attach_comm(self._h, rank, world, unique_id), "attach_comm")
+    def attach_comm(self, rank: int, world: int, unique_id: bytes, timeout_ms: int = 0):
+        """RCCL communicator; its init is bounded by timeout_ms (0: $TRPO_COMM_TIMEOUT_MS or 120 s)."""
+        self._chk(lib().trpo_ctx_attach_comm_timeout(self._h, rank, world, unique_id, int(timeout_ms)), "attach_comm")
+
+    def comm_verify(self, timeout_ms: int = 0):
+        """Bounded self-check of the attached collective (all ranks together): raises TRPOError with
+        .code -6 (no completion) / -7 (wrong sum) / -4 (collective error)."""
+        rc = lib().trpo_ctx_comm_verify(self._h, int(timeout_ms))
+        if rc < 0:
+            err = TRPOError("comm_verify failed (%d): %s" % (rc, last_error()))
+            err.code = rc
+            raise err
+
+    def wait(self, timeout_ms: int = 0):
+        """Wait for the enqueued work at most timeout_ms (TRPOError with .code -6 on time-out)."""
+        rc = lib().trpo_ctx_wait(self._h, int(timeout_ms))
+        if rc < 0:
+            err = TRPOError("wait failed (%d): %s" % (rc, last_error()))
+            err.code = rc
+            raise err
+
+    def comm_abort(self):
+        """Abandon the collective (RCCL abort / peer error flag); the context is then only good for close()."""
+        return lib().trpo_ctx_comm_abort(self._h)
 
     def attach_group(self, group: "Group", rank: int):
         """Join an in-process host group as `rank` (call concurrently from one thread per rank)."""
