@@ -211,6 +211,13 @@ double trpo_ctx_cg(trpo_ctx *ctx, const double *b, size_t max_iter, double resid
                    int verbose);
 /* Per-iteration values CG prints: rdotr[i], |x|[i] for i = 0..iters. */
 int trpo_ctx_cg_history(const trpo_ctx *ctx, double *rdotr, double *xnorm, size_t cap, size_t *iters);
+/* The fp32 stall guard of the last trpo_ctx_cg / trpo_ctx_update (and the file entry points), DESIGN §3:
+ * ritz_residual = the smallest relative Ritz residual of the solve's Lanczos matrix (from its CG
+ * coefficients); below $TRPO_RITZ_RERUN (default 1e-15) the reference's fp64 CG loses orthogonality and
+ * its step is its rounding's, so the solve was repeated in fp64 (*fp64_rerun = 1; one-rank contexts; a
+ * "[WARN]" line on stderr).  orth_loss = the largest fraction of a new residual the fp32 path's
+ * reorthogonalisation removed.  Any pointer may be NULL.  No reference counterpart. */
+int trpo_ctx_cg_status(const trpo_ctx *ctx, double *ritz_residual, double *orth_loss, int *fp64_rerun);
 
 /* Device-resident benchmarking hooks: b stays in HBM, no host round trip. */
 int trpo_ctx_upload_b(trpo_ctx *ctx, const double *b);

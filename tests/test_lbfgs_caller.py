@@ -102,3 +102,31 @@ def test_reference_lbfgs_drives_device_evaluate():
     # the caller reads the fitted network back from W/B (src/TRPO_Lightweight.c:679-693): evaluate
     # left the last evaluated x there, as the reference's does
     assert np.all(np.isfinite(param_dev.W[0]))
+    _time_fits(ref, param_dev, param, x0)
+
+
+def _time_fits(ref, param_dev, param_ref, x0, reps=5):
+    """C5's baseline fit timed with the caller's own optimiser (liblbfgs as the trainer
+    calls it) on the device evaluate, beside the same optimiser on the reference's CPU evaluate (one
+    host core).  bench.py may not run anything under oracle/ outside its CPU-baseline leg, so this GPU
+    test is where the fit is timed; with TRPO_TIMING_OUT set, the medians go to that JSON file
+    (profiles/r04_lbfgs_fit_timing.json)."""
+    import json
+    import time
+    t_dev, t_ref = [], []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        rc, _, _ = _fit(ref, C.cast(trpo_amd.lib().evaluate, C.c_void_p), param_dev, x0)
+        t_dev.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        _fit(ref, C.cast(ref.evaluate, C.c_void_p), param_ref, x0)
+        t_ref.append(time.perf_counter() - t0)
+    out = {"what": "liblbfgs 1.10 lbfgs() (src/lbfgs.c, default parameters, max_iterations 25, the trainer's "
+                   "call, src/TRPO_Lightweight.c:676) fitting the [16,16,16,1] baseline on 20 x 150 samples",
+           "device_evaluate_fit_ms": 1e3 * float(np.median(t_dev)),
+           "reference_cpu_evaluate_fit_ms_1core": 1e3 * float(np.median(t_ref)), "lbfgs_rc": int(rc), "reps": reps}
+    print("[timing]", json.dumps(out))
+    path = os.environ.get("TRPO_TIMING_OUT")
+    if path:
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)

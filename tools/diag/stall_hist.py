@@ -21,11 +21,15 @@ from test_gpu_random_shapes import _draw  # noqa: E402
 def one(name, layers, acts, th, obs, std, b, maxiter, resth, damping=0.1):
     ref = oracle.cg(layers, acts, th, obs, std, b, maxiter, resth, damping, verbose=False)
     with trpo_amd.Context(layers, acts, th, obs, std, damping) as c:
+        os.environ["TRPO_RITZ_RERUN"] = "0"            # the fp32 solve as it is (no fp64 re-solve)
         x = c.cg(b, maxiter, resth)
+        st = c.cg_status()
+        os.environ.pop("TRPO_RITZ_RERUN")
         rr, xn, it = c.cg_history()
     e = np.linalg.norm(x - ref["x"]) / np.linalg.norm(ref["x"])
     h = ref.get("rdotr")
-    print("%s  err %.2e  iters dev %d ref %s" % (name, e, it, ref.get("iters")))
+    print("%s  err %.2e  iters dev %d ref %s  orth_loss %.3e  ritz %.3e" % (name, e, it, ref.get("iters"),
+                                                                         st["orth_loss"], st["ritz_residual"]))
     print("   dev rdotr  " + " ".join("%.2e" % v for v in rr))
     if h is not None:
         print("   ref rdotr  " + " ".join("%.2e" % v for v in h))

@@ -83,6 +83,7 @@ struct trpo_dev_view {
     double *vec_x, *vec_v, *vec_z;
     const int *cg_iter;        // device: iterations of the last CG solve
     const double *cg_hist;     // device: its (rdotr, |x|) history, 2 per iteration
+    const double *cg_stats;    // device: its statistics (Ctl::orth, Ctl::alpha[]), TRPO_CG_STATS doubles
 };
 void trpo_dev_get_view(trpo_dev *d, trpo_dev_view *v);
 // in-place fp64 sum over the attached RCCL communicator (no-op without one)

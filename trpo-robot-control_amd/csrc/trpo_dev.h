@@ -21,6 +21,15 @@ enum { TRPO_VEC_V = 0, TRPO_VEC_Z = 1, TRPO_VEC_X = 2, TRPO_VEC_B = 3, TRPO_VEC_
 
 /* device < 0: $TRPO_DEVICE or 0.  Returns NULL and fills err on failure. */
 trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, const char *ac, char *err, size_t errlen);
+/* the same with the precision forced (f64 != 0: the fp64 mode) instead of read from $TRPO_PRECISION */
+trpo_dev *trpo_dev_create_prec(int device, size_t nl, const size_t *ls, const char *ac, int f64, char *err,
+                               size_t errlen);
+int trpo_dev_device(const trpo_dev *d);
+int trpo_dev_is_f64(const trpo_dev *d);
+/* copies of the problem a context holds (fp64): obs [n][L0], std [A], rollout (trpo_update.hip) */
+int trpo_dev_get_obs(trpo_dev *d, double *host);
+int trpo_dev_get_std(trpo_dev *d, double *host);
+int trpo_dev_get_rollout(trpo_dev *d, double *mean, double *action, double *adv);
 void trpo_dev_destroy(trpo_dev *d);
 
 int trpo_dev_set_theta(trpo_dev *d, const double *theta);
@@ -53,6 +62,11 @@ const char *trpo_dev_comm_backend(const trpo_dev *d);
 
 int trpo_dev_upload(trpo_dev *d, int slot, const double *host);
 int trpo_dev_download(trpo_dev *d, int slot, double *host);
+/* x and the last CG solve's statistics, one synchronisation: stats[0] = the largest fraction of a new
+ * residual the reorthogonalisation removed (0 without it), stats[1 + k] = alpha_k, k < 64; rdotr[0..iters]
+ * the residual history (cap entries at most) */
+#define TRPO_CG_STATS 65
+int trpo_dev_download_x_cg(trpo_dev *d, double *host, double *stats, double *rdotr, size_t cap, size_t *iters);
 
 int trpo_dev_fvp(trpo_dev *d);                 /* enqueue z = F v  (slots V -> Z) */
 int trpo_dev_fvp_src(trpo_dev *d, const double *src);   /* enqueue z = F src (any device vector) -> Z */
@@ -77,7 +91,7 @@ int trpo_dev_surrogate(trpo_dev *d, const double *fullstep, int k0, int nk, doub
  * pinned host memory. */
 int trpo_dev_update_solve(trpo_dev *d, size_t maxiter, double resth, double *b, double *x, double *z,
                           double *adv_sum, size_t *iters, double *rdotr_hist, double *xnorm_hist,
-                          double max_kl, double *surr0, double *shs_lm);
+                          double max_kl, double *surr0, double *shs_lm, double *stats);
 /* shs_lm (optional, 2): the step size shs = 0.5 x.Fx and lm = sqrt(shs / max_kl) as the device computed
  * them (fullstep = x / lm, fixed-order sum); surr0 (optional): the surrogate sum of the full step
  * theta + fullstep, the line search's first candidate, in the same synchronisation. */

@@ -65,7 +65,157 @@ struct trpo_ctx {
     double damping;
     double *theta;             /* host copy of the current parameters (line search base) */
     int have_roll;             /* rollout uploaded for the current samples */
+    trpo_dev *twin;            /* fp64 twin of the problem (the fp32 stall guard's re-solve), lazily built */
+    double last_orth;          /* the last CG solve's orthogonality-loss statistic (ctl->orth) */
+    double last_ritz;          /* its smallest relative Ritz residual (the stall guard's test) */
+    int last_rerun;            /* 1 when the last solve's result came from the fp64 twin */
 };
+
+/* fp32 stall guard.  The fp32 path reorthogonalises every new CG residual
+ * and so converges like exact-arithmetic CG.  The reference's plain fp64 recurrence
+ * (src/TRPO_CG.c:65-103) does not where its residuals lose orthogonality -- which, by Paige's theory of
+ * the Lanczos process, happens once a Ritz value of the solve has converged to near machine precision:
+ * |q . r_k| ~ eps ||A|| / (Ritz residual).  The solve's own CG coefficients give that test: alpha_k and
+ * beta_k = rdotr_{k+1} / rdotr_k form the Lanczos matrix T_k, and a Ritz pair (theta, s) of T_k has the
+ * residual sqrt(beta_k) / alpha_k |s_k|.  When the smallest one, relative to the largest Ritz value,
+ * falls below TRPO_RITZ_RERUN (default 1e-15, about 10 eps64) the reference's own step is its rounding's,
+ * not the exact one (random-shape draw 23: 7e-17, the fp32 step 1.2e-3 from the reference; the next
+ * smallest case 1.6e-15, 7e-6; tools/diag/ritz_probe.py), and the solve is repeated in fp64 on a twin of
+ * the context (the reference's arithmetic, no reorthogonalisation), built on first use from the
+ * context's own device-resident problem.  One rank only: a sharded context reports the statistic
+ * (trpo_ctx_cg_status) and warns.  The coefficients of the fp32 trajectory carry ~1e-7 relative noise;
+ * the Ritz residual is insensitive to it (the probe perturbs them: unchanged to 2 digits). */
+static double ritz_threshold(void) {
+    const char *e = getenv("TRPO_RITZ_RERUN");
+    return e ? atof(e) : 1e-15;
+}
+
+/* eigen-decomposition of the symmetric k x k matrix a (row-major, destroyed) by cyclic Jacobi; w the
+ * eigenvalues, v the eigenvectors as columns (k <= 64) */
+static void jacobi_eig(double *a, int k, double *w, double *v) {
+    for (int i = 0; i < k; ++i)
+        for (int j = 0; j < k; ++j) v[i * k + j] = i == j ? 1.0 : 0.0;
+    for (int sweep = 0; sweep < 100; ++sweep) {
+        double off = 0.0, tot = 0.0;
+        for (int i = 0; i < k; ++i)
+            for (int j = 0; j < k; ++j) {
+                tot += a[i * k + j] * a[i * k + j];
+                if (i != j) off += a[i * k + j] * a[i * k + j];
+            }
+        if (off <= 1e-36 * tot) break;
+        for (int p = 0; p < k; ++p)
+            for (int q = p + 1; q < k; ++q) {
+                const double apq = a[p * k + q];
+                if (apq == 0.0) continue;
+                const double th = (a[q * k + q] - a[p * k + p]) / (2.0 * apq);
+                const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1.0));
+                const double cs = 1.0 / sqrt(t * t + 1.0), sn = t * cs;
+                for (int r = 0; r < k; ++r) {                 /* a <- a J (columns p, q) */
+                    const double x = a[r * k + p], y = a[r * k + q];
+                    a[r * k + p] = cs * x - sn * y;
+                    a[r * k + q] = sn * x + cs * y;
+                }
+                for (int r = 0; r < k; ++r) {                 /* a <- J^T a (rows p, q) */
+                    const double x = a[p * k + r], y = a[q * k + r];
+                    a[p * k + r] = cs * x - sn * y;
+                    a[q * k + r] = sn * x + cs * y;
+                }
+                for (int r = 0; r < k; ++r) {                 /* v <- v J */
+                    const double x = v[r * k + p], y = v[r * k + q];
+                    v[r * k + p] = cs * x - sn * y;
+                    v[r * k + q] = sn * x + cs * y;
+                }
+            }
+    }
+    for (int i = 0; i < k; ++i) w[i] = a[i * k + i];
+}
+
+/* smallest relative Ritz residual over the Lanczos matrices T_1 .. T_iters of a CG solve (alpha_k,
+ * rdotr_k as the device recorded them; iters <= 64); 1 when there is nothing to test */
+static double ritz_min(const double *alpha, const double *rdotr, size_t iters) {
+    const int K = iters > 64 ? 64 : (int)iters;
+    double best = 1.0;
+    double *a = (double *)malloc(sizeof(double) * 3 * 64 * 64 + sizeof(double) * 64);
+    if (!a) return best;
+    double *v = a + 64 * 64, *w = v + 64 * 64;
+    for (int k = 1; k <= K; ++k) {
+        int ok = 1;
+        for (int j = 0; j < k; ++j) ok &= alpha[j] > 0.0 && rdotr[j] > 0.0 && isfinite(alpha[j]);
+        if (!ok || !(rdotr[k] >= 0.0)) break;
+        for (int i = 0; i < k * k; ++i) a[i] = 0.0;
+        for (int j = 0; j < k; ++j) {
+            const double bj = rdotr[j + 1] / rdotr[j];
+            a[j * k + j] = 1.0 / alpha[j] + (j > 0 ? (rdotr[j] / rdotr[j - 1]) / alpha[j - 1] : 0.0);
+            if (j + 1 < k) a[j * k + j + 1] = a[(j + 1) * k + j] = sqrt(bj) / alpha[j];
+        }
+        jacobi_eig(a, k, w, v);
+        double wmax = 0.0;
+        for (int i = 0; i < k; ++i) wmax = fabs(w[i]) > wmax ? fabs(w[i]) : wmax;
+        const double bk = sqrt(rdotr[k] / rdotr[k - 1]) / alpha[k - 1];
+        for (int i = 0; i < k && wmax > 0.0; ++i) {
+            const double res = bk * fabs(v[(k - 1) * k + i]) / wmax;
+            best = res < best ? res : best;
+        }
+    }
+    free(a);
+    return best;
+}
+
+static void drop_twin(trpo_ctx *c) {
+    if (c && c->twin) {
+        trpo_dev_destroy(c->twin);
+        c->twin = NULL;
+    }
+}
+
+/* stats = [orth, alpha_0 .. alpha_63] and the rdotr history of the solve just run */
+static int needs_rerun(trpo_ctx *c, const double *stats, const double *rdotr, size_t iters) {
+    c->last_orth = stats[0];
+    c->last_ritz = ritz_min(stats + 1, rdotr, iters);
+    const double th = ritz_threshold();
+    if (!(th > 0.0) || !(c->last_ritz < th) || trpo_dev_is_f64(c->dev)) return 0;
+    int world = 1;
+    trpo_dev_comm_info(c->dev, NULL, &world, NULL);
+    if (world > 1) {
+        fprintf(stderr, "[WARN] CG: a Ritz value converged to %.1e (relative residual): the reference's fp64 CG "
+                        "loses orthogonality here; sharded context, not re-solved in fp64\n", c->last_ritz);
+        return 0;
+    }
+    return 1;
+}
+
+static trpo_dev *get_twin(trpo_ctx *c) {
+    if (c->twin) return c->twin;
+    char err[256] = {0};
+    trpo_dev *t = trpo_dev_create_prec(trpo_dev_device(c->dev), c->nl, c->ls, c->ac, 1, err, sizeof err);
+    if (!t) {
+        set_err("fp64 twin: %s", err);
+        return NULL;
+    }
+    const size_t L0 = c->ls[0], A = c->ls[c->nl - 1], n = c->n;
+    double *obs = (double *)malloc(sizeof(double) * (n * L0 + 1)), *stdv = (double *)malloc(sizeof(double) * A);
+    double *roll = c->have_roll ? (double *)malloc(sizeof(double) * (n * (2 * A + 1) + 1)) : NULL;
+    int rc = (!obs || !stdv || (c->have_roll && !roll)) ? TRPO_E_NOMEM : trpo_dev_get_obs(c->dev, obs);
+    if (!rc) rc = trpo_dev_get_std(c->dev, stdv);
+    if (!rc) rc = trpo_dev_set_theta(t, c->theta);
+    if (!rc) rc = trpo_dev_set_std(t, stdv);
+    if (!rc) rc = trpo_dev_set_obs(t, obs, n);
+    if (!rc) rc = trpo_dev_set_damping(t, c->damping);
+    if (!rc && c->have_roll) {
+        rc = trpo_dev_get_rollout(c->dev, roll, roll + n * A, roll + 2 * n * A);
+        if (!rc) rc = trpo_dev_set_rollout(t, roll, roll + n * A, roll + 2 * n * A, n);
+    }
+    free(obs);
+    free(stdv);
+    free(roll);
+    if (rc) {
+        set_err("fp64 twin: rebuilding the problem failed (code %d)", rc);
+        trpo_dev_destroy(t);
+        return NULL;
+    }
+    c->twin = t;
+    return t;
+}
 
 static int check_shape(size_t nl, const size_t *ls, const char *ac) {
     if (nl < 2 || nl > MAX_LAYERS || !ls || !ac) {
@@ -121,6 +271,7 @@ trpo_ctx *trpo_ctx_create(size_t num_layers, const size_t *layer_size, const cha
 
 void trpo_ctx_destroy(trpo_ctx *c) {
     if (!c) return;
+    drop_twin(c);
     trpo_dev_destroy(c->dev);
     free(c->theta);
     free(c);
@@ -128,12 +279,14 @@ void trpo_ctx_destroy(trpo_ctx *c) {
 
 int trpo_ctx_set_theta(trpo_ctx *c, const double *theta) {
     if (!c || !theta) return TRPO_E_INVALID;
+    drop_twin(c);
     int rc = trpo_dev_set_theta(c->dev, theta);
     if (!rc) memcpy(c->theta, theta, c->P * sizeof(double));
     return rc;
 }
 int trpo_ctx_set_obs(trpo_ctx *c, const double *obs, size_t n) {
     if (!c || (!obs && n)) return TRPO_E_INVALID;
+    drop_twin(c);
     int rc = trpo_dev_set_obs(c->dev, obs, n);
     if (!rc) c->n = n;
     c->have_roll = 0;                  /* a rollout belongs to one set of samples */
@@ -141,11 +294,13 @@ int trpo_ctx_set_obs(trpo_ctx *c, const double *obs, size_t n) {
 }
 int trpo_ctx_set_std(trpo_ctx *c, const double *stdv) {
     if (!c || !stdv) return TRPO_E_INVALID;
+    drop_twin(c);
     return trpo_dev_set_std(c->dev, stdv);
 }
 int trpo_ctx_set_damping(trpo_ctx *c, double d) {
     if (!c) return TRPO_E_INVALID;
     c->damping = d;
+    if (c->twin) trpo_dev_set_damping(c->twin, d);
     return trpo_dev_set_damping(c->dev, d);
 }
 size_t trpo_ctx_num_params(const trpo_ctx *c) { return c ? c->P : 0; }
@@ -159,6 +314,7 @@ int trpo_ctx_attach_comm(trpo_ctx *c, int rank, int world, const void *id) {
 }
 int trpo_ctx_attach_comm_timeout(trpo_ctx *c, int rank, int world, const void *id, long timeout_ms) {
     if (!c || (world > 1 && !id)) return TRPO_E_INVALID;
+    drop_twin(c);
     const int rc = trpo_dev_set_comm(c->dev, rank, world, id, timeout_ms);
     if (rc == TRPO_E_TIMEOUT) set_err("RCCL init (rank %d of %d) did not complete within its time limit", rank, world);
     return rc;
@@ -246,9 +402,30 @@ double trpo_ctx_fvp(trpo_ctx *c, const double *v, double *out) {
 double trpo_ctx_cg(trpo_ctx *c, const double *b, size_t max_iter, double th, double *x, int verbose) {
     if (!c || !b || !x) return TRPO_E_INVALID;
     const double t0 = now_s();
+    double stats[TRPO_CG_STATS], rdh[66];
+    size_t its = 0;
+    trpo_dev *hd = c->dev;                             /* the context whose solve x comes from */
+    c->last_rerun = 0;
     int rc = trpo_dev_upload(c->dev, TRPO_VEC_B, b);
     if (!rc) rc = trpo_dev_cg(c->dev, max_iter, th);
-    if (!rc) rc = trpo_dev_download(c->dev, TRPO_VEC_X, x);
+    if (!rc) rc = trpo_dev_download_x_cg(c->dev, x, stats, rdh, 66, &its);
+    if (!rc && needs_rerun(c, stats, rdh, its)) {
+        trpo_dev *t = get_twin(c);
+        if (t) {
+            rc = trpo_dev_upload(t, TRPO_VEC_B, b);
+            if (!rc) rc = trpo_dev_cg(t, max_iter, th);
+            if (!rc) rc = trpo_dev_download(t, TRPO_VEC_X, x);
+            if (!rc) {
+                c->last_rerun = 1;
+                hd = t;
+                fprintf(stderr, "[WARN] CG: a Ritz value converged to %.1e (relative residual), where the "
+                                "reference's fp64 CG loses orthogonality; solved again in fp64\n", c->last_ritz);
+            }
+        } else {
+            fprintf(stderr, "[WARN] CG: a Ritz value converged to %.1e and the fp64 re-solve is unavailable: %s\n",
+                    c->last_ritz, g_err);
+        }
+    }
     const double t1 = now_s();
     if (rc) {
         set_err("CG failed on the device (code %d)", rc);
@@ -259,7 +436,7 @@ double trpo_ctx_cg(trpo_ctx *c, const double *b, size_t max_iter, double th, dou
         size_t iters = 0;
         double *rr = (double *)malloc(sizeof(double) * (max_iter + 1));
         double *xn = (double *)malloc(sizeof(double) * (max_iter + 1));
-        if (rr && xn && !trpo_dev_cg_history(c->dev, rr, xn, max_iter + 1, &iters)) {
+        if (rr && xn && !trpo_dev_cg_history(hd, rr, xn, max_iter + 1, &iters)) {
             for (size_t i = 0; i <= iters; ++i)
                 printf("CG Iter[%zu] Residual Norm=%.12e, Soln Norm=%.12e\n", i, rr[i], xn[i]);
         }
@@ -271,7 +448,15 @@ double trpo_ctx_cg(trpo_ctx *c, const double *b, size_t max_iter, double th, dou
 
 int trpo_ctx_cg_history(const trpo_ctx *c, double *rdotr, double *xnorm, size_t cap, size_t *iters) {
     if (!c) return TRPO_E_INVALID;
-    return trpo_dev_cg_history(c->dev, rdotr, xnorm, cap, iters);
+    return trpo_dev_cg_history(c->last_rerun && c->twin ? c->twin : c->dev, rdotr, xnorm, cap, iters);
+}
+
+int trpo_ctx_cg_status(const trpo_ctx *c, double *ritz_residual, double *orth_loss, int *fp64_rerun) {
+    if (!c) return TRPO_E_INVALID;
+    if (ritz_residual) *ritz_residual = c->last_ritz;
+    if (orth_loss) *orth_loss = c->last_orth;
+    if (fp64_rerun) *fp64_rerun = c->last_rerun;
+    return 0;
 }
 
 /* ------------------------------------------------------------------------- */
@@ -279,6 +464,7 @@ int trpo_ctx_cg_history(const trpo_ctx *c, double *rdotr, double *xnorm, size_t 
 /* ------------------------------------------------------------------------- */
 int trpo_ctx_set_rollout(trpo_ctx *c, const double *mean, const double *action, const double *adv) {
     if (!c || (c->n && (!mean || !action || !adv))) return TRPO_E_INVALID;
+    drop_twin(c);
     int rc = trpo_dev_set_rollout(c->dev, mean, action, adv, c->n);
     c->have_roll = rc == 0;
     if (rc) set_err("rollout upload failed (code %d)", rc);
@@ -303,12 +489,32 @@ double trpo_ctx_update(trpo_ctx *c, size_t max_iter, double resth, double max_kl
     const double t0 = now_s();
     double adv_sum = 0.0, surr0 = 0.0, shs_lm[2] = {0.0, 0.0};
     /* policy gradient (:254-378), CG (:383-628) and FVP(x) (:633-832) on the device, one sync */
-    double *rr = verbose ? (double *)malloc(sizeof(double) * (max_iter + 1)) : NULL;
-    double *xn = verbose ? (double *)malloc(sizeof(double) * (max_iter + 1)) : NULL;
-    int rc = (verbose && (!rr || !xn)) ? TRPO_E_NOMEM
-                                       : trpo_dev_update_solve(c->dev, max_iter, resth, b, x, z, &adv_sum,
-                                                               &inf.cg_iters, rr, xn, max_kl,
-                                                               max_bt > 0 ? &surr0 : NULL, shs_lm);
+    double *rr = (double *)malloc(sizeof(double) * (max_iter + 1));
+    double *xn = (double *)malloc(sizeof(double) * (max_iter + 1));
+    double stats[TRPO_CG_STATS];
+    trpo_dev *dv = c->dev;                 /* the context the update's results come from */
+    c->last_rerun = 0;
+    int rc = (!rr || !xn) ? TRPO_E_NOMEM
+                          : trpo_dev_update_solve(c->dev, max_iter, resth, b, x, z, &adv_sum, &inf.cg_iters, rr, xn,
+                                                  max_kl, max_bt > 0 ? &surr0 : NULL, shs_lm, stats);
+    if (!rc && needs_rerun(c, stats, rr, inf.cg_iters < max_iter ? inf.cg_iters : max_iter)) {
+        /* the fp32 stall guard: the whole device phase again on the fp64 twin (its line search too) */
+        trpo_dev *t = get_twin(c);
+        if (t) {
+            rc = trpo_dev_update_solve(t, max_iter, resth, b, x, z, &adv_sum, &inf.cg_iters, rr, xn, max_kl,
+                                       max_bt > 0 ? &surr0 : NULL, shs_lm, NULL);
+            if (!rc) {
+                dv = t;
+                c->last_rerun = 1;
+                fprintf(stderr, "[WARN] TRPO_Update: a Ritz value of the CG solve converged to %.1e (relative "
+                                "residual), where the reference's fp64 CG loses orthogonality; update solved again "
+                                "in fp64\n", c->last_ritz);
+            }
+        } else {
+            fprintf(stderr, "[WARN] TRPO_Update: a Ritz value converged to %.1e and the fp64 re-solve is "
+                            "unavailable: %s\n", c->last_ritz, g_err);
+        }
+    }
     if (!rc && verbose) /* src/TRPO_CG.c:56 -- one line per iteration */
         for (size_t i = 0; i <= inf.cg_iters && i <= max_iter; ++i)
             printf("CG Iter[%zu] Residual Norm=%.12e, Soln Norm=%.12e\n", i, rr[i], xn[i]);
@@ -334,7 +540,7 @@ double trpo_ctx_update(trpo_ctx *c, size_t max_iter, double resth, double max_kl
     for (size_t i = 0; i < P; ++i) neggdotstepdir += b[i] * x[i];
     memcpy(theta_out, x, P * sizeof(double));        /* reference quirk: theta starts as x */
     const double rate = neggdotstepdir / lm;
-    const double N = trpo_dev_n_total(c->dev);
+    const double N = trpo_dev_n_total(dv);
     const double fval = -adv_sum / N;
     if (verbose) printf("fval before %.14e\n", fval);
     inf.shs = shs;
@@ -351,7 +557,7 @@ double trpo_ctx_update(trpo_ctx *c, size_t max_iter, double resth, double max_kl
         if (k0 == 0)
             surr[0] = surr0;       /* evaluated by the device with the solve (same fullstep, bit for bit) */
         else
-            rc = trpo_dev_surrogate(c->dev, fullstep, k0, nk, surr);
+            rc = trpo_dev_surrogate(dv, fullstep, k0, nk, surr);
         if (rc) {
             set_err("line search failed on the device (code %d)", rc);
             ret = rc < 0 ? rc : TRPO_E_DEVICE;

@@ -62,7 +62,22 @@ struct Ctl {                   // device-side control block of one context
     int iter;
     int done;
     int zero;                  // always 0: "never skip" flag for standalone FVPs
+    double orth;               // max over the solve's steps of the fraction of |r'|^2 the residual
+                               // reorthogonalisation removed (sum c^2 / |r'|^2)
+    double alpha[64];          // the step lengths alpha_k of the first 64 steps (CG_AMAX): with the
+                               // rdotr history they give the Lanczos matrix of the solve, whose Ritz
+                               // residuals are the fp32 stall guard's test (trpo_host.c)
 };
+constexpr int CG_AMAX = 64;
+static_assert(offsetof(Ctl, alpha) == offsetof(Ctl, orth) + sizeof(double) && TRPO_CG_STATS == 1 + CG_AMAX,
+              "Ctl: orth, alpha[] contiguous (one copy exports the statistics)");
+
+// block 0, one lane: ctl->orth = max(ctl->orth, cs / |r'|^2) with |r'|^2 = |r''|^2 + cs
+__device__ __forceinline__ void note_orth(double *orth, double cs, double nr) {
+    const double tot = nr + cs;
+    const double f = tot > 0.0 ? cs / tot : 0.0;
+    *orth = f > *orth ? f : *orth;
+}
 
 struct CgSt {                  // ping-ponged CG scalars (state k = before FVP k)
     double rdotr;
@@ -1223,6 +1238,7 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
                 A.ctl->resth = A.init_resth;
                 A.ctl->rdotr = rr;
                 A.ctl->iter = 0;
+                A.ctl->orth = 0.0;
                 A.ctl->done = (rr < A.init_resth || A.init_maxiter == 0) ? 1 : 0;
             }
         }
@@ -1311,6 +1327,8 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
             A.ctl->rdotr = nr;
             A.ctl->iter = it;
             A.ctl->done = done;
+            note_orth(&A.ctl->orth, cs, nr);
+            if (it <= CG_AMAX) A.ctl->alpha[it - 1] = alpha;
         }
         if (done) return;                              // block-uniform (identical in every block)
         STAMP(11);
@@ -2228,7 +2246,9 @@ fvp_coop_kernel(IterArgs A, Net net) {
             rv[e] -= alpha * zv[e];
             rv[e] -= cr * r0;
         }
-        if (ro && A.nq > 0) qcorrect<EP>((const T *)A.q, (const T *)A.qz, A.P, A.Ps, A.nq, Q::THREADS, shq, alpha, rv);
+        double cs = cr * cr * sin.rdotr;
+        if (ro && A.nq > 0)
+            cs += qcorrect<EP>((const T *)A.q, (const T *)A.qz, A.P, A.Ps, A.nq, Q::THREADS, shq, alpha, rv);
         double s2[2] = {0.0, 0.0};
 #pragma unroll
         for (int e = 0; e < EP; ++e) {
@@ -2262,6 +2282,8 @@ fvp_coop_kernel(IterArgs A, Net net) {
             A.ctl->rdotr = nr;
             A.ctl->iter = it;
             A.ctl->done = done;
+            note_orth(&A.ctl->orth, cs, nr);
+            if (it <= CG_AMAX) A.ctl->alpha[it - 1] = alpha;
         }
         if (done) return;                                  // block-uniform
         __syncthreads();
@@ -2825,6 +2847,7 @@ cg_init_kernel(const double *__restrict__ b, double *x, double *r, double *p, in
         ctl->resth = resth;
         ctl->rdotr = rr;
         ctl->iter = 0;
+        ctl->orth = 0.0;
         st->rdotr = rr;
         st->xx = 0.0;
         st->iter = 0;
@@ -2927,17 +2950,19 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
         rv[e] -= alpha * zv[e];
         rv[e] -= cr * r0;
     }
+    double cs = cr * cr * sin.rdotr;                     // the removed components, squared (ctl->orth)
     if constexpr (QREG) {
         if (ro) {
 #pragma unroll
             for (int i = 0; i < QCAP; ++i) {
                 const double c = -alpha * s1[2 + i];         // zero for the slots >= nq
+                cs += c * c;
 #pragma unroll
                 for (int e = 0; e < E; ++e) rv[e] -= c * qv[i][e];
             }
         }
     } else {
-        if (ro && nq > 0) qcorrect<E>(qbuf, qz, P, Ps, nq, 1024, shq, alpha, rv);
+        if (ro && nq > 0) cs += qcorrect<E>(qbuf, qz, P, Ps, nq, 1024, shq, alpha, rv);
     }
     double rr = 0.0, xx = 0.0;
 #pragma unroll
@@ -2978,6 +3003,8 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
         hist[2 * it] = nr;
         hist[2 * it + 1] = sqrt(xn);
         ctl->done = (nr < th || it >= maxiter) ? 1 : 0;
+        if (ro) note_orth(&ctl->orth, cs, nr);
+        if (it <= CG_AMAX) ctl->alpha[it - 1] = alpha;
     }
     // every thread's reads of acc were consumed before block_sums_dpp's barriers
     for (int e = threadIdx.x; e < zero_len; e += 1024) acc_zero[e] = 0.0;
@@ -3078,6 +3105,7 @@ cg_last_kernel(const double *__restrict__ acc, int R_in, const double *__restric
         hist[2 * it] = nr;
         hist[2 * it + 1] = sqrt(xn2);
         ctl->done = (nr < th || it >= maxiter) ? 1 : 0;
+        if (it <= CG_AMAX) ctl->alpha[it - 1] = alpha;
     }
     // every thread's reads of acc were consumed before the block reduction's barrier
     for (int e = tid; e < zero_len; e += CGL_T) acc_zero[e] = 0.0;
@@ -3267,6 +3295,8 @@ cg_axpy_kernel(const double *__restrict__ dots, int G, const double *__restrict_
         ctl->rdotr = nr;
         ctl->iter = it;
         ctl->done = done;
+        note_orth(&ctl->orth, cs, nr);
+        if (it <= CG_AMAX) ctl->alpha[it - 1] = alpha;
     }
 }
 
@@ -3605,7 +3635,12 @@ static int hgroup_allreduce(trpo_dev *d, double *buf, size_t count) {
     // copies by KERNEL through the mapped buffer, not hipMemcpyAsync: a host-to-device hipMemcpyAsync
     // into buf followed by kernels reading buf gave intermittently stale reads (ranks diverging in
     // whole 512-element cg_axpy slices, 6 of 10 sharded 2x64 solves; tools/diag/shard_race.py)
-    if (ok) hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv((long)count, 256)), dim3(256), 0, d->stream,
+#ifndef TRPO_HGROUP_MEMCPY
+#define TRPO_HGROUP_MEMCPY 0      // diagnostic builds: the copies as hipMemcpyAsync instead
+#endif
+    if (ok && TRPO_HGROUP_MEMCPY)
+        ok = hipMemcpyAsync(d->gbuf, buf, sizeof(double) * count, hipMemcpyDeviceToHost, d->stream) == hipSuccess;
+    else if (ok) hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv((long)count, 256)), dim3(256), 0, d->stream,
                                (const double *)buf, d->gbuf_dev, (int)count);
     ok = ok && hipGetLastError() == hipSuccess;
     ok = ok && hipStreamSynchronize(d->stream) == hipSuccess;
@@ -3626,8 +3661,11 @@ static int hgroup_allreduce(trpo_dev *d, double *buf, size_t count) {
     if (!sum) return -4;
     memcpy(d->gbuf, sum, sizeof(double) * count);
     free(sum);
-    hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv((long)count, 256)), dim3(256), 0, d->stream,
-                       (const double *)d->gbuf_dev, buf, (int)count);
+    if (TRPO_HGROUP_MEMCPY)
+        HCHK(hipMemcpyAsync(buf, d->gbuf, sizeof(double) * count, hipMemcpyHostToDevice, d->stream));
+    else
+        hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv((long)count, 256)), dim3(256), 0, d->stream,
+                           (const double *)d->gbuf_dev, buf, (int)count);
     HCHK(hipGetLastError());
     HCHK(hipStreamSynchronize(d->stream));
     return 0;
@@ -3675,6 +3713,19 @@ static void bind_fast_no(trpo_dev *d) {
     name_fast(d);
 }
 
+static int g_force_prec = -1;        // trpo_dev_create_prec: -1 = TRPO_PRECISION, 0 fp32, 1 fp64
+extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, const char *ac, char *err,
+                                     size_t errlen);
+static pthread_mutex_t g_prec_mu = PTHREAD_MUTEX_INITIALIZER;
+extern "C" trpo_dev *trpo_dev_create_prec(int device, size_t nl, const size_t *ls, const char *ac, int f64,
+                                          char *err, size_t errlen) {
+    pthread_mutex_lock(&g_prec_mu);
+    g_force_prec = f64 ? 1 : 0;
+    trpo_dev *d = trpo_dev_create(device, nl, ls, ac, err, errlen);
+    g_force_prec = -1;
+    pthread_mutex_unlock(&g_prec_mu);
+    return d;
+}
 extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, const char *ac, char *err,
                                      size_t errlen) {
 #define FAIL(...)                                      \
@@ -3765,7 +3816,7 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
     {
         // precision mode: "fp64" runs the FVP in fp64 (v_mfma_f64_16x16x4_f64) -- the reference's
         // own precision -- through the cooperative kernel, which covers every tile-kernel shape
-        const char *ep = getenv("TRPO_PRECISION");
+        const char *ep = g_force_prec >= 0 ? (g_force_prec ? "fp64" : "fp32") : getenv("TRPO_PRECISION");
         d->f64 = ep && (strcmp(ep, "fp64") == 0 || strcmp(ep, "64") == 0 || strcmp(ep, "double") == 0);
         if (ep && !d->f64 && strcmp(ep, "fp32") != 0 && strcmp(ep, "32") != 0 && strcmp(ep, "float") != 0)
             FAIL("TRPO_PRECISION=%s: expected fp32 or fp64", ep);
@@ -4462,8 +4513,40 @@ static size_t peer_slot_doubles(const trpo_dev *d) {
     return s;
 }
 
+// The peer exchange runs only on the HIP runtime the library was built and rpath-linked against
+// (TRPO_HIP_LIBDIR).  Under the copy a PyTorch wheel bundles (ROCm 7.0's, loaded first by a process that
+// imports torch before this library) one in-process peer-attached FVP left every LATER context of the
+// process computing wrong FVPs (2e-3 .. 5e-3 relative, varying run to run), bisected in round 4
+// (tools/diag/torch_first_bisect.py: two contexts attached through peer windows, one standalone FVP
+// each, then a fresh single context; not with the system runtime, not with the host group, not with the
+// same two contexts driven concurrently unattached, not after plain allocate/free of uncached memory).
+// The cause is not found, so the exchange is refused there instead of risking silent wrong results.
+static int peer_runtime_ok(char *msg, size_t len) {
+#ifdef TRPO_HIP_LIBDIR
+    Dl_info info;
+    char a[4096], b[4096];
+    if (!dladdr(reinterpret_cast<void *>(&hipGetDeviceCount), &info) || !info.dli_fname) return 1;
+    if (!realpath(info.dli_fname, a) || !realpath(TRPO_HIP_LIBDIR, b)) return 1;
+    char *slash = strrchr(a, '/');
+    if (slash) *slash = 0;
+    if (strcmp(a, b) != 0) {
+        snprintf(msg, len, "peer exchange refused: this process runs the HIP runtime in %s, the library was built and "
+                 "validated against %s (load libtrpo_mi355x.so before importing torch)", a, b);
+        return 0;
+    }
+#endif
+    (void)msg;
+    (void)len;
+    return 1;
+}
+
 extern "C" int trpo_dev_peer_open(trpo_dev *d, void *handle64) {
     if (!d) return -1;
+    char why[640];
+    if (!getenv("TRPO_PEER_ANY_RUNTIME") && !peer_runtime_ok(why, sizeof why)) {
+        fprintf(stderr, "[trpo_mi355x] %s\n", why);
+        return -4;
+    }
     HCHK(hipSetDevice(d->device));
     if (!d->peer) {
         d->peer = trpo_peer_create(d->device, peer_slot_doubles(d));
@@ -4573,6 +4656,53 @@ extern "C" int trpo_dev_download(trpo_dev *d, int slot, double *host) {
     d->hst_pending = 0;
     memcpy(host, d->hst, sizeof(double) * d->P);
     return trpo_dev_comm_error(d);
+}
+
+// x (slot X) and what the fp32 stall guard reads of the last solve -- ctl->iter, ctl->orth, alpha[] and
+// the rdotr history -- in one synchronisation
+extern "C" int trpo_dev_download_x_cg(trpo_dev *d, double *host, double *stats, double *rdotr, size_t cap,
+                                      size_t *iters) {
+    if (!d || !host || !stats || !rdotr || !iters) return -1;
+    HCHK(hipSetDevice(d->device));
+    const int cw = (int)cdiv(sizeof(Ctl), sizeof(double)), hw = 2 * d->hist_cap;
+    if (ensure_hst(d, (size_t)d->P + cw + hw)) return -2;
+    hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream,
+                       (const double *)d->vec[TRPO_VEC_X], d->hst_dev, d->P);
+    hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv(cw, 256)), dim3(256), 0, d->stream, (const double *)d->ctl,
+                       d->hst_dev + d->P, cw);
+    if (hw) hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv(hw, 256)), dim3(256), 0, d->stream,
+                               (const double *)d->hist, d->hst_dev + d->P + cw, hw);
+    HCHK(hipGetLastError());
+    HCHK(hipStreamSynchronize(d->stream));
+    d->hst_pending = 0;
+    memcpy(host, d->hst, sizeof(double) * d->P);
+    Ctl c;
+    memcpy(&c, d->hst + d->P, sizeof c);
+    stats[0] = c.orth;
+    memcpy(stats + 1, c.alpha, sizeof(double) * CG_AMAX);
+    *iters = (size_t)c.iter;
+    for (size_t k = 0; k <= (size_t)c.iter && k < cap && (int)k < d->hist_cap; ++k)
+        rdotr[k] = d->hst[d->P + cw + 2 * k];
+    return trpo_dev_comm_error(d);
+}
+
+// what a twin context needs to rebuild this one's problem (the host layer's fp64 re-solve)
+extern "C" int trpo_dev_device(const trpo_dev *d) { return d ? d->device : -1; }
+extern "C" int trpo_dev_is_f64(const trpo_dev *d) { return d ? d->f64 : 0; }
+extern "C" int trpo_dev_get_obs(trpo_dev *d, double *host) {
+    if (!d || (!host && d->n)) return -1;
+    if (!d->n) return 0;
+    HCHK(hipSetDevice(d->device));
+    HCHK(hipMemcpyAsync(host, d->obs64, sizeof(double) * d->n * d->net.L[0], hipMemcpyDeviceToHost, d->stream));
+    HCHK(hipStreamSynchronize(d->stream));
+    return 0;
+}
+extern "C" int trpo_dev_get_std(trpo_dev *d, double *host) {
+    if (!d || !host) return -1;
+    HCHK(hipSetDevice(d->device));
+    HCHK(hipMemcpyAsync(host, d->std64, sizeof(double) * d->net.A, hipMemcpyDeviceToHost, d->stream));
+    HCHK(hipStreamSynchronize(d->stream));
+    return 0;
 }
 
 static IterArgs plain_args(trpo_dev *d, const int *skip) {
@@ -5216,6 +5346,7 @@ void trpo_dev_get_view(trpo_dev *d, trpo_dev_view *v) {
     v->vec_z = d->vec[TRPO_VEC_Z];
     v->cg_iter = &d->ctl->iter;
     v->cg_hist = d->hist;
+    v->cg_stats = &d->ctl->orth;
 }
 
 int trpo_dev_allreduce64(trpo_dev *d, double *buf, size_t count) { return allreduce(d, buf, count); }

@@ -817,6 +817,31 @@ extern "C" int trpo_dev_set_rollout(trpo_dev *d, const double *mean, const doubl
     return 0;
 }
 
+// the uploaded rollout back to the host (a twin context's rebuild): mean [n][A], action [n][A], adv [n]
+extern "C" int trpo_dev_get_rollout(trpo_dev *d, double *mean, double *action, double *adv) {
+    if (!d) return -1;
+    trpo_dev_view v;
+    trpo_dev_get_view(d, &v);
+    UpdState *u = state(d);
+    if (!u->have_roll || u->roll_n != v.n) return -3;
+    if (!v.n) return 0;
+    if (!mean || !action || !adv) return -1;
+    HCHK(hipSetDevice(v.device));
+    const int A = v.net.A, W = 2 * A + 1;
+    double *h = (double *)malloc(sizeof(double) * v.n * W);
+    if (!h) return -3;
+    int rc = hipMemcpyAsync(h, u->roll, sizeof(double) * v.n * W, hipMemcpyDeviceToHost, v.stream) ? -2 : 0;
+    if (!rc) rc = hipStreamSynchronize(v.stream) ? -2 : 0;
+    if (!rc)
+        for (size_t s = 0; s < v.n; ++s) {
+            memcpy(mean + s * A, h + s * W, sizeof(double) * A);
+            memcpy(action + s * A, h + s * W + A, sizeof(double) * A);
+            adv[s] = h[s * W + 2 * A];
+        }
+    free(h);
+    return rc;
+}
+
 // enqueue the policy gradient into slot B; *adv_dev = device address of the global sum(Adv)
 static int enqueue_policy_gradient(trpo_dev *d, const double **adv_dev) {
     if (!d) return -1;
@@ -904,13 +929,15 @@ static int enqueue_update_device(trpo_dev *d, size_t maxiter, double resth, doub
     }
     hipLaunchKernelGGL(export_solve_kernel, dim3(cdiv(P > H ? P : H, 256)), dim3(256), 0, v.stream, v.vec_b, v.vec_x,
                        v.vec_z, adv_dev, v.cg_iter, v.cg_hist, P, H, u->hst_dev);
+    hipLaunchKernelGGL(copy64_kernel, dim3(1), dim3(128), 0, v.stream, v.cg_stats, u->hst_dev + 3 * P + 5 + H,
+                       TRPO_CG_STATS);
     HCHK(hipGetLastError());
     return 0;
 }
 
 extern "C" int trpo_dev_update_solve(trpo_dev *d, size_t maxiter, double resth, double *b, double *x, double *z,
                                      double *adv_sum, size_t *iters, double *rdotr_hist, double *xnorm_hist,
-                                     double max_kl, double *surr0, double *shs_lm) {
+                                     double max_kl, double *surr0, double *shs_lm, double *stats) {
     if (!d || !b || !x || !z || !adv_sum || maxiter > 100000) return -1;
     trpo_dev_view v;
     trpo_dev_get_view(d, &v);
@@ -921,7 +948,7 @@ extern "C" int trpo_dev_update_solve(trpo_dev *d, size_t maxiter, double resth, 
     const size_t bytes = sizeof(double) * P;
     const bool surr = surr0 != nullptr;
     // outside any graph: buffers, and the rollout rows of the policy-gradient kernel (new rollout only)
-    if (ensure_host(u, (size_t)3 * P + 5 + H)) return -2;
+    if (ensure_host(u, (size_t)3 * P + 5 + H + TRPO_CG_STATS)) return -2;
     if (!u->fs) HCHK(hipMalloc((void **)&u->fs, sizeof(double) * P));
     if (trpo_dev_pg_prepare(d, u->roll, u->roll_gen) < 0) return -2;
     // (capturing this whole sequence into one graph was measured: ~3 % faster per update, ~10 ms to
@@ -930,6 +957,7 @@ extern "C" int trpo_dev_update_solve(trpo_dev *d, size_t maxiter, double resth, 
     if (rc) return rc;
     HCHK(hipStreamSynchronize(v.stream));
     if (surr0) *surr0 = u->hst[3 * P + 2 + H];
+    if (stats) memcpy(stats, u->hst + 3 * P + 5 + H, sizeof(double) * TRPO_CG_STATS);
     if (shs_lm) {
         shs_lm[0] = u->hst[3 * P + 3 + H];
         shs_lm[1] = u->hst[3 * P + 4 + H];

@@ -125,6 +125,8 @@ def lib():
     L.trpo_ctx_cg.argtypes = [C.c_void_p, _dp, sz, C.c_double, _dp, C.c_int]
     L.trpo_ctx_cg_history.restype = C.c_int
     L.trpo_ctx_cg_history.argtypes = [C.c_void_p, _dp, _dp, sz, P(sz)]
+    L.trpo_ctx_cg_status.restype = C.c_int
+    L.trpo_ctx_cg_status.argtypes = [C.c_void_p, P(C.c_double), P(C.c_double), P(C.c_int)]
     for name in ("trpo_ctx_enqueue_fvp", "trpo_ctx_enqueue_fvp_kernel_only", "trpo_ctx_synchronize"):
         getattr(L, name).restype = C.c_int
         getattr(L, name).argtypes = [C.c_void_p]
@@ -512,6 +514,14 @@ class Context:
         n = it.value + 1
         return rr[:n], xn[:n], it.value
 
+    def cg_status(self):
+        """The fp32 stall guard of the last cg() / update(): dict(ritz_residual = the smallest relative
+        Ritz residual of the solve, orth_loss = the largest fraction of a new residual the
+        reorthogonalisation removed, fp64_rerun = the solve was repeated in fp64)."""
+        rz, o, r = C.c_double(0.0), C.c_double(0.0), C.c_int(0)
+        self._chk(lib().trpo_ctx_cg_status(self._h, C.byref(rz), C.byref(o), C.byref(r)), "cg_status")
+        return dict(ritz_residual=rz.value, orth_loss=o.value, fp64_rerun=bool(r.value))
+
     def set_rollout(self, mean, action, adv):
         """Mean [n][A], Action [n][A], Advantage [n] of this context's samples (TRPO_Update)."""
         A = self.layers[-1]
@@ -531,7 +541,9 @@ class Context:
         t = self._chk(lib().trpo_ctx_update(self._h, max_iter, residual_th, max_kl, max_backtracks, accept_ratio,
                                             th, b, x, C.byref(info), 1 if verbose else 0), "update")
         k = info.evaluated
-        return dict(theta=th, b=b, x=x, shs=info.shs, lagrange=info.lagrange, gnorm=info.gnorm,
+        st = self.cg_status()
+        return dict(theta=th, b=b, x=x, shs=info.shs, ritz_residual=st["ritz_residual"], orth_loss=st["orth_loss"],
+                    fp64_rerun=st["fp64_rerun"], lagrange=info.lagrange, gnorm=info.gnorm,
                     fval=info.fval_before, rate=info.expected_improve_rate, accepted=info.accepted, evaluated=k,
                     actual=np.array(info.actual[:k]), expected=np.array(info.expected[:k]),
                     ratio=np.array(info.ratio[:k]), cg_iters=info.cg_iters, seconds=t)
