@@ -39,11 +39,13 @@ struct Net {
 
 // Pinned host staging buffers that the host writes and kernels read (uploads), or kernels write and
 // the host reads (results through the mapped pointer), are allocated COHERENT (hipHostMallocDefault is
-// non-coherent under HIP_HOST_COHERENT=0, the default: the GPU may cache its lines).  They are only
-// ever accessed by kernels through the mapped pointer and by the host -- never by hipMemcpyAsync: a
-// hipMemcpyAsync to / from such a buffer, with kernels reading the device side right after, gave
-// intermittently stale device data (the host-group all-reduce, tools/diag/shard_race.py: 6 of 10
-// sharded 2x64 solves diverged between ranks; 0 of 10 with copy kernels).
+// non-coherent under HIP_HOST_COHERENT=0, the default: the GPU may cache its lines), and are moved by
+// copy kernels through the mapped pointer (~5 us against ~20 us for a pageable hipMemcpyAsync).
+// Round 2 blamed hipMemcpyAsync for ranks of the host-group all-reduce diverging in whole 512-element
+// slices (6 of 10 sharded 2x64 solves, tools/diag/shard_race.py); round 4 re-ran it with the
+// hipMemcpyAsync form restored (TRPO_HGROUP_MEMCPY=1) on top of the cg_axpy same-launch fix: 0 of 10,
+// like the copy kernels (profiles/r04_diag/torch_first_bisect_and_probes.log) -- the divergence was
+// the cg_axpy race (one 512-element block), not the copy engine.
 #define TRPO_HOST_COHERENT (hipHostMallocMapped | hipHostMallocCoherent)
 
 static inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
