@@ -153,7 +153,8 @@ def test_repeated_updates_deterministic(layers, monkeypatch):
     """A trainer-like sequence on one context -- several updates, set_theta / set_rollout between them,
     a rejected full step, each update repeated -- is deterministic: a run with every CG launched
     eagerly (TRPO_NO_GRAPH=1) and a run on the captured, replayed CG graphs agree bit for bit (the
-    device state the update reuses across calls: forward cache, replica sets, rollout rows, graphs)."""
+    device state the update reuses across calls: forward cache, replica sets, rollout rows, graphs).  Eager
+    is the default launch form since round 4 (TRPO_CG_GRAPH=1 selects the graph)."""
     from trpo_amd import synth
     n = 3000
     th0, obs = synth.make_theta(layers), synth.make_obs(n, layers[0])
@@ -178,7 +179,9 @@ def test_repeated_updates_deterministic(layers, monkeypatch):
     monkeypatch.setenv("TRPO_NO_GRAPH", "1")         # read by the library at every CG enqueue
     eager = run()
     monkeypatch.delenv("TRPO_NO_GRAPH")
+    monkeypatch.setenv("TRPO_CG_GRAPH", "1")
     graph = run()
+    monkeypatch.delenv("TRPO_CG_GRAPH")
     for a, e in zip(graph, eager):
         for x, y in zip(a, e):
             np.testing.assert_array_equal(x, y)

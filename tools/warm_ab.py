@@ -28,13 +28,20 @@ print(json.dumps({"ms": 1e3 * t / K}))
 ''' % (ROOT, os.path.join(ROOT, "trpo-robot-control_amd"))
 
 trials = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+configs = ((20, 5, 0, ""), (20, 5, 1, ""), (500, 50, 0, ""), (20, 50, 0, ""), (100, 5, 0, ""))
+if len(sys.argv) > 2 and sys.argv[2] == "graph":       # CG graph vs eager launches (TRPO_NO_GRAPH)
+    configs = ((20, 5, 0, ""), (20, 5, 0, "TRPO_NO_GRAPH=1"), (500, 50, 0, ""), (500, 50, 0, "TRPO_NO_GRAPH=1"))
 res = {}
 for t in range(trials):
-    for K, W, pre in ((20, 5, 0), (20, 5, 1), (500, 50, 0), (20, 50, 0), (100, 5, 0)):
+    for K, W, pre, env in configs:
+        e = dict(os.environ)
+        if env:
+            k, v = env.split("=")
+            e[k] = v
         p = subprocess.run([sys.executable, "-c", CHILD, str(K), str(W), str(pre)], capture_output=True, text=True,
-                           timeout=120)
+                           timeout=120, env=e)
         ms = json.loads(p.stdout.strip().splitlines()[-1])["ms"] if p.returncode == 0 else None
-        res.setdefault("K%d W%d pre%d" % (K, W, pre), []).append(ms)
-        print("trial %d K=%d W=%d pre=%d: %s ms" % (t, K, W, pre, ms), flush=True)
+        res.setdefault("K%d W%d pre%d %s" % (K, W, pre, env), []).append(ms)
+        print("trial %d K=%d W=%d pre=%d %s: %s ms" % (t, K, W, pre, env, ms), flush=True)
 for k, v in res.items():
     print(k, " ".join("%.4f" % x for x in v if x))

@@ -5132,8 +5132,16 @@ extern "C" int trpo_dev_cg(trpo_dev *d, size_t maxiter, double resth) {
     int rc = ensure_hist(d, maxiter);
     if (rc) return rc;
     d->cg_last_iters = maxiter;
-    const char *ng = getenv("TRPO_NO_GRAPH");
-    if ((ng && atoi(ng)) || d->no_graph || d->group) return enqueue_cg_body(d, maxiter, resth);
+    // Launch form of the solve (round 4): eager stream launches unless an RCCL communicator is attached
+    // (or TRPO_CG_GRAPH=1).  A replayed hipGraph runs its 11 kernels back to back, but consecutive graph
+    // launches left ~3 us of idle GPU between solves; 11 eager launches cost the host ~40 us, far less
+    // than the ~95 us the GPU spends on a 50k solve, so the stream never drains: 10-iteration CG at
+    // N = 50k 0.1031 -> 0.1000 ms per solve for 20 solves after 5, 0.0984 -> 0.0953 for 500 after 50
+    // (profiles/r04_graph_vs_eager.log).  Under RCCL the captured graph stays: an eager solve would also
+    // pay the host-side cost of ten ncclAllReduce enqueues per solve.
+    const char *ng = getenv("TRPO_NO_GRAPH"), *eg = getenv("TRPO_CG_GRAPH");
+    const bool graph = eg ? atoi(eg) != 0 : d->comm != NULL;
+    if ((ng && atoi(ng)) || d->no_graph || d->group || !graph) return enqueue_cg_body(d, maxiter, resth);
     // the graph bakes (maxiter, resth) into cg_init's arguments: key on both
     if (!d->cg_exec || d->cg_graph_iters != maxiter || d->cg_graph_resth != resth) {
         if (d->cg_exec) {
