@@ -64,22 +64,6 @@ def report(name, layers, acts, th, obs, std, b, maxiter=10, resth=1e-10, damping
           flush=True)
 
 
-for name in ("fix_cg_n3150_th1e-10", "fix_cg_n3150_th0", "syn_sigma_cg", "syn_arm_cg_n50000"):
-    c = cases.case(name)
-    X = cases.inputs(c)
-    report(name, X["layers"], X["acfunc"], X["theta"], X["obs"], X["std"], X["vin"], c["maxiter"], c["resth"],
-           X["damping"])
-from test_gpu_random_shapes import _draw  # noqa: E402
-
-for seed in range(36):
-    layers, acts, n, std = _draw(seed)
-    th = synth.make_theta(layers, seed=100 + seed)
-    obs = synth.make_obs(n, layers[0], seed=200 + seed)
-    mean, action, adv = synth.make_rollout(layers, acts, th, obs, std, seed=500 + seed)
-    b, _ = oracle.policy_grad(layers, acts, th, obs, mean, action, adv)
-    report("draw %d %s %s" % (seed, layers, acts), layers, acts, th, obs, std, b)
-
-
 def noisy_probe():
     """the same Ritz test from coefficients carrying the fp32 path's ~1e-7 relative noise"""
     rng = np.random.default_rng(0)
@@ -97,4 +81,22 @@ def noisy_probe():
         print("draw %d: reorth coefficients %.2e, noisy %s" % (seed, ritz_min(al, be), " ".join("%.1e" % v for v in vals)))
 
 
-noisy_probe()
+
+if __name__ == "__main__":
+    for name in ("fix_cg_n3150_th1e-10", "fix_cg_n3150_th0", "syn_sigma_cg", "syn_arm_cg_n50000"):
+        c = cases.case(name)
+        X = cases.inputs(c)
+        report(name, X["layers"], X["acfunc"], X["theta"], X["obs"], X["std"], X["vin"], c["maxiter"], c["resth"],
+               X["damping"])
+    from test_gpu_random_shapes import _draw  # noqa: E402
+
+    for seed in range(36):
+        layers, acts, n, std = _draw(seed)
+        th = synth.make_theta(layers, seed=100 + seed)
+        obs = synth.make_obs(n, layers[0], seed=200 + seed)
+        mean, action, adv = synth.make_rollout(layers, acts, th, obs, std, seed=500 + seed)
+        b, _ = oracle.policy_grad(layers, acts, th, obs, mean, action, adv)
+        report("draw %d %s %s" % (seed, layers, acts), layers, acts, th, obs, std, b)
+
+
+    noisy_probe()
