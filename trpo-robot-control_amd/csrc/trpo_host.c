@@ -90,84 +90,80 @@ static double ritz_threshold(void) {
     return e ? atof(e) : 1e-15;
 }
 
-/* eigen-decomposition of the symmetric k x k matrix a (row-major, destroyed) by cyclic Jacobi; w the
- * eigenvalues, v the eigenvectors as columns (k <= 64) */
-static void jacobi_eig(double *a, int k, double *w, double *v) {
-    for (int i = 0; i < k; ++i)
-        for (int j = 0; j < k; ++j) v[i * k + j] = i == j ? 1.0 : 0.0;
-    for (int sweep = 0; sweep < 30; ++sweep) {
-        double off = 0.0, tot = 0.0;
-        for (int i = 0; i < k; ++i)
-            for (int j = 0; j < k; ++j) {
-                tot += a[i * k + j] * a[i * k + j];
-                if (i != j) off += a[i * k + j] * a[i * k + j];
+/* eigenvalues d[] of the symmetric tridiagonal matrix (diagonal d, e[i] = T[i][i+1] for i < n - 1) and
+ * the LAST components zl[] of its eigenvectors: implicit QL with Wilkinson shifts, the last row of the
+ * eigenvector matrix carried alone (O(n^2)); -1 if it does not converge */
+static int tql_last(double *d, double *e, double *zl, int n) {
+    for (int i = 0; i < n; ++i) zl[i] = i == n - 1 ? 1.0 : 0.0;
+    e[n - 1] = 0.0;
+    for (int l = 0; l < n; ++l) {
+        int iter = 0, m;
+        do {
+            for (m = l; m < n - 1; ++m) {
+                const double dd = fabs(d[m]) + fabs(d[m + 1]);
+                if (fabs(e[m]) <= 2.2e-16 * dd) break;
             }
-        /* converged to rounding: off-diagonal norm below eps x the matrix norm (a stricter test never
-         * ends -- rounding keeps the off-diagonal at ~eps -- and 100 sweeps cost 0.15 ms per update) */
-        if (off <= 1e-33 * tot) break;
-        int rotated = 0;
-        for (int p = 0; p < k; ++p)
-            for (int q = p + 1; q < k; ++q) {
-                const double apq = a[p * k + q];
-                if (fabs(apq) <= 1e-18 * sqrt(fabs(a[p * k + p] * a[q * k + q]))) continue;
-                rotated = 1;
-                const double th = (a[q * k + q] - a[p * k + p]) / (2.0 * apq);
-                const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1.0));
-                const double cs = 1.0 / sqrt(t * t + 1.0), sn = t * cs;
-                for (int r = 0; r < k; ++r) {                 /* a <- a J (columns p, q) */
-                    const double x = a[r * k + p], y = a[r * k + q];
-                    a[r * k + p] = cs * x - sn * y;
-                    a[r * k + q] = sn * x + cs * y;
+            if (m != l) {
+                if (iter++ == 60) return -1;
+                double g = (d[l + 1] - d[l]) / (2.0 * e[l]);
+                double r = hypot(g, 1.0);
+                g = d[m] - d[l] + e[l] / (g + copysign(r, g));
+                double sn = 1.0, cs = 1.0, p = 0.0;
+                int i;
+                for (i = m - 1; i >= l; --i) {
+                    double f = sn * e[i];
+                    const double b = cs * e[i];
+                    e[i + 1] = (r = hypot(f, g));
+                    if (r == 0.0) {
+                        d[i + 1] -= p;
+                        e[m] = 0.0;
+                        break;
+                    }
+                    sn = f / r;
+                    cs = g / r;
+                    g = d[i + 1] - p;
+                    r = (d[i] - g) * sn + 2.0 * cs * b;
+                    d[i + 1] = g + (p = sn * r);
+                    g = cs * r - b;
+                    f = zl[i + 1];                       /* the last eigenvector row, rotated alone */
+                    zl[i + 1] = sn * zl[i] + cs * f;
+                    zl[i] = cs * zl[i] - sn * f;
                 }
-                for (int r = 0; r < k; ++r) {                 /* a <- J^T a (rows p, q) */
-                    const double x = a[p * k + r], y = a[q * k + r];
-                    a[p * k + r] = cs * x - sn * y;
-                    a[q * k + r] = sn * x + cs * y;
-                }
-                for (int r = 0; r < k; ++r) {                 /* v <- v J */
-                    const double x = v[r * k + p], y = v[r * k + q];
-                    v[r * k + p] = cs * x - sn * y;
-                    v[r * k + q] = sn * x + cs * y;
-                }
+                if (r == 0.0 && i >= l) continue;
+                d[l] -= p;
+                e[l] = g;
+                e[m] = 0.0;
             }
-        if (!rotated) break;
+        } while (m != l);
     }
-    for (int i = 0; i < k; ++i) w[i] = a[i * k + i];
+    return 0;
 }
 
 /* smallest relative Ritz residual of the Lanczos matrix T_iters of a CG solve (alpha_k, rdotr_k as the
  * device recorded them; iters <= 64); 1 when there is nothing to test.  Only the last T: a Ritz value
  * that has converged stays converged, and over the goldens and the 36 random draws the minimum over
- * T_1 .. T_iters always sat at the last one (tools/diag/ritz_probe.py); ~8 us on the host for 10 steps. */
+ * T_1 .. T_iters always sat at the last one (tools/diag/ritz_probe.py); ~1 us on the host for 10 steps. */
 static double ritz_min(const double *alpha, const double *rdotr, size_t iters) {
     int K = iters > 64 ? 64 : (int)iters;
-    double best = 1.0;
     for (int j = 0; j < K; ++j)                /* the valid prefix (a converged solve stops early) */
         if (!(alpha[j] > 0.0) || !(rdotr[j] > 0.0) || !isfinite(alpha[j]) || !(rdotr[j + 1] >= 0.0)) {
             K = j;
             break;
         }
-    if (K < 1) return best;
-    double *a = (double *)malloc(sizeof(double) * (2 * (size_t)K * K + K));
-    if (!a) return best;
-    double *v = a + K * K, *w = v + K * K;
-    for (int k = K; k <= K; ++k) {
-        for (int i = 0; i < k * k; ++i) a[i] = 0.0;
-        for (int j = 0; j < k; ++j) {
-            const double bj = rdotr[j + 1] / rdotr[j];
-            a[j * k + j] = 1.0 / alpha[j] + (j > 0 ? (rdotr[j] / rdotr[j - 1]) / alpha[j - 1] : 0.0);
-            if (j + 1 < k) a[j * k + j + 1] = a[(j + 1) * k + j] = sqrt(bj) / alpha[j];
-        }
-        jacobi_eig(a, k, w, v);
-        double wmax = 0.0;
-        for (int i = 0; i < k; ++i) wmax = fabs(w[i]) > wmax ? fabs(w[i]) : wmax;
-        const double bk = sqrt(rdotr[k] / rdotr[k - 1]) / alpha[k - 1];
-        for (int i = 0; i < k && wmax > 0.0; ++i) {
-            const double res = bk * fabs(v[(k - 1) * k + i]) / wmax;
-            best = res < best ? res : best;
-        }
+    if (K < 1) return 1.0;
+    double d[64], e[64], zl[64];
+    for (int j = 0; j < K; ++j) {
+        d[j] = 1.0 / alpha[j] + (j > 0 ? (rdotr[j] / rdotr[j - 1]) / alpha[j - 1] : 0.0);
+        e[j] = j + 1 < K ? sqrt(rdotr[j + 1] / rdotr[j]) / alpha[j] : 0.0;
     }
-    free(a);
+    if (tql_last(d, e, zl, K)) return 1.0;
+    double wmax = 0.0, best = 1.0;
+    for (int i = 0; i < K; ++i) wmax = fabs(d[i]) > wmax ? fabs(d[i]) : wmax;
+    const double bk = sqrt(rdotr[K] / rdotr[K - 1]) / alpha[K - 1];
+    for (int i = 0; i < K && wmax > 0.0; ++i) {
+        const double res = bk * fabs(zl[i]) / wmax;
+        best = res < best ? res : best;
+    }
     return best;
 }
 
