@@ -97,6 +97,8 @@ int trpo_dev_allreduce64(trpo_dev *d, double *buf, size_t count);
 // when it changes.
 int trpo_dev_pg_sums_fast(trpo_dev *d, const double *roll64, unsigned roll_gen, const double **zacc);
 int trpo_dev_pg_prepare(trpo_dev *d, const double *roll64, unsigned roll_gen);
+// the update path's CG (graph-replayed unless TRPO_CG_GRAPH=0: it sits between other kernels)
+int trpo_dev_cg_in_sequence(trpo_dev *d, size_t maxiter, double resth);
 // forward-cache bookkeeping after a CG solve
 void trpo_dev_ycache_written(trpo_dev *d);
 // per-context storage of the update path (owned by trpo_update.hip)

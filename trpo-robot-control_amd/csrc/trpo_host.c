@@ -323,6 +323,7 @@ int trpo_ctx_attach_comm_timeout(trpo_ctx *c, int rank, int world, const void *i
     drop_twin(c);
     const int rc = trpo_dev_set_comm(c->dev, rank, world, id, timeout_ms);
     if (rc == TRPO_E_TIMEOUT) set_err("RCCL init (rank %d of %d) did not complete within its time limit", rank, world);
+    else if (rc) set_err("RCCL attach (rank %d of %d) failed (code %d; ncclCommInitRank's reason on stderr)", rank, world, rc);
     return rc;
 }
 int trpo_ctx_comm_verify(trpo_ctx *c, long timeout_ms) {

@@ -5125,7 +5125,13 @@ void trpo_dev_ycache_written(trpo_dev *d) {
     if (cg_writes_ycache(d, d->cg_last_iters)) d->yc_valid = 1;
 }
 
-extern "C" int trpo_dev_cg(trpo_dev *d, size_t maxiter, double resth) {
+static int dev_cg(trpo_dev *d, size_t maxiter, double resth, bool in_sequence);
+extern "C" int trpo_dev_cg(trpo_dev *d, size_t maxiter, double resth) { return dev_cg(d, maxiter, resth, false); }
+// the CG of the update path's device phase: between other kernels of one submission the replayed graph
+// is the cheaper form (0.169 vs 0.176 ms per armDOF_0 update, 0.614 vs 0.623 ms for 2x64, N = 50k:
+// profiles/r04_launch_form_ab.log) -- no consecutive graphs there, and 11 fewer host launches
+int trpo_dev_cg_in_sequence(trpo_dev *d, size_t maxiter, double resth) { return dev_cg(d, maxiter, resth, true); }
+static int dev_cg(trpo_dev *d, size_t maxiter, double resth, bool in_sequence) {
     if (!d || d->n_total <= 0) return -1;
     HCHK(hipSetDevice(d->device));
     if (maxiter > 100000) return -1;
@@ -5140,7 +5146,7 @@ extern "C" int trpo_dev_cg(trpo_dev *d, size_t maxiter, double resth) {
     // (profiles/r04_graph_vs_eager.log).  Under RCCL the captured graph stays: an eager solve would also
     // pay the host-side cost of ten ncclAllReduce enqueues per solve.
     const char *ng = getenv("TRPO_NO_GRAPH"), *eg = getenv("TRPO_CG_GRAPH");
-    const bool graph = eg ? atoi(eg) != 0 : d->comm != NULL;
+    const bool graph = eg ? atoi(eg) != 0 : (d->comm != NULL || in_sequence);
     if ((ng && atoi(ng)) || d->no_graph || d->group || !graph) return enqueue_cg_body(d, maxiter, resth);
     // the graph bakes (maxiter, resth) into cg_init's arguments: key on both
     if (!d->cg_exec || d->cg_graph_iters != maxiter || d->cg_graph_resth != resth) {

@@ -908,7 +908,7 @@ static int enqueue_surrogate(trpo_dev *d, const double *fs, int k0, int nk);
 static int enqueue_update_device(trpo_dev *d, size_t maxiter, double resth, double max_kl, bool surr) {
     const double *adv_dev = nullptr;
     int rc = enqueue_policy_gradient(d, &adv_dev);             // :254-378
-    if (!rc) rc = trpo_dev_cg(d, maxiter, resth);               // :383-628 (the context's CG graph)
+    if (!rc) rc = trpo_dev_cg_in_sequence(d, maxiter, resth);   // :383-628 (the context's CG graph)
     if (rc) return rc;
     trpo_dev_ycache_written(d);
     trpo_dev_view v;
