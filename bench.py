@@ -25,7 +25,6 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import socket
 import subprocess
 import sys
 import tempfile
@@ -63,11 +62,10 @@ def parse_args():
 def relaunch(args) -> int:
     """--gpus N without a torch.distributed environment: start N rank processes (one per GPU) with
     torch.distributed.run and exit with its code.  Nothing in this process has touched HIP."""
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    # --standalone: the rendezvous store binds a free port itself (a port probed here and passed on
+    # can be taken by another process on a shared box before torchrun binds it: EADDRINUSE, seen once)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--standalone", "--local-addr", "127.0.0.1",
+           "--nnodes=1", "--nproc-per-node=%d" % args.gpus, os.path.abspath(__file__)] + sys.argv[1:]
     return subprocess.run(cmd).returncode
 
 
@@ -538,33 +536,50 @@ def extras_single(device, dist, reps):
 
 
 def extras_multi(device, dist, b, x_rccl, comm="rccl"):
-    """N > 1: the same sharded solve with the peer-window exchange in place of RCCL (A/B on the driver's
-    multi-GPU node), and one sharded TRPO update (config C5) under RCCL."""
-    import numpy as np
-    from trpo_amd import synth
+    """N > 1: the same sharded solve with the other collectives in place of the headline's (A/B on the
+    driver's multi-GPU node): RCCL or the peer-window exchange (flag hand-off), and the peer exchange in
+    its tagged-granule form (TRPO_PEER_PROTO=2: the data is its own flag, one xGMI trip fewer per
+    exchange, measured 1.4 us slower than the flag form on one GPU); and one sharded TRPO update
+    (config C5) under the headline's collective."""
     out = {}
-    res, ctx = None, None
     other = "rccl" if comm == "peer" else "peer"
+    out["C4_%s_exchange" % other] = _solve_multi(device, dist, b, x_rccl, other, {})
+    out["C4_peer_granule_exchange"] = _solve_multi(device, dist, b, x_rccl, "peer", {"TRPO_PEER_PROTO": "2"})
     try:
-        ctx, _, _, _, rec = make_ctx_agreed(ARM, N_TOTAL, dist, device, other, b, plan=(other,))
+        out["C5_update_armDOF_0_N50000"] = _update_multi(device, dist, comm)
+    except Exception as e:                      # noqa: BLE001 -- recorded; the headline line still prints
+        out["C5_update_armDOF_0_N50000"] = {"error": "%s: %s" % (type(e).__name__, e)}
+    return out
+
+
+def _solve_multi(device, dist, b, x_ref, backend, env):
+    """The headline's sharded solve on one collective (env: library knobs set while the context and its
+    collective are created, the same on every rank), timed like the headline (50 after 5)."""
+    import numpy as np
+    res, ctx = None, None
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        ctx, _, _, _, rec = make_ctx_agreed(ARM, N_TOTAL, dist, device, backend, b, plan=(backend,))
     except SystemExit as e:                     # recorded; every rank skips together (agreed inside)
         res = {"error": str(e)}
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     if ctx is not None:
         try:
             t = time_steps(ctx, dist, 50, 5, b)
             x = ctx.download_x()
             res = {"ms_per_step": 1e3 * t / 50, "fvp_samples_per_s": CG_ITERS * N_TOTAL / (t / 50),
                    "backend": ctx.comm_backend, "n_gpus": dist.world, "verify": rec["verify"],
-                   "x_relL2_vs_headline": float(np.linalg.norm(x - x_rccl) / np.linalg.norm(x_rccl))}
+                   "x_relL2_vs_headline": float(np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref))}
         except Exception as e:                  # noqa: BLE001
             res = {"error": "%s: %s" % (type(e).__name__, e)}
         ctx.close()
-    out["C4_%s_exchange" % other] = res
-    try:
-        out["C5_update_armDOF_0_N50000"] = _update_multi(device, dist, comm)
-    except Exception as e:                      # noqa: BLE001 -- recorded; the headline line still prints
-        out["C5_update_armDOF_0_N50000"] = {"error": "%s: %s" % (type(e).__name__, e)}
-    return out
+    return res
 
 
 def _update_multi(device, dist, comm):

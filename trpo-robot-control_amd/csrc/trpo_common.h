@@ -119,6 +119,7 @@ int trpo_peer_allreduce(trpo_peer *p, hipStream_t st, const double *in, int R, i
 int trpo_peer_error(const trpo_peer *p);
 size_t trpo_peer_slot(const trpo_peer *p);
 int trpo_peer_fenced(const trpo_peer *p);
+int trpo_peer_proto(const trpo_peer *p);      // 1 flag + batched loads, 2 tagged granules, 0 round-3 loops
 void trpo_peer_set_error(trpo_peer *p);
 
 #endif

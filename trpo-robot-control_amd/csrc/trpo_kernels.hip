@@ -4602,7 +4602,10 @@ extern "C" const char *trpo_hip_runtime_path(void) {
 extern "C" const char *trpo_dev_comm_backend(const trpo_dev *d) {
     if (!d) return "";
     if (d->comm_aborted) return "aborted";
-    if (d->peer_on) return trpo_peer_fenced(d->peer) ? "peer-xgmi (uncached window, fenced hand-off)" : "peer-xgmi (uncached window)";
+    if (d->peer_on)
+        return trpo_peer_proto(d->peer) == 2 ? "peer-xgmi (uncached window, tagged granules)"
+               : trpo_peer_fenced(d->peer)   ? "peer-xgmi (uncached window, fenced hand-off)"
+                                             : "peer-xgmi (uncached window)";
     if (d->comm) return "rccl";
     if (d->group) return "host-group";
     return "none";

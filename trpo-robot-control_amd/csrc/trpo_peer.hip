@@ -24,6 +24,11 @@
 // which read that set) has completed.
 // A poll that does not see its flag within 3 s sets an error word (pinned host memory) instead of
 // spinning forever; later exchanges then skip the wait (results invalid, but the GPU is released).
+// The exchange is a chain of dependent memory round trips (~1.5 us each on one GPU), so the loads of
+// steps 1 and 5 go out in rounds with every load of a round in flight (round 4: the per-element loops
+// cost one trip per element and replica; tools/peer_floor.py on one GPU, the exchange of the rank that
+// arrives second: 9.9 -> 7.3 us, profiles/r04_peer_exchange_floor_1gpu.txt).  TRPO_PEER_PROTO selects
+// 1 (this form, default), 0 (the round-3 loops) or 2 (peer_granule_kernel below: no flag at all).
 //
 // Memory ordering (round 4).  The window is allocated uncached, and every exchanged byte is stored and
 // loaded at system scope, so on the system ROCm no cache can hold a stale line of it.  That property
@@ -58,9 +63,12 @@ struct trpo_peer {
     int rank, world;
     int connected;                   // windows carry the exchange numbering: one connect per window
     int fence;                       // release / acquire around the flag hand-off (TRPO_PEER_FENCE, default 1)
+    int proto;                       // TRPO_PEER_PROTO: 1 flag + batched loads (default), 2 tagged granules, 0 the round-3 loops
 };
 
-static size_t win_doubles(size_t S) { return 2 * (size_t)PEER_WMAX * S + (size_t)PEER_WMAX * FLAG_STRIDE; }
+static size_t flag_doubles(size_t S) { return 2 * (size_t)PEER_WMAX * S + (size_t)PEER_WMAX * FLAG_STRIDE; }
+// + the tagged-granule data region: [2 sets][PEER_WMAX slots][S elements][2 granules] u64
+static size_t win_doubles(size_t S) { return flag_doubles(S) + 4 * (size_t)PEER_WMAX * S; }
 
 // global (not flat) address space for the window accesses: the window pointers come from memory,
 // where the compiler cannot infer it, and flat operations also count in lgkmcnt
@@ -74,20 +82,48 @@ __device__ __forceinline__ double ld_sys(const double *p) {
     return __hip_atomic_load(gptr(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Loads are issued in rounds of PE elements per thread with every replica / slot load of the round
+// in flight together (R <= PE_R and world <= PEER_WMAX loads per element, clamped indices, values
+// selected after): one memory round trip per round instead of one per element and per replica.  The
+// counter, the done flag and the first round's inputs go out together, before the done test.
+constexpr int PE = 4, PE_R = 8;
+template <bool BATCH>
 __global__ void __launch_bounds__(PEER_T)
 peer_exchange_kernel(const double *__restrict__ in, int R, int Rstride, int count, double *const *wins, int rank,
                      int world, int S, double *__restrict__ out, unsigned long long *cnt, int *err, const int *done,
                      int fence) {
-    if (done && *done) return;                     // converged CG: every rank skips the same exchanges
     const int t = blockIdx.x, tid = threadIdx.x;
+    if (!BATCH && done && *done) return;          // converged CG: every rank skips the same exchanges
     const unsigned long long e = cnt[t] + 1;
     const int set = (int)(e & 1);
     // 1 + 2: local replica sum (replica order) pushed into slot `rank` of rank t's window
     double *dst = wins[t] + ((size_t)set * PEER_WMAX + rank) * S;
-    for (int i = tid; i < count; i += PEER_T) {
-        double v = in[i];
-        for (int k = 1; k < R; ++k) v += in[(long)k * Rstride + i];
-        st_sys(dst + i, v);
+    if (BATCH) {
+        const int dn = done ? *done : 0;
+        for (int i0 = 0; i0 < count; i0 += PE * PEER_T) {
+            double v[PE][PE_R];
+#pragma unroll
+            for (int k = 0; k < PE; ++k)
+#pragma unroll
+                for (int r = 0; r < PE_R; ++r)
+                    v[k][r] = in[(long)min(r, R - 1) * Rstride + min(i0 + tid + k * PEER_T, count - 1)];
+            if (dn) return;                           // (grid-uniform) after the loads were issued
+#pragma unroll
+            for (int k = 0; k < PE; ++k) {
+                const int i = i0 + tid + k * PEER_T;
+                double s = v[k][0];
+#pragma unroll
+                for (int r = 1; r < PE_R; ++r) s += r < R ? v[k][r] : 0.0;
+                for (int r = PE_R; r < R; ++r) s += in[(long)r * Rstride + min(i, count - 1)];
+                if (i < count) st_sys(dst + i, s);
+            }
+        }
+    } else {
+        for (int i = tid; i < count; i += PEER_T) {
+            double v = in[i];
+            for (int k = 1; k < R; ++k) v += in[(long)k * Rstride + i];
+            st_sys(dst + i, v);
+        }
     }
     // 3: every storing wave drained, a workgroup barrier, then (fence) one system-scope release and its
     // own drain, then the flag
@@ -125,11 +161,125 @@ peer_exchange_kernel(const double *__restrict__ in, int R, int Rstride, int coun
     // 5: slice t of the elements (system-scope loads), summed over the slots in rank order
     const int per = (count + world - 1) / world, lo = t * per, hi = min(count, lo + per);
     const double *src = own + (size_t)set * PEER_WMAX * S;
-    for (int i = lo + tid; i < hi; i += PEER_T) {
-        double s = ld_sys(src + i);
-        for (int r = 1; r < world; ++r) s += ld_sys(src + (size_t)r * S + i);
-        out[i] = s;
+    if (BATCH) {
+        constexpr int PE5 = 2;
+        for (int i0 = lo; i0 < hi; i0 += PE5 * PEER_T) {
+            double v[PE5][PEER_WMAX];
+#pragma unroll
+            for (int k = 0; k < PE5; ++k)
+#pragma unroll
+                for (int r = 0; r < PEER_WMAX; ++r)
+                    v[k][r] = r < world ? ld_sys(src + (size_t)r * S + min(i0 + tid + k * PEER_T, hi - 1)) : 0.0;
+#pragma unroll
+            for (int k = 0; k < PE5; ++k) {
+                const int i = i0 + tid + k * PEER_T;
+                double s = v[k][0];
+#pragma unroll
+                for (int r = 1; r < PEER_WMAX; ++r) s += r < world ? v[k][r] : 0.0;
+                if (i < hi) out[i] = s;
+            }
+        }
+    } else {
+        for (int i = lo + tid; i < hi; i += PEER_T) {
+            double s = ld_sys(src + i);
+            for (int r = 1; r < world; ++r) s += ld_sys(src + (size_t)r * S + i);
+            out[i] = s;
+        }
     }
+    if (tid == 0) cnt[t] = e;
+}
+
+// The same exchange with the data as its own flag (TRPO_PEER_PROTO=2): every fp64 travels as two
+// 8-byte granules {tag = (uint32) e, 32 bits of the value}, each one system-scope store -- single-copy
+// atomic, so a reader sees a granule either from exchange e or from an older one, and the tag says
+// which.  The reader polls the granules of its slice in all ranks' slots until every tag reads e, then
+// sums in rank order.  No drain-before-flag, no flag, no release / acquire (nothing is published
+// through a second location): one store pass and one polled load pass, against the flag form's
+// stores, drain, release, flag, poll, acquire and slot loads.  Two sets, by the same argument as the
+// flag form (workgroup t of a rank writes set e & 1 for exchange e + 2 only after reading every
+// rank's granules of e + 1, i.e. after every rank finished exchange e).
+__device__ __forceinline__ void st_sys64(unsigned long long *p, unsigned long long v) {
+    __hip_atomic_store((gu64 *)(size_t)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ unsigned long long ld_sys64(const unsigned long long *p) {
+    return __hip_atomic_load((gu64 *)(size_t)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__global__ void __launch_bounds__(PEER_T)
+peer_granule_kernel(const double *__restrict__ in, int R, int Rstride, int count, double *const *wins, int rank,
+                    int world, int S, double *__restrict__ out, unsigned long long *cnt, int *err, const int *done,
+                    size_t goff) {
+    const int t = blockIdx.x, tid = threadIdx.x;
+    const unsigned long long e = cnt[t] + 1;
+    const unsigned long long tag = (e & 0xffffffffULL) << 32;
+    const int set = (int)(e & 1);
+    const int dn = done ? *done : 0;
+    // 1: local replica sum (replica order) pushed as tagged granules into slot `rank` of rank t's window
+    unsigned long long *dst =
+        reinterpret_cast<unsigned long long *>(wins[t] + goff) + 2 * ((size_t)set * PEER_WMAX + rank) * S;
+    for (int i0 = 0; i0 < count; i0 += PE * PEER_T) {
+        double v[PE][PE_R];
+#pragma unroll
+        for (int k = 0; k < PE; ++k)
+#pragma unroll
+            for (int r = 0; r < PE_R; ++r)
+                v[k][r] = in[(long)min(r, R - 1) * Rstride + min(i0 + tid + k * PEER_T, count - 1)];
+        if (dn) return;                               // (grid-uniform) after the loads were issued
+#pragma unroll
+        for (int k = 0; k < PE; ++k) {
+            const int i = i0 + tid + k * PEER_T;
+            double s = v[k][0];
+#pragma unroll
+            for (int r = 1; r < PE_R; ++r) s += r < R ? v[k][r] : 0.0;
+            for (int r = PE_R; r < R; ++r) s += in[(long)r * Rstride + min(i, count - 1)];
+            if (i < count) {
+                const unsigned long long b = (unsigned long long)__double_as_longlong(s);
+                st_sys64(dst + 2 * i, tag | (b & 0xffffffffULL));
+                st_sys64(dst + 2 * i + 1, tag | (b >> 32));
+            }
+        }
+    }
+    // 2: slice t of the elements, polled in every rank's slot of the OWN window until all tags read e
+    const int per = (count + world - 1) / world, lo = t * per, hi = min(count, lo + per);
+    const unsigned long long *src =
+        reinterpret_cast<const unsigned long long *>(wins[rank] + goff) + 2 * (size_t)set * PEER_WMAX * S;
+    constexpr int PE5 = 2;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    int failed = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (int i0 = lo; i0 < hi; i0 += PE5 * PEER_T) {
+        unsigned long long g[PE5][PEER_WMAX][2];
+        for (;;) {
+            bool ok = true;
+#pragma unroll
+            for (int k = 0; k < PE5; ++k)
+#pragma unroll
+                for (int r = 0; r < PEER_WMAX; ++r) {
+                    const size_t a = 2 * ((size_t)r * S + min(i0 + tid + k * PEER_T, hi - 1));
+                    g[k][r][0] = r < world ? ld_sys64(src + a) : tag;
+                    g[k][r][1] = r < world ? ld_sys64(src + a + 1) : tag;
+                    ok = ok && (g[k][r][0] >> 32) == (tag >> 32) && (g[k][r][1] >> 32) == (tag >> 32);
+                }
+            if (ok || failed) break;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > WAIT_TICKS) {
+                __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                failed = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+#pragma unroll
+        for (int k = 0; k < PE5; ++k) {
+            const int i = i0 + tid + k * PEER_T;
+            double s = 0.0;
+#pragma unroll
+            for (int r = 0; r < PEER_WMAX; ++r) {
+                const double x = __longlong_as_double(
+                    (long long)((g[k][r][0] & 0xffffffffULL) | ((g[k][r][1] & 0xffffffffULL) << 32)));
+                s = r == 0 ? x : (r < world ? s + x : s);
+            }
+            if (i < hi) out[i] = s;
+        }
+    }
+    __syncthreads();                                  // every wave's reads of set e & 1 are done
     if (tid == 0) cnt[t] = e;
 }
 
@@ -160,6 +310,8 @@ trpo_peer *trpo_peer_create(int device, size_t S) {
     // release / acquire make it correct on any window; see the header comment)
     const char *ef = getenv("TRPO_PEER_FENCE");
     p->fence = !(ef && atoi(ef) == 0);
+    const char *eb = getenv("TRPO_PEER_PROTO");
+    p->proto = eb ? atoi(eb) : 1;
     if (hipExtMallocWithFlags((void **)&p->win, bytes, hipDeviceMallocUncached) != hipSuccess) {
         (void)hipGetLastError();
         p->win = NULL;
@@ -247,8 +399,15 @@ int trpo_peer_allreduce(trpo_peer *p, hipStream_t st, const double *in, int R, i
                         const int *done) {
     if (!p || count < 0 || (size_t)count > p->S || R < 1 || in == out) return -1;
     if (count == 0) return 0;
-    hipLaunchKernelGGL(peer_exchange_kernel, dim3(p->world), dim3(PEER_T), 0, st, in, R, Rstride, count, p->dwins,
-                       p->rank, p->world, (int)p->S, out, p->cnt, p->err_d, done, p->fence);
+    if (p->proto == 2)
+        hipLaunchKernelGGL(peer_granule_kernel, dim3(p->world), dim3(PEER_T), 0, st, in, R, Rstride, count, p->dwins,
+                           p->rank, p->world, (int)p->S, out, p->cnt, p->err_d, done, flag_doubles(p->S));
+    else if (p->proto == 1)
+        hipLaunchKernelGGL(peer_exchange_kernel<true>, dim3(p->world), dim3(PEER_T), 0, st, in, R, Rstride, count,
+                           p->dwins, p->rank, p->world, (int)p->S, out, p->cnt, p->err_d, done, p->fence);
+    else
+        hipLaunchKernelGGL(peer_exchange_kernel<false>, dim3(p->world), dim3(PEER_T), 0, st, in, R, Rstride, count,
+                           p->dwins, p->rank, p->world, (int)p->S, out, p->cnt, p->err_d, done, p->fence);
     HCHK(hipGetLastError());
     return 0;
 }
@@ -256,6 +415,7 @@ int trpo_peer_allreduce(trpo_peer *p, hipStream_t st, const double *in, int R, i
 int trpo_peer_error(const trpo_peer *p) { return p && p->err_h ? __atomic_load_n(p->err_h, __ATOMIC_ACQUIRE) : 0; }
 size_t trpo_peer_slot(const trpo_peer *p) { return p ? p->S : 0; }
 int trpo_peer_fenced(const trpo_peer *p) { return p ? p->fence : 0; }
+int trpo_peer_proto(const trpo_peer *p) { return p ? p->proto : 0; }
 // abandon the exchange (trpo_dev_comm_abort): later exchanges skip their waits and report the error
 void trpo_peer_set_error(trpo_peer *p) {
     if (p && p->err_h) __atomic_store_n(p->err_h, 1, __ATOMIC_RELEASE);
