@@ -19,6 +19,9 @@ Measured in this order: the secondary configs (extra), the dominant kernel's HIP
 (roofline), then the headline's timed region (W untimed solves, exactly K timed ones).  At N > 1
 the headline's collective is set up stage by stage with cross-rank agreement, self-checked and
 hash-checked before anything is timed (make_ctx_agreed; comm.verify / comm.fallback in the line).
+At N = 1, after the timed region, roofline.traffic is measured in the same run: two rocprofv3 PMC
+passes (FETCH_SIZE, WRITE_SIZE, one per child process of this script on the headline workload;
+measure_traffic); --no-pmc, or a failed pass, falls back to the newest committed profile.
 """
 from __future__ import annotations
 
@@ -54,6 +57,9 @@ def parse_args():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--comm", choices=("rccl", "peer"), default="rccl",
                     help="N > 1: collective of the headline solve (peer: the peer-window exchange over xGMI)")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="N = 1: take roofline.traffic from the newest committed profile instead of measuring it")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)   # internal: see measure_traffic
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the secondary configs (C2, C3 2x64, fp64, C5, baseline, N sweep)")
     return ap.parse_args()
@@ -642,8 +648,72 @@ def latest_traffic_json():
     return files[-1] if files else None
 
 
+PMC_KERNEL = "fvp_mlp3_kernel<1, 1, 1, 1, 5, 3"       # the CG-iteration kernel (MODE 3, every QB variant)
+
+
+def pmc_child(device):
+    """--pmc-child: the headline workload (armDOF_0, the seeded 50k batch, b) for a few CG solves,
+    run by measure_traffic under rocprofv3's counter collection; nothing printed on stdout."""
+    from trpo_amd import synth
+    ctx, _, _ = make_ctx(ARM, N_TOTAL, _OneRank(), device)
+    ctx.upload_b(synth.make_b(num_params(ARM)))
+    for _ in range(5):
+        ctx.enqueue_cg(CG_ITERS, 0.0)
+    ctx.synchronize()
+    ctx.close()
+
+
+class _OneRank:
+    rank, world, local_rank = 0, 1, 0
+
+
+def measure_traffic(device):
+    """roofline.traffic measured in this run (N = 1): two child processes of this script (--pmc-child, the
+    headline workload) under rocprofv3, one counter per pass as MI355X_MICROARCH.md's HBM section
+    prescribes (FETCH_SIZE, then WRITE_SIZE, each in its own run, kernel dispatches serialised by the
+    profiler), each pass under its own hard time limit; per-launch HBM bytes of the CG-iteration kernel =
+    2 x median FETCH_SIZE (the gfx950 wide-read undercount) + median WRITE_SIZE, KiB -> bytes.  The
+    parent is idle meanwhile (after its timed region).  Returns (bytes, source) or (None, reason)."""
+    import csv
+    import shutil
+    import statistics
+    prof = shutil.which("rocprofv3") or ("/opt/rocm/bin/rocprofv3" if os.path.exists("/opt/rocm/bin/rocprofv3") else None)
+    if not prof:
+        return None, "rocprofv3 not found"
+    med = {}
+    with tempfile.TemporaryDirectory(prefix="trpo_pmc_") as tmp:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            out = os.path.join(tmp, counter)
+            cmd = ["timeout", "-s", "KILL", "90", prof, "--pmc", counter, "--output-format", "csv", "-d", out,
+                   "-o", "run", "--", sys.executable, os.path.abspath(__file__), "--pmc-child"]
+            env = dict(os.environ, TRPO_BENCH_DEVICE=str(device))
+            r = subprocess.run(cmd, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+            if r.returncode != 0:
+                return None, "rocprofv3 --pmc %s exited %d: %s" % (counter, r.returncode, r.stderr[-300:].strip())
+            files = [os.path.join(dp, fn) for dp, _, fns in os.walk(out) for fn in fns
+                     if fn.endswith("counter_collection.csv")]
+            if not files:
+                return None, "no counter_collection.csv from the %s pass" % counter
+            per = {}
+            for row in csv.DictReader(open(files[0])):
+                if PMC_KERNEL in row["Kernel_Name"] and row["Counter_Name"] == counter:
+                    per[row["Dispatch_Id"]] = per.get(row["Dispatch_Id"], 0.0) + float(row["Counter_Value"])
+            if not per:
+                return None, "no %s dispatches of %s" % (counter, PMC_KERNEL)
+            med[counter] = (statistics.median(per.values()), len(per))
+    fetch = 2.0 * med["FETCH_SIZE"][0] * 1024
+    write = med["WRITE_SIZE"][0] * 1024
+    return fetch + write, {"measured": "in this run", "fetch_bytes": fetch, "write_bytes": write,
+                           "dispatches": [med["FETCH_SIZE"][1], med["WRITE_SIZE"][1]],
+                           "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount) + WRITE_SIZE"}
+
+
 def main():
     args = parse_args()
+    if args.pmc_child:
+        sys.path[:0] = [os.path.join(ROOT, "trpo-robot-control_amd")]
+        pmc_child(int(os.environ.get("TRPO_BENCH_DEVICE", "0")))
+        return
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(relaunch(args))
     sys.path[:0] = [os.path.join(ROOT, "trpo-robot-control_amd"), os.path.join(ROOT, "oracle")]
@@ -710,12 +780,16 @@ def main():
     hbm_bound = bytes_alg / (PEAK_HBM_GBS * 1e9) >= flops / (PEAK_FP32_TFLOPS * 1e12)
 
     traffic, tsrc = None, None
-    tpath = os.environ.get("TRPO_TRAFFIC_JSON") or latest_traffic_json()
-    if tpath and os.path.exists(tpath) and dist.world == 1:
-        # HBM bytes per launch of this kernel at this workload, from the newest committed rocprofv3 PMC
-        # passes (tools/profile_round.sh: FETCH_SIZE x2 + WRITE_SIZE, separate passes)
-        traffic = json.load(open(tpath))["traffic_bytes"]
-        tsrc = os.path.relpath(tpath, ROOT)
+    if dist.world == 1 and not args.no_pmc and os.environ.get("TRPO_TRAFFIC_JSON") is None:
+        traffic, tsrc = measure_traffic(device)
+    if traffic is None and dist.world == 1:
+        # fallback: HBM bytes per launch of this kernel at this workload from the newest committed
+        # rocprofv3 PMC passes (tools/profile_round.sh: FETCH_SIZE x2 + WRITE_SIZE, separate passes)
+        why = tsrc
+        tpath = os.environ.get("TRPO_TRAFFIC_JSON") or latest_traffic_json()
+        if tpath and os.path.exists(tpath):
+            traffic = json.load(open(tpath))["traffic_bytes"]
+            tsrc = {"measured": "committed profile " + os.path.relpath(tpath, ROOT), "why_not_live": why}
 
     result = {
         "metric": "FVP samples/sec + 10-iter CG wall time, armDOF_0 policy",
