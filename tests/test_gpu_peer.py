@@ -93,6 +93,58 @@ def test_peer_cg_lockstep_and_golden(bounds):
     assert cases.rel_l2(x0, cases.expected(c)) <= CG_TOL
 
 
+@pytest.mark.parametrize("proto", ["0", "1", "2"])
+def test_peer_exchange_forms_agree(proto, monkeypatch):
+    """The three forms of the exchange kernel (TRPO_PEER_PROTO, read when the window is created):
+    0 the round-3 per-element loops, 1 the batched load rounds (default), 2 the flagless tagged
+    granules.  Same rank-order sums => the CG solve (the replica-set exchange of the CG graph) and a
+    standalone FVP (the in-place exchange) are bit-identical across the forms (checked against form 1
+    run here), on three ranks with ragged shards (slices that are not a multiple of the load round)."""
+    c = cases.case("syn_arm_cg_n50000")
+    x = cases.inputs(c)
+    bounds = [(0, 10000), (10000, 30001), (30001, 50000)]
+
+    def run(p):
+        monkeypatch.setenv("TRPO_PEER_PROTO", p)
+        ctxs = _shards(x, bounds)
+        try:
+            return run_peer_ranks(ctxs, lambda ctx, r: (ctx.cg(x["vin"], c["maxiter"], c["resth"]), ctx.fvp(x["vin"]),
+                                                        ctx.comm_info()["backend"]),
+                                  warm=lambda ctx: (ctx.cg(x["vin"], c["maxiter"], c["resth"]), ctx.fvp(x["vin"])))
+        finally:
+            for ctx in ctxs:
+                ctx.close()
+
+    ref = run("1")
+    got = run(proto)
+    for r in range(len(bounds)):
+        np.testing.assert_array_equal(got[r][0], ref[0][0])     # CG: lockstep and equal to form 1
+        np.testing.assert_array_equal(got[r][1], ref[0][1])     # standalone FVP (in-place exchange)
+        assert ("tagged granules" in got[r][2]) == (proto == "2"), got[r][2]
+    assert cases.rel_l2(got[0][0], cases.expected(c)) <= CG_TOL
+
+    # a long message: the 2x64 policy's FVP (P = 5 443 > one load round of 4 x 256 elements; slices
+    # of ~2 700 per rank > one round of 2 x 256) through the in-place exchange, vs one context
+    L2, n = [15, 64, 64, 3], 6000
+    th, obs, v = synth.make_theta(L2), synth.make_obs(n, L2[0]), synth.make_v(synth.num_params(L2))
+
+    def run2(p):
+        monkeypatch.setenv("TRPO_PEER_PROTO", p)
+        ctxs = [trpo_amd.Context(L2, "lttl", th, obs[lo:hi], np.ones(3), 0.1) for lo, hi in ((0, 2500), (2500, n))]
+        try:
+            return run_peer_ranks(ctxs, lambda ctx, r: ctx.fvp(v), warm=lambda ctx: ctx.fvp(v))
+        finally:
+            for ctx in ctxs:
+                ctx.close()
+
+    z1, zp = run2("1"), run2(proto)
+    with trpo_amd.Context(L2, "lttl", th, obs, np.ones(3), 0.1) as one:
+        zone = one.fvp(v)
+    for r in range(2):
+        np.testing.assert_array_equal(zp[r], z1[0])
+    assert cases.rel_l2(zp[0], zone) <= 1e-6
+
+
 def test_peer_matches_host_group():
     """The same shards through the host-staged group: the exchange only changes the summation order
     (per-rank replica sums first), so the steps agree to rounding."""
