@@ -2070,6 +2070,9 @@ __device__ __forceinline__ typename PT<T>::V dvec(const T *base, int g) {
     return v;
 }
 
+#ifndef TRPO_COOP_XT
+#define TRPO_COOP_XT 1
+#endif
 template <typename T, int T0, int TH>
 struct CoopCfg {
     static constexpr bool F64 = sizeof(T) == 8;
@@ -2078,12 +2081,16 @@ struct CoopCfg {
 #endif
     static constexpr int WAVES = F64 ? (TH > 1 ? 4 : TRPO_F64_TH1_WAVES) : 8;   // fp64 exchanges: twice the bytes
     static constexpr int GW = TH, NG = WAVES / GW, THREADS = 64 * WAVES;
+    // XT (fp32): the y1 and g2 exchange rows padded by one V after every 16 lanes (68 V per 64-lane row),
+    // so that RGW1 reads its operands TRANSPOSED straight from them, conflict-free (see the kernel)
+    static constexpr bool XT = !F64 && GW > 1 && TRPO_COOP_XT;
+    static constexpr int XR = XT ? 68 : 64;
     static constexpr int NW = T0 + TH + 4;                 // accumulator vectors per lane per wave
     static constexpr int SLAB = TH * NW * 256;             // T per block partial
     // LDS in V (4 x T) units: exchange buffers [parity][group][row tile][...][lane]
-    static constexpr int XB = 0, XB_N = GW > 1 ? 2 * NG * TH * 2 * 64 : 0;
+    static constexpr int XB = 0, XB_N = GW > 1 ? 2 * NG * TH * 2 * XR : 0;
     static constexpr int PB = XB + XB_N, PB_N = GW > 1 ? 2 * NG * TH * 2 * 64 : 0;
-    static constexpr int GB = PB + PB_N, GB_N = GW > 1 ? 2 * NG * TH * 64 : 0;
+    static constexpr int GB = PB + PB_N, GB_N = GW > 1 ? 2 * NG * TH * XR : 0;
     static constexpr int EX_V = GB + GB_N;
     static constexpr int SROWS = 16 * (TH + 1 > T0 + 1 ? TH + 1 : T0 + 1);   // per-wave transpose rows
     static constexpr int SCR = SROWS * SCR_LD;             // T per wave
@@ -2351,9 +2358,10 @@ fvp_coop_kernel(IterArgs A, Net net) {
         const int tc = min(tile, ntiles - 1);
         const bool live = tile < ntiles && tc * 16 + c < n;
         const int par = step & 1;
-        V *xb = LV + Q::XB + ((par * Q::NG + grp) * TH) * 128;     // [row tile][2][64]
+        V *xb = LV + Q::XB + ((par * Q::NG + grp) * TH) * 2 * Q::XR;   // [row tile][2][64 (+4 pad)]
         V *pb = LV + Q::PB + ((par * Q::NG + grp) * TH) * 128;
-        V *gb = LV + Q::GB + ((par * Q::NG + grp) * TH) * 64;
+        V *gb = LV + Q::GB + ((par * Q::NG + grp) * TH) * Q::XR;        // [row tile][64 (+4 pad)]
+        const int xl = Q::XT ? lane + (lane >> 4) : lane;               // this lane's V in such a row
         V x0[T0];
 #pragma unroll
         for (int kt = 0; kt < T0; ++kt) x0[kt] = xn[kt];
@@ -2394,13 +2402,13 @@ fvp_coop_kernel(IterArgs A, Net net) {
         }
         V y1[T1], r1[T1];
         if constexpr (Q::GW > 1) {
-            xb[w * 128 + lane] = y1w;
-            if constexpr (FV) xb[w * 128 + 64 + lane] = r1w;
+            xb[w * 2 * Q::XR + xl] = y1w;
+            if constexpr (FV) xb[w * 2 * Q::XR + Q::XR + xl] = r1w;
             __syncthreads();
 #pragma unroll
             for (int kt = 0; kt < T1; ++kt) {
-                y1[kt] = xb[kt * 128 + lane];
-                r1[kt] = FV ? xb[kt * 128 + 64 + lane] : zero4;
+                y1[kt] = xb[kt * 2 * Q::XR + xl];
+                r1[kt] = FV ? xb[kt * 2 * Q::XR + Q::XR + xl] : zero4;
             }
         } else {
             y1[0] = y1w;
@@ -2505,10 +2513,10 @@ fvp_coop_kernel(IterArgs A, Net net) {
         sB2 += g2w;
         V g2[T2];
         if constexpr (Q::GW > 1) {
-            gb[w * 64 + lane] = g2w;
+            gb[w * Q::XR + xl] = g2w;
             __syncthreads();
 #pragma unroll
-            for (int kt = 0; kt < T2; ++kt) g2[kt] = gb[kt * 64 + lane];
+            for (int kt = 0; kt < T2; ++kt) g2[kt] = gb[kt * Q::XR + xl];
         } else {
             g2[0] = g2w;
         }
@@ -2521,6 +2529,26 @@ fvp_coop_kernel(IterArgs A, Net net) {
         const V g1w = actv_bwd<T>(a1, y1w, t);
         sB1 += g1w;
         // ---- RGW1 tiles (at, w) += Y1_at . G2_w^T ----
+        if constexpr (Q::XT) {
+            // both operands read transposed from the exchange rows, which hold them in the D layout
+            // (lane l = sample + 16 (feature / 4), register feature % 4; +1 V per 16 lanes): lane (c, g)
+            // needs feature c of samples 4g .. 4g + 3, i.e. floats 4 (4g + s + 17 (c / 4)) + c % 4 of the
+            // row -- stride 4 floats in s (ds_read2_b32 pairs), banks 16g + 4 (c / 4) + c % 4 + 4s mod 64:
+            // all 64 lanes distinct.  Same products in the same order as the scratch transpose below.
+            const T *xbf = reinterpret_cast<const T *>(xb), *gbf = reinterpret_cast<const T *>(gb);
+            const int bt = 4 * (4 * g + 17 * (c >> 2)) + (c & 3);
+            V gg;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) gg[s] = gbf[w * 4 * Q::XR + bt + 4 * s];
+#pragma unroll
+            for (int at = 0; at < T1; ++at) {
+                V ya;
+#pragma unroll
+                for (int s = 0; s < 4; ++s) ya[s] = xbf[at * 8 * Q::XR + bt + 4 * s];
+#pragma unroll
+                for (int s = 0; s < 4; ++s) accW1[at] = PT<T>::mfma(ya[s], gg[s], accW1[at]);
+            }
+        } else {
 #pragma unroll
         for (int at = 0; at < T1; ++at) scr_put_t<T>(scr, 16 * at, y1[at], c, g);
         scr_put_t<T>(scr, 16 * T1, g2w, c, g);
@@ -2532,6 +2560,7 @@ fvp_coop_kernel(IterArgs A, Net net) {
 #pragma unroll
                 for (int s = 0; s < 4; ++s) accW1[at] = PT<T>::mfma(ya[s], gg[s], accW1[at]);
             }
+        }
         }
         // ---- RGW0 tiles (kt0, w) += X0_kt0 . G1_w^T ----
 #pragma unroll
