@@ -926,12 +926,34 @@ __device__ __forceinline__ int scr_off(int row, int chunk) {
     return row * SCR_LD3 + 4 * chunk;
 #endif
 }
+// TRPO_SCR_XT (round 4): the tile is stored as it is held -- ONE ds_write_b128 of the lane's D-layout
+// registers at V index lane + lane / 16 (a 4-float pad after every 16 lanes; 272 of the 320 floats a
+// tile slot has) -- and read transposed: lane (c, g) takes feature c of samples 4g .. 4g + 3 from
+// floats 4 (4g + 17 (c / 4)) + c % 4 + 4s of the slot (two ds_read2_b32; banks 16g + 4 (c / 4) +
+// c % 4 + 4s mod 64, distinct over the 64 lanes).  5 LDS instructions per transpose -> 3.
+#ifndef TRPO_SCR_XT
+#define TRPO_SCR_XT 1
+#endif
 __device__ __forceinline__ void scr_put(float *scr, int row0, f4 t, int c, int g) {
+#if TRPO_SCR_XT
+    reinterpret_cast<f4 *>(scr)[(row0 >> 4) * 68 + c + 17 * g] = t;
+#else
 #pragma unroll
     for (int r = 0; r < 4; ++r) scr[scr_off(row0 + 4 * g + r, c >> 2) + (c & 3)] = t[r];
+#endif
 }
 __device__ __forceinline__ f4 scr_get(const float *scr, int row0, int c, int g) {
+#if TRPO_SCR_XT
+    const float *p = scr + (row0 >> 4) * 272 + 4 * (4 * g + 17 * (c >> 2)) + (c & 3);
+    f4 r;
+    r[0] = p[0];
+    r[1] = p[4];
+    r[2] = p[8];
+    r[3] = p[12];
+    return r;
+#else
     return *reinterpret_cast<const f4 *>(scr + scr_off(row0 + c, g));
+#endif
 }
 
 // ACT >= 0: activations of layers 1..3 fixed at compile time (a1 | a2 << 2 | a3 << 4);
