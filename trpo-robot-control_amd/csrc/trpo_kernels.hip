@@ -2076,12 +2076,26 @@ __device__ __forceinline__ V actv_bwd(int a, V y, V g) {
 }
 template <typename T>
 __device__ __forceinline__ void scr_put_t(T *scr, int row0, typename PT<T>::V t, int c, int g) {
+    if constexpr (sizeof(T) == 4 && TRPO_SCR_XT) {      // fp32: the scr_put form (one 16-byte store)
+        reinterpret_cast<typename PT<T>::V *>(scr)[(row0 >> 4) * 68 + c + 17 * g] = t;
+    } else {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) scr[(row0 + PT<T>::neu(g, r)) * SCR_LD + c] = t[r];
+        for (int r = 0; r < 4; ++r) scr[(row0 + PT<T>::neu(g, r)) * SCR_LD + c] = t[r];
+    }
 }
 template <typename T>
 __device__ __forceinline__ typename PT<T>::V scr_get_t(const T *scr, int row0, int c, int g) {
-    return *reinterpret_cast<const typename PT<T>::V *>(scr + (row0 + c) * SCR_LD + 4 * g);
+    if constexpr (sizeof(T) == 4 && TRPO_SCR_XT) {      // fp32: the scr_get form (transposed reads)
+        const T *p = scr + (row0 >> 4) * 272 + 4 * (4 * g + 17 * (c >> 2)) + (c & 3);
+        typename PT<T>::V r;
+        r[0] = p[0];
+        r[1] = p[4];
+        r[2] = p[8];
+        r[3] = p[12];
+        return r;
+    } else {
+        return *reinterpret_cast<const typename PT<T>::V *>(scr + (row0 + c) * SCR_LD + 4 * g);
+    }
 }
 // a D-layout vector of natural-order values (biases, 1/sigma^2): lane group g, register r -> neu(g, r)
 template <typename T>
