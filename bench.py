@@ -790,7 +790,7 @@ def main():
         tpath = os.environ.get("TRPO_TRAFFIC_JSON") or latest_traffic_json()
         if tpath and os.path.exists(tpath):
             traffic = json.load(open(tpath))["traffic_bytes"]
-            tsrc = {"measured": "committed profile " + os.path.relpath(tpath, ROOT), "why_not_live": why}
+            tsrc = {"measured": "profile file " + os.path.relpath(tpath, ROOT), "why_not_live": why}
 
     result = {
         "metric": "FVP samples/sec + 10-iter CG wall time, armDOF_0 policy",
