@@ -688,7 +688,11 @@ def measure_traffic(device):
             cmd = ["timeout", "-s", "KILL", "90", prof, "--pmc", counter, "--output-format", "csv", "-d", out,
                    "-o", "run", "--", sys.executable, os.path.abspath(__file__), "--pmc-child"]
             env = dict(os.environ, TRPO_BENCH_DEVICE=str(device))
-            r = subprocess.run(cmd, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+            try:
+                r = subprocess.run(cmd, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
+                                   timeout=120)
+            except (OSError, subprocess.SubprocessError) as e:      # no `timeout` binary, a stuck child, ...
+                return None, "rocprofv3 --pmc %s: %s: %s" % (counter, type(e).__name__, e)
             if r.returncode != 0:
                 return None, "rocprofv3 --pmc %s exited %d: %s" % (counter, r.returncode, r.stderr[-300:].strip())
             files = [os.path.join(dp, fn) for dp, _, fns in os.walk(out) for fn in fns
