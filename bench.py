@@ -668,6 +668,19 @@ class _OneRank:
     rank, world, local_rank = 0, 1, 0
 
 
+def pmc_median(path, counter, kernel=PMC_KERNEL):
+    """(median over dispatches of `kernel` of the counter's per-dispatch total, dispatch count) from a
+    rocprofv3 counter_collection.csv (one row per counter instance), or None if no dispatch matched."""
+    import csv
+    import statistics
+    per = {}
+    with open(path) as fh:
+        for row in csv.DictReader(fh):
+            if kernel in row["Kernel_Name"] and row["Counter_Name"] == counter:
+                per[row["Dispatch_Id"]] = per.get(row["Dispatch_Id"], 0.0) + float(row["Counter_Value"])
+    return (statistics.median(per.values()), len(per)) if per else None
+
+
 def measure_traffic(device):
     """roofline.traffic measured in this run (N = 1): two child processes of this script (--pmc-child, the
     headline workload) under rocprofv3, one counter per pass as MI355X_MICROARCH.md's HBM section
@@ -675,9 +688,7 @@ def measure_traffic(device):
     profiler), each pass under its own hard time limit; per-launch HBM bytes of the CG-iteration kernel =
     2 x median FETCH_SIZE (the gfx950 wide-read undercount) + median WRITE_SIZE, KiB -> bytes.  The
     parent is idle meanwhile (after its timed region).  Returns (bytes, source) or (None, reason)."""
-    import csv
     import shutil
-    import statistics
     prof = shutil.which("rocprofv3") or ("/opt/rocm/bin/rocprofv3" if os.path.exists("/opt/rocm/bin/rocprofv3") else None)
     if not prof:
         return None, "rocprofv3 not found"
@@ -699,13 +710,10 @@ def measure_traffic(device):
                      if fn.endswith("counter_collection.csv")]
             if not files:
                 return None, "no counter_collection.csv from the %s pass" % counter
-            per = {}
-            for row in csv.DictReader(open(files[0])):
-                if PMC_KERNEL in row["Kernel_Name"] and row["Counter_Name"] == counter:
-                    per[row["Dispatch_Id"]] = per.get(row["Dispatch_Id"], 0.0) + float(row["Counter_Value"])
-            if not per:
+            m = pmc_median(files[0], counter)
+            if m is None:
                 return None, "no %s dispatches of %s" % (counter, PMC_KERNEL)
-            med[counter] = (statistics.median(per.values()), len(per))
+            med[counter] = m
     fetch = 2.0 * med["FETCH_SIZE"][0] * 1024
     write = med["WRITE_SIZE"][0] * 1024
     return fetch + write, {"measured": "in this run", "fetch_bytes": fetch, "write_bytes": write,

@@ -229,3 +229,29 @@ def test_headline_exits_when_no_collective_passes(monkeypatch):
     import pytest
     with pytest.raises(SystemExit):
         _agreed(monkeypatch, local_fails={(0, "attach"), (1, "attach"), (2, "attach")})
+
+
+def test_pmc_median_per_dispatch(tmp_path):
+    """roofline.traffic's parser (bench.pmc_median): per-dispatch totals over counter instances, the
+    median over the CG-iteration kernel's dispatches only; None when no dispatch matches."""
+    import bench
+    p = tmp_path / "run_counter_collection.csv"
+    rows = ["Dispatch_Id,Kernel_Name,Counter_Name,Counter_Value"]
+    k3 = "void fvp_mlp3_kernel<1, 1, 1, 1, 5, 3, 4, 11>(double const*)"
+    for d, vals in ((1, (100.0, 20.0)), (2, (110.0, 20.0)), (3, (500.0, 0.0))):
+        for v in vals:
+            rows.append('%d,"%s",FETCH_SIZE,%s' % (d, k3 if d < 3 else "cg_last_kernel(double const*)", v))
+    rows.append('4,"%s",WRITE_SIZE,7.0' % k3)
+    p.write_text("\n".join(rows) + "\n")
+    assert bench.pmc_median(str(p), "FETCH_SIZE") == (125.0, 2)
+    assert bench.pmc_median(str(p), "WRITE_SIZE") == (7.0, 1)
+    assert bench.pmc_median(str(p), "FETCH_SIZE", kernel="no such kernel") is None
+
+
+def test_measure_traffic_without_profiler(monkeypatch):
+    """No rocprofv3 on the host: measure_traffic reports why and the bench falls back (no exception)."""
+    import shutil
+    import bench
+    monkeypatch.setattr(shutil, "which", lambda name: None)
+    monkeypatch.setattr(bench.os.path, "exists", lambda p: False)
+    assert bench.measure_traffic(0) == (None, "rocprofv3 not found")
