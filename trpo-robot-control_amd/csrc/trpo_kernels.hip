@@ -2365,6 +2365,47 @@ fvp_coop_kernel(IterArgs A, Net net) {
             vb1w[s] = vget(C::VB1 + 16 * w + PT<T>::neu(g, s));
             vb2[s] = vget(C::VB2 + PT<T>::neu(g2, s));
         }
+        if (A.init && blockIdx.x == gridDim.x - 1) {
+            // the CG start of the distributed path fused into its first FVP (v_nat = b): the block
+            // with the fewest tiles writes x = 0, r = p = b, |b|^2, q_0 = b / |b| and the control state
+            // (cg_init_kernel's work, src/TRPO_CG.c:19-43), so the solve needs no init launch
+            #pragma clang fp contract(off)
+            constexpr int EP = (Q::PMAX + Q::THREADS - 1) / Q::THREADS;
+            double bv[EP], red[1] = {0.0};
+#pragma unroll
+            for (int e = 0; e < EP; ++e) {
+                const int q = tid + e * Q::THREADS;
+                const double b0 = A.b_init[min(q, A.P - 1)];
+                bv[e] = q < A.P ? b0 : 0.0;
+                red[0] += bv[e] * bv[e];
+            }
+            block_sums_dpp<1, Q::THREADS / 64>(red, reinterpret_cast<double *>(lds));
+            const double rr = red[0];
+#pragma unroll
+            for (int e = 0; e < EP; ++e) {
+                const int q = tid + e * Q::THREADS;
+                if (q < A.P) {
+                    A.p_out[q] = bv[e];
+                    A.r_out[q] = bv[e];
+                    A.x[q] = 0.0;
+                }
+            }
+            if (A.reorth) qstore<EP>((T *)A.q, A.P, A.Ps, 0, rr, bv, Q::THREADS);     // q_0 = b / |b|
+            if (tid == 0) {
+                A.st_out->rdotr = rr;
+                A.st_out->xx = 0.0;
+                A.st_out->iter = 0;
+                A.hist[0] = rr;
+                A.hist[1] = 0.0;
+                A.ctl->maxiter = A.init_maxiter;
+                A.ctl->resth = A.init_resth;
+                A.ctl->rdotr = rr;
+                A.ctl->iter = 0;
+                A.ctl->orth = 0.0;
+                A.ctl->done = (rr < A.init_resth || A.init_maxiter == 0) ? 1 : 0;
+            }
+            __syncthreads();                               // the LDS scratch goes back to the tiles
+        }
     } else {
 #pragma unroll
         for (int kt = 0; kt < T0; ++kt) vfa0[kt] = FV ? VP[C::VFA0 / 4 + (w * T0 + kt) * 64 + lane] : zero4;
@@ -3542,6 +3583,7 @@ struct trpo_dev {
     int coop;
     int coop_fused;             // CG step fused into the cooperative FVP kernel (MODE 2)
     int coop_dist;              // cooperative path: the CG step over slices (cg_dots / cg_axpy), TRPO_COOP_DIST
+    int cinit;                  // its CG start inside the first FVP launch (TRPO_COOP_CINIT, default 1)
     double *zbuf, *dotsbuf;     // its z (natural order, Ps) and per-block partial dots
     fast_launch_fn k_fvp, k_pg; // the tile kernel serving this shape, FVP and policy-gradient modes
     fast_launch_fn k_fvp_yc, k_cg_yc;   // the same kernel on the forward cache: standalone FVP, CG iteration
@@ -4006,6 +4048,8 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
             // mode keeps the fused cooperative step with its direct |r'|^2 reduction
             const char *ed = getenv("TRPO_COOP_DIST");
             d->coop_dist = !d->f64 && !(ed && atoi(ed) == 0);
+            const char *eci = getenv("TRPO_COOP_CINIT");
+            d->cinit = !(eci && atoi(eci) == 0);
             DMALLOC(d->zbuf, sizeof(double) * d->Ps);
             DMALLOC(d->dotsbuf, sizeof(double) * CGS_K * cdiv(d->Ps / 2, CGS_T));
             DMALLOC(d->imap, sizeof(int) * d->slab);
@@ -5008,7 +5052,7 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
     // the one-wave-per-tile kernel runs the CG start inside K_0 (IterArgs::init): no init launch.
     // Its atomic target acc_slot(0) is zero on entry: zeroed at allocation and by every solve's
     // final cg_update
-    const bool fused_init = d->fast && !d->coop && M > 0;
+    const bool fused_init = d->fast && M > 0 && (!d->coop || (d->coop_dist && d->cinit));
     if (!fused_init)
         CG_DISPATCH(E, cg_init_kernel, dim3(1), dim3(1024), shm, d->stream, b, x, d->rbuf[0], d->pbuf[0], d->P,
                     d->ctl, d->st, d->hist, (int)maxiter, resth, d->vmap, d->vpack, vlen, d->f64,
@@ -5098,6 +5142,21 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
             // forward-activation cache that trpo_dev_ycache_written() then marks valid
             IterArgs a = plain_args(d, j == 0 ? &d->ctl->zero : done);
             a.v_nat = d->pbuf[cur];
+            if (j == 0 && fused_init) {                    // the CG start inside K_0 (v = p_0 = b)
+                a.v_nat = b;
+                a.init = 1;
+                a.b_init = b;
+                a.init_maxiter = (int)maxiter;
+                a.init_resth = resth;
+                a.p_out = d->pbuf[0];
+                a.r_out = d->rbuf[0];
+                a.x = x;
+                a.st_out = d->st;
+                a.ctl = d->ctl;
+                a.hist = d->hist;
+                a.reorth = d->reorth;
+                a.q = d->reorth ? d->qbuf : nullptr;
+            }
             if (d->yc_on) a.yc = reinterpret_cast<float4 *>(d->yc);
             (j > 0 && d->yc_on ? d->k_fvp_yc : d->k_fvp)(dim3(d->grid), d->k_lds, d->stream, a, d->net);
             const int nq = cg_step_nq(d, j);
