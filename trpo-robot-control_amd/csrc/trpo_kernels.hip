@@ -3583,7 +3583,7 @@ struct trpo_dev {
     int coop;
     int coop_fused;             // CG step fused into the cooperative FVP kernel (MODE 2)
     int coop_dist;              // cooperative path: the CG step over slices (cg_dots / cg_axpy), TRPO_COOP_DIST
-    int cinit;                  // its CG start inside the first FVP launch (TRPO_COOP_CINIT, default 1)
+    int cinit;                  // cooperative CG start inside the first FVP launch (TRPO_COOP_CINIT, default 1)
     double *zbuf, *dotsbuf;     // its z (natural order, Ps) and per-block partial dots
     fast_launch_fn k_fvp, k_pg; // the tile kernel serving this shape, FVP and policy-gradient modes
     fast_launch_fn k_fvp_yc, k_cg_yc;   // the same kernel on the forward cache: standalone FVP, CG iteration
@@ -4049,7 +4049,7 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
             const char *ed = getenv("TRPO_COOP_DIST");
             d->coop_dist = !d->f64 && !(ed && atoi(ed) == 0);
             const char *eci = getenv("TRPO_COOP_CINIT");
-            d->cinit = !(eci && atoi(eci) == 0);
+            d->cinit = !(eci && atoi(eci) == 0);         // (read for both cooperative CG forms)
             DMALLOC(d->zbuf, sizeof(double) * d->Ps);
             DMALLOC(d->dotsbuf, sizeof(double) * CGS_K * cdiv(d->Ps / 2, CGS_T));
             DMALLOC(d->imap, sizeof(int) * d->slab);
@@ -5052,7 +5052,7 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
     // the one-wave-per-tile kernel runs the CG start inside K_0 (IterArgs::init): no init launch.
     // Its atomic target acc_slot(0) is zero on entry: zeroed at allocation and by every solve's
     // final cg_update
-    const bool fused_init = d->fast && M > 0 && (!d->coop || (d->coop_dist && d->cinit));
+    const bool fused_init = d->fast && M > 0 && (!d->coop || ((d->coop_dist || d->coop_fused) && d->cinit));
     if (!fused_init)
         CG_DISPATCH(E, cg_init_kernel, dim3(1), dim3(1024), shm, d->stream, b, x, d->rbuf[0], d->pbuf[0], d->P,
                     d->ctl, d->st, d->hist, (int)maxiter, resth, d->vmap, d->vpack, vlen, d->f64,
@@ -5188,6 +5188,21 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
         for (long j = 0; j < M; ++j) {
             // K_0 is never skipped (see the distributed path above): it refreshes the cache
             IterArgs a = plain_args(d, j == 0 ? &d->ctl->zero : done);
+            if (j == 0 && fused_init) {                    // the CG start inside K_0 (v = p_0 = b)
+                a.v_nat = b;
+                a.init = 1;
+                a.b_init = b;
+                a.init_maxiter = (int)maxiter;
+                a.init_resth = resth;
+                a.p_out = d->pbuf[0];
+                a.r_out = d->rbuf[0];
+                a.x = x;
+                a.st_out = d->st;
+                a.ctl = d->ctl;
+                a.hist = d->hist;
+                a.reorth = d->reorth;
+                a.q = d->reorth ? d->qbuf : nullptr;
+            }
             if (j > 0) {
                 const int in = (int)((j - 1) & 1), out = (int)(j & 1);
                 a.update = 1;
