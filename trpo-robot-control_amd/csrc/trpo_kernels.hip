@@ -930,7 +930,8 @@ __device__ __forceinline__ int scr_off(int row, int chunk) {
 // registers at V index lane + lane / 16 (a 4-float pad after every 16 lanes; 272 of the 320 floats a
 // tile slot has) -- and read transposed: lane (c, g) takes feature c of samples 4g .. 4g + 3 from
 // floats 4 (4g + 17 (c / 4)) + c % 4 + 4s of the slot (two ds_read2_b32; banks 16g + 4 (c / 4) +
-// c % 4 + 4s mod 64, distinct over the 64 lanes).  5 LDS instructions per transpose -> 3.
+// c % 4 + 4s mod 64, distinct over the 64 lanes).  hipcc issues the reads as four ds_read_b32 here (not
+// ds_read2_b32: the constant part of the slot address exceeds its 8-bit offsets), so the count stays 5.
 #ifndef TRPO_SCR_XT
 #define TRPO_SCR_XT 1
 #endif
