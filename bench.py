@@ -15,10 +15,12 @@ P-sized partial sum over RCCL (strong scaling, config C4).
 
 Rank 0 prints ONE JSON line.  value = 10 * 50 000 / (seconds per solve), the
 whole-job FVP throughput; ms_per_step = the CG wall time (max over ranks).
-Measured in this order: the secondary configs (extra), the dominant kernel's HIP-event timing
-(roofline), then the headline's timed region (W untimed solves, exactly K timed ones).  At N > 1
-the headline's collective is set up stage by stage with cross-rank agreement, self-checked and
-hash-checked before anything is timed (make_ctx_agreed; comm.verify / comm.fallback in the line).
+Measured in this order at N = 1: the secondary configs (extra), the dominant kernel's HIP-event
+timing (roofline), then the headline's timed region (W untimed solves, exactly K timed ones).  At
+N > 1 the headline's collective is set up stage by stage with cross-rank agreement, self-checked and
+hash-checked before anything is timed (make_ctx_agreed; comm.verify / comm.fallback in the line), the
+headline is timed right after, and the secondary configs follow, each set up and run the same agreed
+way; a watchdog prints the line by a deadline whatever they do (Emitter).
 At N = 1, after the timed region, roofline.traffic is measured in the same run: two rocprofv3 PMC
 passes (FETCH_SIZE, WRITE_SIZE, one per child process of this script on the headline workload;
 measure_traffic); --no-pmc, or a failed pass, falls back to the newest committed profile.
@@ -112,30 +114,46 @@ class Dist:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.group = None           # the group every collective below uses (None: the default group)
+        self.broken = False         # a gloo collective raised: the ranks may be out of step, no more of them
         if self.world > 1:
             import datetime
             import torch.distributed as dist
-            # every rendezvous / agreement is bounded: a rank that dies makes the others raise, not hang
+            # every rendezvous / agreement is bounded: a rank that dies makes the others raise, not hang.
+            # The headline's setup and timed region use the default group (TRPO_GLOO_TIMEOUT_S); the
+            # secondary configs measured after it use a group with a shorter bound, so that their worst
+            # case (one rank stuck) ends well inside the driver's lease
             dist.init_process_group("gloo", timeout=datetime.timedelta(
                 seconds=int(os.environ.get("TRPO_GLOO_TIMEOUT_S", "600"))))
             self.dist = dist
+            self.secondary_group = dist.new_group(backend="gloo", timeout=datetime.timedelta(
+                seconds=int(os.environ.get("TRPO_GLOO_SECONDARY_TIMEOUT_S", "90"))))
+
+    def _coll(self, fn):
+        if self.broken:
+            raise RuntimeError("an earlier gloo collective failed; the ranks may be out of step")
+        try:
+            return fn()
+        except Exception:
+            self.broken = True
+            raise
 
     def barrier(self):
         if self.world > 1:
-            self.dist.barrier()
+            self._coll(lambda: self.dist.barrier(group=self.group))
 
     def bcast_bytes(self, b):
         if self.world == 1:
             return b
         obj = [b]
-        self.dist.broadcast_object_list(obj, src=0)
+        self._coll(lambda: self.dist.broadcast_object_list(obj, src=0, group=self.group))
         return obj[0]
 
     def allgather_bytes(self, b):
         if self.world == 1:
             return [b]
         out = [None] * self.world
-        self.dist.all_gather_object(out, b)
+        self._coll(lambda: self.dist.all_gather_object(out, b, group=self.group))
         return out
 
     def max(self, x: float) -> float:
@@ -143,11 +161,26 @@ class Dist:
             return x
         import torch
         t = torch.tensor([x], dtype=torch.float64)
-        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        self._coll(lambda: self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group))
         return float(t.item())
 
+    def secondary(self):
+        """Context manager: the collectives inside use the secondary group (shorter gloo bound)."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def cm():
+            saved = self.group
+            if self.world > 1:
+                self.group = self.secondary_group
+            try:
+                yield self
+            finally:
+                self.group = saved
+        return cm()
+
     def close(self):
-        if self.world > 1:
+        if self.world > 1 and not self.broken:
             self.dist.destroy_process_group()
 
 
@@ -189,14 +222,33 @@ class StageFault(RuntimeError):
 
 
 def _fault(stage, rank, attempt):
-    """TRPO_BENCH_FAULT=<stage>:<rank>[:<attempt>] (testing): make `stage` fail on `rank` in attempt
-    `attempt` (default 0) of the headline's collective setup.  Stages: STAGES, plus comm-verify /
-    comm-hang, which arm the LIBRARY's self-check fault (TRPO_COMM_FAULT) for that attempt."""
+    """TRPO_BENCH_FAULT=<stage>:<rank>[:<attempt>][,...] (testing): make `stage` fail on `rank` in attempt
+    `attempt` (default 0).  Stages of the headline's collective setup: STAGES, plus comm-verify /
+    comm-hang, which arm the LIBRARY's self-check fault (TRPO_COMM_FAULT) for that attempt.  The
+    secondary configs at N > 1 prefix their stages with their name (`sweep4000000.context:1`,
+    `update.solve:1`, `sweep500000.timed:1`, ...; see run_secondary); `<name>.hang:R` makes rank R block
+    forever inside that secondary (a library call that ignores its bound: the watchdog's case)."""
     spec = os.environ.get("TRPO_BENCH_FAULT", "")
-    if not spec:
-        return False
-    f = spec.split(":")
-    return f[0] == stage and int(f[1]) == rank and (int(f[2]) if len(f) > 2 else 0) == attempt
+    for one in filter(None, spec.split(",")):
+        f = one.split(":")
+        if f[0] == stage and int(f[1]) == rank and (int(f[2]) if len(f) > 2 else 0) == attempt:
+            return True
+    return False
+
+
+def agreed(dist, what, fn):
+    """Run fn() on every rank, then agree (over gloo) that it succeeded everywhere: a failure on any one
+    rank raises StageFault on all of them, so no rank enters the next collective alone."""
+    err, out = None, None
+    try:
+        if _fault(what, dist.rank, 0):
+            raise StageFault("injected fault (TRPO_BENCH_FAULT)")
+        out = fn()
+    except Exception as e:              # noqa: BLE001 -- agreed below, every rank moves on together
+        err = "%s: %s" % (type(e).__name__, e)
+    if dist.max(0.0 if err is None else 1.0) != 0.0:
+        raise StageFault(err or "another rank failed at %s" % what)
+    return out
 
 
 def x_digest(x):
@@ -205,7 +257,7 @@ def x_digest(x):
     return hashlib.sha256(np.ascontiguousarray(x, np.float64).tobytes()).hexdigest()[:16]
 
 
-def make_ctx_agreed(L, n_total, dist, device, comm, b, plan=None):
+def make_ctx_agreed(L, n_total, dist, device, comm, b, plan=None, tag=None):
     """The headline context at N > 1, set up stage by stage with the ranks agreeing (over gloo) after
     EVERY stage, so a failure on one rank alone never leaves the others in a mismatched collective:
       context   create this rank's context (its shard)
@@ -218,8 +270,10 @@ def make_ctx_agreed(L, n_total, dist, device, comm, b, plan=None):
       hash      x from every rank: identical bits (sha256 all-gathered)
     On a failure anywhere every rank aborts its collective (ncclCommAbort / the peer error flag), closes
     its context and moves to the next backend of `plan` (default: the requested one, the other, the
-    requested one again); SystemExit when none passes.
+    requested one again); SystemExit when none passes.  tag: a secondary config's name, prefixed to the
+    stage names of TRPO_BENCH_FAULT (`<tag>.<stage>`).
     Returns (ctx, theta, obs, backend, record) -- record = {"verify": ..., "fallback": [...] or None}."""
+    pre = tag + "." if tag else ""
     import numpy as np
     import trpo_amd
     from trpo_amd import synth
@@ -230,7 +284,7 @@ def make_ctx_agreed(L, n_total, dist, device, comm, b, plan=None):
         ctx, stage, err, attached, digest = None, None, None, False, None
         lib_fault = None
         for kind in ("comm-verify", "comm-hang"):
-            if _fault(kind, dist.rank, attempt):
+            if _fault(pre + kind, dist.rank, attempt):
                 lib_fault = "%s:%d" % (kind.split("-")[1], dist.rank)
         saved = os.environ.pop("TRPO_COMM_FAULT", None)
         if lib_fault:
@@ -239,7 +293,7 @@ def make_ctx_agreed(L, n_total, dist, device, comm, b, plan=None):
         try:
             for stage in STAGES:
                 try:
-                    if _fault(stage, dist.rank, attempt):
+                    if _fault(pre + stage, dist.rank, attempt):
                         raise StageFault("injected fault (TRPO_BENCH_FAULT)")
                     if stage == "context":
                         theta = synth.make_theta(L)
@@ -274,7 +328,7 @@ def make_ctx_agreed(L, n_total, dist, device, comm, b, plan=None):
                     boot = dist.allgather_bytes(boot) if c == "peer" else dist.bcast_bytes(boot)
                 elif stage == "hash":
                     digests = dist.allgather_bytes(digest.encode())
-                    if len(set(digests)) != 1 or _fault("hash-mismatch", dist.rank, attempt):
+                    if len(set(digests)) != 1 or _fault(pre + "hash-mismatch", dist.rank, attempt):
                         err = "x differs across ranks: %s" % sorted(set(d.decode() for d in digests))
                     if dist.max(0.0 if err is None else 1.0) != 0.0:
                         raise StageFault(err or "another rank saw differing x")
@@ -297,22 +351,38 @@ def make_ctx_agreed(L, n_total, dist, device, comm, b, plan=None):
     raise SystemExit("bench.py: no collective passed setup and self-check: %s" % failed)
 
 
-def time_steps(ctx, dist, steps, warmup, b):
+def time_steps(ctx, dist, steps, warmup, b, tag="headline"):
     """K timed solves after W warm-up ones, bracketed by barrier + completion on both sides; the wait
-    is bounded at N > 1 (trpo_ctx_wait spins on the stream, so it costs what a synchronize costs)."""
+    is bounded at N > 1 (trpo_ctx_wait polls the stream, so it costs what a synchronize costs).  The
+    barriers are agreements (`agreed`): a rank whose solves fail or time out makes every rank raise
+    StageFault together instead of leaving the others in a mismatched collective."""
     wait = ctx.synchronize if dist.world == 1 else (lambda: ctx.wait(COMM_TIMEOUT_MS))
-    ctx.upload_b(b)
-    for _ in range(warmup):
-        ctx.enqueue_cg(CG_ITERS, 0.0)
-    wait()
-    dist.barrier()
+
+    def warm():
+        ctx.upload_b(b)
+        for _ in range(warmup):
+            ctx.enqueue_cg(CG_ITERS, 0.0)
+        wait()
+
+    agreed(dist, tag + ".warmup", warm)               # the barrier in front of the timed region
+    err = None
     t0 = time.perf_counter()
-    for _ in range(steps):
-        ctx.enqueue_cg(CG_ITERS, 0.0)
-    wait()
+    try:
+        if _fault(tag + ".timed", dist.rank, 0):
+            raise StageFault("injected fault (TRPO_BENCH_FAULT)")
+        for _ in range(steps):
+            ctx.enqueue_cg(CG_ITERS, 0.0)
+        wait()
+    except Exception as e:              # noqa: BLE001 -- agreed below
+        err = "%s: %s" % (type(e).__name__, e)
     t1 = time.perf_counter()
-    dist.barrier()
+    agreed(dist, tag + ".timed-check", lambda: _raise(err))   # the barrier behind it
     return dist.max(t1 - t0)
+
+
+def _raise(err):
+    if err is not None:
+        raise StageFault(err)
 
 
 def _cpu_model():
@@ -466,8 +536,8 @@ def bench_baseline(device, num_ep=20, ep_len=150, reps=50):
         for _ in range(reps):
             f, g = b.evaluate(x)
         dev = (time.perf_counter() - t0) / reps
-        # the whole baseline fit a trainer runs per iteration: L-BFGS (scipy's L-BFGS-B standing in for
-        # the caller's liblbfgs, at most 25 iterations) driving the device objective
+        # a baseline fit under a second driver, scipy's L-BFGS-B (at most 25 iterations) on the device
+        # objective; the fit a trainer runs -- the caller's liblbfgs -- is caller_lbfgs_fit below
         fits = []
         for _ in range(3):
             t0 = time.perf_counter()
@@ -483,162 +553,255 @@ def bench_baseline(device, num_ep=20, ep_len=150, reps=50):
     return {"evaluate_us": 1e6 * dev, "cpu_port_evaluate_us_1core": 1e6 * cpu, "samples": num_ep * ep_len,
             "grad_relL2_vs_cpu": float(np.linalg.norm(g - go) / np.linalg.norm(go)),
             "what": "host-visible wall per L-BFGS callback incl. x upload and g/f download",
-            "lbfgs_fit25_ms": 1e3 * sorted(fits)[1], "lbfgs_fit25_evals": int(info["funcalls"]),
-            "cpu_port_lbfgs_fit25_ms_1core": 1e3 * cpu_fit,
-            "fit_x_relL2_vs_cpu_fit": float(np.linalg.norm(xd - xo) / np.linalg.norm(xo))}
+            "scipy_lbfgsb_fit25_ms": 1e3 * sorted(fits)[1], "scipy_lbfgsb_fit25_evals": int(info["funcalls"]),
+            "cpu_port_scipy_lbfgsb_fit25_ms_1core": 1e3 * cpu_fit,
+            "scipy_fit_x_relL2_vs_cpu_fit": float(np.linalg.norm(xd - xo) / np.linalg.norm(xo)),
+            "caller_liblbfgs_fit": caller_lbfgs_fit(device)}
 
 
-def extras_single(device, dist, reps):
-    """Secondary configs at N=1 (SURVEY §8d C2, C3 for the 2x64 MLP, the fp64 mode, C5)."""
+def caller_lbfgs_fit(device, reps=5):
+    """The baseline fit with the CALLER's optimiser (liblbfgs 1.10, src/lbfgs.c, as
+    src/TRPO_Lightweight.c:676 calls it) on the device evaluate, and on the reference's CPU evaluate
+    beside it: tests/lbfgs_fit_child.py (test infrastructure, like the CPU baseline) in a child process,
+    which also checks that both fits end at the same point.  None where oracle/_ref is not built."""
+    child = os.path.join(ROOT, "tests", "lbfgs_fit_child.py")
+    if not os.path.exists(os.path.join(ROOT, "oracle", "_ref", "libref_lbfgs.so")):
+        return {"error": "oracle/_ref/libref_lbfgs.so not built (make -C oracle ref)"}
+    env = dict(os.environ, HIP_VISIBLE_DEVICES=os.environ.get("HIP_VISIBLE_DEVICES", str(device)))
+    p = subprocess.run([sys.executable, child, str(reps)], capture_output=True, text=True, timeout=180, env=env)
+    if p.returncode != 0:
+        return {"error": "lbfgs_fit_child exited %d: %s" % (p.returncode, p.stderr[-400:])}
+    return json.loads(p.stdout.strip().splitlines()[-1])
+
+
+def c5_iteration(u, bl):
+    """One training iteration's learning step: TRPO_Update + the baseline fit by the caller's liblbfgs
+    (the trainer's own optimiser; scipy's L-BFGS-B fit is reported in the baseline row only)."""
+    fit = bl.get("caller_liblbfgs_fit") or {}
+    if "device_evaluate_fit_ms" not in fit:
+        return {"error": "no caller-liblbfgs fit timing: %s" % fit.get("error")}
+    cpu_u = u.get("cpu_reference_compute_s_1core")
+    return {"device_ms": u["update_ms"] + fit["device_evaluate_fit_ms"],
+            "cpu_reference_ms_1core": (1e3 * cpu_u + fit["reference_cpu_evaluate_fit_ms_1core"]
+                                       if cpu_u is not None else None),
+            "what": "TRPO_Update (N=50000, device) + the value-baseline fit by the caller's liblbfgs 1.10 "
+                    "(max 25 iterations, 20x150 batch) on the device evaluate; CPU: the reference's "
+                    "TRPO_Update + the same liblbfgs on the reference's evaluate, 1 core; rollouts not included"}
+
+
+def _guarded(extra, key, fn, lock=None):
+    """extra[key] = fn(), or {"error": ...} if it raised: a secondary config never ends the run."""
+    try:
+        val = fn()
+    except (Exception, SystemExit) as e:        # noqa: BLE001 -- recorded; the headline line still prints
+        val = {"error": "%s: %s" % (type(e).__name__, e)}
+    if lock is not None:
+        with lock:
+            extra[key] = val
+    else:
+        extra[key] = val
+    return val
+
+
+def extras_single(device, dist, reps, lock=None):
+    """Secondary configs at N=1 (SURVEY §8d C2, C3 for the 2x64 MLP, the fp64 mode, C5), each guarded:
+    a failing one is recorded as {"error": ...} and the rest still run."""
     from trpo_amd import synth
     extra = {}
     L2 = [15, 64, 64, 3]
-    c2res = {}
-    for tag, env in (("", None), ("_recompute", "0")):
-        # C2: repeated FVP calls on one context reuse the forward-activation cache (theta unchanged);
-        # a first call after set_theta recomputes the forward pass -- timed too (TRPO_YCACHE=0)
-        if env is not None:
-            os.environ["TRPO_YCACHE"] = env
-        c2, _, _ = make_ctx(L2, 4096, dist, device)
-        os.environ.pop("TRPO_YCACHE", None)
-        c2.upload_v(synth.make_v(num_params(L2)))
-        k2 = c2.time_ms(0, reps)
-        f2 = c2.time_ms(1, reps)
-        fl = flops_per_sample_cached(L2) if env is None else flops_per_sample(L2)
-        c2res.update({"fvp_ms" + tag: f2, "kernel_ms" + tag: k2, "fvp_samples_per_s" + tag: 4096 / (f2 * 1e-3),
-                      "kernel_tflops" + tag: fl * 4096 / (k2 * 1e-3) / 1e12})
-        c2.close()
-    extra["C2_fvp_2x64_N4096"] = c2res
+
+    def c2():
+        c2res = {}
+        for tag, env in (("", None), ("_recompute", "0")):
+            # C2: repeated FVP calls on one context reuse the forward-activation cache (theta unchanged);
+            # a first call after set_theta recomputes the forward pass -- timed too (TRPO_YCACHE=0)
+            if env is not None:
+                os.environ["TRPO_YCACHE"] = env
+            try:
+                ctx, _, _ = make_ctx(L2, 4096, dist, device)
+            finally:
+                os.environ.pop("TRPO_YCACHE", None)
+            try:
+                ctx.upload_v(synth.make_v(num_params(L2)))
+                k2 = ctx.time_ms(0, reps)
+                f2 = ctx.time_ms(1, reps)
+            finally:
+                ctx.close()
+            fl = flops_per_sample_cached(L2) if env is None else flops_per_sample(L2)
+            c2res.update({"fvp_ms" + tag: f2, "kernel_ms" + tag: k2, "fvp_samples_per_s" + tag: 4096 / (f2 * 1e-3),
+                          "kernel_tflops" + tag: fl * 4096 / (k2 * 1e-3) / 1e12})
+        return c2res
+
+    def c3(L, prec):
+        ctx, _, _ = make_ctx(L, N_TOTAL, dist, device, precision=prec)
+        try:
+            K3 = 100                                 # 100 solves after 10 (as the headline: a steady-state rate)
+            t3 = time_steps(ctx, dist, K3, 10, synth.make_b(num_params(L)), tag="c3")
+            if prec is None and ctx.kernel_name.endswith(" coop"):
+                # fp32 cooperative path: the CG step runs over slices (cg_dots / cg_axpy, DESIGN §5.3), so the
+                # per-iteration tile kernel is the standalone cached-forward FVP kernel (MODE 3)
+                ctx.upload_v(synth.make_v(num_params(L)))
+                k3 = ctx.time_ms(0, 50)
+                kdesc = " (FVP kernel, cached forward; per iteration + slab reduce + cg_dots + cg_axpy)"
+            else:
+                k3 = ctx.time_ms(3, 10, CG_ITERS)
+                kdesc = " (CG-iteration kernel, cached forward)"
+            name = ctx.kernel_name
+        finally:
+            ctx.close()
+        return {"cg_wall_ms": 1e3 * t3 / K3, "fvp_samples_per_s": CG_ITERS * N_TOTAL / (t3 / K3),
+                "cg_iter_kernel_ms": k3, "kernel": name + kdesc,
+                "kernel_tflops": flops_per_sample_cached(L) * N_TOTAL / (k3 * 1e-3) / 1e12,
+                "kernel_tflops_recompute_equiv": flops_per_sample(L) * N_TOTAL / (k3 * 1e-3) / 1e12,
+                "peak_tflops": PEAK_FP64_TFLOPS if prec == "fp64" else PEAK_FP32_TFLOPS}
+
+    _guarded(extra, "C2_fvp_2x64_N4096", c2, lock)
     for key, L, prec in (("C3_cg10_2x64_N50000", L2, None),
                          ("C3_cg10_armDOF_0_N50000_fp64", ARM, "fp64"), ("C3_cg10_2x64_N50000_fp64", L2, "fp64")):
-        c3, _, _ = make_ctx(L, N_TOTAL, dist, device, precision=prec)
-        K3 = 100                                 # 100 solves after 10 (as the headline: a steady-state rate)
-        t3 = time_steps(c3, dist, K3, 10, synth.make_b(num_params(L)))
-        if prec is None and c3.kernel_name.endswith(" coop"):
-            # fp32 cooperative path: the CG step runs over slices (cg_dots / cg_axpy, DESIGN §5.3), so the
-            # per-iteration tile kernel is the standalone cached-forward FVP kernel (MODE 3)
-            c3.upload_v(synth.make_v(num_params(L)))
-            k3 = c3.time_ms(0, 50)
-            kdesc = " (FVP kernel, cached forward; per iteration + slab reduce + cg_dots + cg_axpy)"
-        else:
-            k3 = c3.time_ms(3, 10, CG_ITERS)
-            kdesc = " (CG-iteration kernel, cached forward)"
-        extra[key] = {"cg_wall_ms": 1e3 * t3 / K3, "fvp_samples_per_s": CG_ITERS * N_TOTAL / (t3 / K3),
-                      "cg_iter_kernel_ms": k3, "kernel": c3.kernel_name + kdesc,
-                      "kernel_tflops": flops_per_sample_cached(L) * N_TOTAL / (k3 * 1e-3) / 1e12,
-                      "kernel_tflops_recompute_equiv": flops_per_sample(L) * N_TOTAL / (k3 * 1e-3) / 1e12,
-                      "peak_tflops": PEAK_FP64_TFLOPS if prec == "fp64" else PEAK_FP32_TFLOPS}
-        c3.close()
-    extra["C5_update_armDOF_0_N50000"] = bench_update(device)
-    extra["C5_update_2x64_N50000"] = bench_update(device, L=L2, cpu_ref=False)
-    extra["C5_baseline_evaluate_N3000"] = bench_baseline(device)
-    u, bl = extra["C5_update_armDOF_0_N50000"], extra["C5_baseline_evaluate_N3000"]
-    extra["C5_iteration_armDOF_0"] = {
-        "device_ms": u["update_ms"] + bl["lbfgs_fit25_ms"],
-        "cpu_reference_ms_1core": (1e3 * u["cpu_reference_compute_s_1core"] + bl["cpu_port_lbfgs_fit25_ms_1core"]
-                                   if "cpu_reference_compute_s_1core" in u else None),
-        "what": "sum of the two measured stages of one training iteration's learning step: TRPO_Update "
-                "(N=50000) + the L-BFGS baseline fit (at most 25 iterations, 20x150 batch); rollouts not included"}
+        _guarded(extra, key, lambda: c3(L, prec), lock)
+    u = _guarded(extra, "C5_update_armDOF_0_N50000", lambda: bench_update(device), lock)
+    _guarded(extra, "C5_update_2x64_N50000", lambda: bench_update(device, L=L2, cpu_ref=False), lock)
+    bl = _guarded(extra, "C5_baseline_evaluate_N3000", lambda: bench_baseline(device), lock)
+    if "update_ms" in u and "evaluate_us" in bl:
+        _guarded(extra, "C5_iteration_armDOF_0", lambda: c5_iteration(u, bl), lock)
     return extra
 
 
-def extras_multi(device, dist, b, x_rccl, comm="rccl"):
-    """N > 1: the same sharded solve with the other collectives in place of the headline's (A/B on the
-    driver's multi-GPU node): RCCL or the peer-window exchange (flag hand-off), and the peer exchange in
-    its tagged-granule form (TRPO_PEER_PROTO=2: the data is its own flag, one xGMI trip fewer per
-    exchange, measured 1.4 us slower than the flag form on one GPU); and one sharded TRPO update
-    (config C5) under the headline's collective."""
-    out = {}
+def extras_multi(device, dist, b, x_ref, comm="rccl", out=None, lock=None):
+    """N > 1, measured AFTER the headline: the same sharded solve with the other collectives in place of
+    the headline's (A/B on the driver's multi-GPU node): RCCL or the peer-window exchange (flag hand-off),
+    and the peer exchange in its tagged-granule form (TRPO_PEER_PROTO=2: the data is its own flag, one
+    xGMI trip fewer per exchange); and one sharded TRPO update (config C5) under the headline's collective.
+    Every one goes through run_secondary (agreed setup, agreed steps, abort + close in `finally`);
+    results go into `out` as they complete (under `lock`: the watchdog may serialise it meanwhile)."""
+    out = {} if out is None else out
     other = "rccl" if comm == "peer" else "peer"
-    out["C4_%s_exchange" % other] = _solve_multi(device, dist, b, x_rccl, other, {})
-    out["C4_peer_granule_exchange"] = _solve_multi(device, dist, b, x_rccl, "peer", {"TRPO_PEER_PROTO": "2"})
-    try:
-        out["C5_update_armDOF_0_N50000"] = _update_multi(device, dist, comm)
-    except Exception as e:                      # noqa: BLE001 -- recorded; the headline line still prints
-        out["C5_update_armDOF_0_N50000"] = {"error": "%s: %s" % (type(e).__name__, e)}
+    runs = (("C4_%s_exchange" % other, "other", other, _solve_body(dist, b, x_ref), None),
+            ("C4_peer_granule_exchange", "granule", "peer", _solve_body(dist, b, x_ref), {"TRPO_PEER_PROTO": "2"}),
+            ("C5_update_armDOF_0_N50000", "update", comm, _update_body(dist), None))
+    for key, tag, backend, body, env in runs:
+        if dist.broken:                          # a gloo bound expired: the ranks may be out of step
+            out[key] = {"error": "skipped: an earlier secondary's gloo collective failed"}
+            continue
+        _guarded(out, key, lambda: run_secondary(dist, device, tag, backend, N_TOTAL, b, body, env=env), lock)
     return out
 
 
-def _solve_multi(device, dist, b, x_ref, backend, env):
-    """The headline's sharded solve on one collective (env: library knobs set while the context and its
-    collective are created, the same on every rank), timed like the headline (50 after 5)."""
-    import numpy as np
-    res, ctx = None, None
-    old = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
-    try:
-        ctx, _, _, _, rec = make_ctx_agreed(ARM, N_TOTAL, dist, device, backend, b, plan=(backend,))
-    except SystemExit as e:                     # recorded; every rank skips together (agreed inside)
-        res = {"error": str(e)}
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
-    if ctx is not None:
+def run_secondary(dist, device, tag, backend, n, b, body, env=None):
+    """One secondary config at N > 1: its context through make_ctx_agreed (plan = this backend only:
+    per-stage agreement, the collective's self-check, the x-hash), then body(ctx, record) whose steps
+    are agreed too; the context is closed in `finally`, its collective aborted first when anything
+    failed.  Collectives run on the secondary gloo group (shorter bound).  Faults: TRPO_BENCH_FAULT
+    stages `<tag>.<stage>` (make_ctx_agreed), `<tag>.body` (any rank raising inside the body), and
+    `<tag>.hang` (a rank blocking forever inside the body: only the watchdog ends that)."""
+    ctx, ok = None, False
+    old = {k: os.environ.get(k) for k in (env or {})}
+    with dist.secondary():
         try:
-            t = time_steps(ctx, dist, 50, 5, b)
-            x = ctx.download_x()
-            res = {"ms_per_step": 1e3 * t / 50, "fvp_samples_per_s": CG_ITERS * N_TOTAL / (t / 50),
-                   "backend": ctx.comm_backend, "n_gpus": dist.world, "verify": rec["verify"],
-                   "x_relL2_vs_headline": float(np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref))}
-        except Exception as e:                  # noqa: BLE001
-            res = {"error": "%s: %s" % (type(e).__name__, e)}
-        ctx.close()
-    return res
+            os.environ.update(env or {})
+            try:
+                ctx, _, _, _, rec = make_ctx_agreed(ARM, n, dist, device, backend, b, plan=(backend,), tag=tag)
+            finally:
+                for k, v in old.items():
+                    if v is None:
+                        os.environ.pop(k, None)
+                    else:
+                        os.environ[k] = v
+            if _fault(tag + ".hang", dist.rank, 0):
+                while True:
+                    time.sleep(3600)
+            agreed(dist, tag + ".body", lambda: None)
+            res = body(ctx, rec, tag)
+            ok = True
+            return res
+        finally:
+            if ctx is not None:
+                if not ok:
+                    ctx.comm_abort()
+                ctx.close()
 
 
-def _update_multi(device, dist, comm):
+def _solve_body(dist, b, x_ref):
+    """The headline's sharded solve on this context, timed like the headline (50 after 5)."""
+    import numpy as np
+
+    def body(ctx, rec, tag):
+        t = time_steps(ctx, dist, 50, 5, b, tag=tag)
+        x = agreed(dist, tag + ".result", ctx.download_x)
+        return {"ms_per_step": 1e3 * t / 50, "fvp_samples_per_s": CG_ITERS * N_TOTAL / (t / 50),
+                "backend": ctx.comm_backend, "n_gpus": dist.world, "verify": rec["verify"],
+                "x_relL2_vs_headline": float(np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref))}
+    return body
+
+
+def _update_body(dist):
     """C5: one TRPO policy update over the sharded rollout (policy-gradient / FVP / surrogate all-reduces)."""
     import numpy as np
     from trpo_amd import synth
-    theta = synth.make_theta(ARM)
-    obs_all = synth.make_obs(N_TOTAL, ARM[0])
-    std = np.ones(ARM[-1])
-    mean, action, adv = synth.make_rollout(ARM, "lttl", theta, obs_all, std)
-    ctx, _, obs = make_ctx(ARM, N_TOTAL, dist, device, comm=comm)
     from trpo_amd.dist import shard_range
-    lo, hi = shard_range(N_TOTAL, dist.rank, dist.world)
-    ctx.set_rollout(mean[lo:hi], action[lo:hi], adv[lo:hi])
-    ctx_backend = ctx.comm_backend
-    for _ in range(3):
-        r = ctx.update()
-    dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(20):
-        r = ctx.update()
-    wall = dist.max((time.perf_counter() - t0) / 20)
-    ctx.close()
-    return {"update_ms": 1e3 * wall, "accepted": r["accepted"], "cg_iters": int(r["cg_iters"]), "samples": N_TOTAL,
-            "n_gpus": dist.world, "comm": ctx_backend,
-            "what": "sharded rollout; all-reduces of the policy gradient, every FVP and the surrogate sums; "
-                    "host-visible wall per update (max over ranks)"}
+
+    def body(ctx, rec, tag):
+        theta = synth.make_theta(ARM)
+        obs_all = synth.make_obs(N_TOTAL, ARM[0])
+        mean, action, adv = synth.make_rollout(ARM, "lttl", theta, obs_all, np.ones(ARM[-1]))
+        lo, hi = shard_range(N_TOTAL, dist.rank, dist.world)
+        agreed(dist, tag + ".rollout", lambda: ctx.set_rollout(mean[lo:hi], action[lo:hi], adv[lo:hi]))
+        r = None
+        for _ in range(3):
+            r = agreed(dist, tag + ".warmup-update", ctx.update)
+        t0 = time.perf_counter()
+        for _ in range(20):
+            r = agreed(dist, tag + ".update", ctx.update)
+        wall = dist.max((time.perf_counter() - t0) / 20)
+        return {"update_ms": 1e3 * wall, "accepted": r["accepted"], "cg_iters": int(r["cg_iters"]),
+                "samples": N_TOTAL, "n_gpus": dist.world, "comm": ctx.comm_backend,
+                "what": "sharded rollout; all-reduces of the policy gradient, every FVP and the surrogate sums; "
+                        "host-visible wall per update (max over ranks; each update followed by a cross-rank "
+                        "agreement, as a trainer's step would be)"}
+    return body
 
 
-def sweep(device, dist, steps=10, comm="rccl"):
+def sweep(device, dist, steps=10, comm="rccl", out=None, lock=None):
     """C4's N sweep: the same sharded 10-iteration solve at larger batches (whole-job rates).  At one
     rank each row also carries the CG-iteration kernel's roofline at that N (HIP events, same units as
     the headline `roofline`): the 50k headline is latency-bound, these rows show the kernel's
-    throughput regime.  At N > 1 ranks a weak-scaling row (50k samples per rank) is added."""
+    throughput regime.  At N > 1 ranks a weak-scaling row (50k samples per rank) is added, and every
+    row goes through run_secondary.  Each row is guarded: one that fails is recorded as an error."""
     from trpo_amd import synth
-    out = {}
+    out = {} if out is None else out
+    b = synth.make_b(num_params(ARM))
     ns = list(SWEEP_N) + ([N_TOTAL * dist.world] if dist.world > 1 else [])
-    for n in ns:
-        ctx, _, _ = make_ctx(ARM, n, dist, device, comm=comm)
-        t = time_steps(ctx, dist, steps, 2, synth.make_b(num_params(ARM)))
-        row = {"ms_per_step": 1e3 * t / steps, "fvp_samples_per_s": CG_ITERS * n / (t / steps),
-               "n_gpus": dist.world}
-        if dist.world > 1 and n == N_TOTAL * dist.world:
-            row["scaling"] = "weak (50000 samples per rank)"
-        if dist.world == 1:
+
+    def row_multi(n):
+        def body(ctx, rec, tag):
+            t = time_steps(ctx, dist, steps, 2, b, tag=tag)
+            row = {"ms_per_step": 1e3 * t / steps, "fvp_samples_per_s": CG_ITERS * n / (t / steps),
+                   "n_gpus": dist.world, "backend": ctx.comm_backend}
+            if n == N_TOTAL * dist.world:
+                row["scaling"] = "weak (50000 samples per rank)"
+            return row
+        return run_secondary(dist, device, "sweep%d" % n, comm, n, b, body)
+
+    def row_single(n):
+        ctx, _, _ = make_ctx(ARM, n, dist, device)
+        try:
+            t = time_steps(ctx, dist, steps, 2, b, tag="sweep%d" % n)
+            row = {"ms_per_step": 1e3 * t / steps, "fvp_samples_per_s": CG_ITERS * n / (t / steps),
+                   "n_gpus": dist.world}
             k3 = ctx.time_ms(3, 5, CG_ITERS)
             bytes_alg = bytes_per_fvp_cached(ARM, ctx.n) + bytes_cg_step(ARM)
             row.update({"cg_iter_kernel_ms": k3, "alg_bytes_per_launch": bytes_alg,
                         "hbm_frac_algorithmic": bytes_alg / (k3 * 1e-3) / 1e9 / PEAK_HBM_GBS,
                         "fp32_frac": flops_per_sample_cached(ARM) * ctx.n / (k3 * 1e-3) / 1e12 / PEAK_FP32_TFLOPS})
-        out["cg10_armDOF_0_N%d" % n] = row
-        ctx.close()
+            return row
+        finally:
+            ctx.close()
+
+    for n in ns:
+        _guarded(out, "cg10_armDOF_0_N%d" % n, (lambda n=n: row_multi(n)) if dist.world > 1 else (lambda n=n: row_single(n)),
+                 lock)
+        if dist.broken:
+            break
     return out
 
 
@@ -749,29 +912,27 @@ def main():
 
     P = num_params(ARM)
     b = synth.make_b(P)
+    emitter = Emitter(json_fd, dist.rank)
     if dist.world > 1:
         ctx, theta, obs_local, args.comm, setup = make_ctx_agreed(ARM, N_TOTAL, dist, device, args.comm, b)
     else:
         (ctx, theta, obs_local), setup = make_ctx(ARM, N_TOTAL, dist, device), {"verify": None, "fallback": None}
     comm = ctx.comm_info()
 
-    # Order of the measurements: the secondary configs first, then the dominant kernel's event timing,
-    # then the headline's timed region LAST.  A 20-solve region (2 ms) right after a cold start caught
-    # the GPU before its clock had settled: per solve 0.1035 ms at K=20/W=5 against 0.0982 ms at
+    # Order of the measurements.  N = 1: the secondary configs first, then the dominant kernel's event
+    # timing, then the headline's timed region LAST.  A 20-solve region (2 ms) right after a cold start
+    # caught the GPU before its clock had settled: per solve 0.1035 ms at K=20/W=5 against 0.0982 ms at
     # K=500/W=50 on one box, 0.1020 ms with the 2 ms of kernel timing in front (profiles/r04_warm_ab.log);
-    # measured last, the headline sees the steady state a trainer's repeated updates run in.  The timed
-    # region itself is unchanged: W untimed solves, then exactly K full solves between barriers.
-    extra = None
-    if not args.no_extra:
-        ctx.upload_b(b)
-        ctx.enqueue_cg(CG_ITERS, 0.0)
-        ctx.wait(COMM_TIMEOUT_MS)
-        x_pre = ctx.download_x()
-        extra = extras_single(device, dist, 200) if dist.world == 1 else extras_multi(device, dist, b, x_pre, args.comm)
-        try:
-            extra["C4_sweep"] = sweep(device, dist, comm=args.comm)
-        except Exception as e:                  # noqa: BLE001 -- recorded; the headline line still prints
-            extra["C4_sweep"] = {"error": "%s: %s" % (type(e).__name__, e)}
+    # measured last, the headline sees the steady state a trainer's repeated updates run in.  N > 1: the
+    # headline's timed region comes right after its agreed setup, and the secondary configs (each with
+    # its own agreed setup, shorter gloo bound, abort + close on failure) only after it, under a
+    # watchdog that prints the headline line by the deadline whatever a secondary does.
+    # The timed region itself is the same in both: W untimed solves, then exactly K full solves between
+    # barriers.
+    extra = {} if not args.no_extra else None
+    if extra is not None and dist.world == 1:
+        extra.update(extras_single(device, dist, 200))
+        extra["C4_sweep"] = sweep(device, dist, comm=args.comm)
 
     # the dominant kernel: the fused CG-iteration kernel (9 of the 10 launches of a solve), timed alone
     # with HIP events on the context's stream, averaged over the iterations K_1..K_9 of a solve
@@ -791,18 +952,6 @@ def main():
     achieved_gbs = bytes_alg / (k3 * 1e-3) / 1e9
     achieved_tflops = flops / (k3 * 1e-3) / 1e12
     hbm_bound = bytes_alg / (PEAK_HBM_GBS * 1e9) >= flops / (PEAK_FP32_TFLOPS * 1e12)
-
-    traffic, tsrc = None, None
-    if dist.world == 1 and not args.no_pmc and os.environ.get("TRPO_TRAFFIC_JSON") is None:
-        traffic, tsrc = measure_traffic(device)
-    if traffic is None and dist.world == 1:
-        # fallback: HBM bytes per launch of this kernel at this workload from the newest committed
-        # rocprofv3 PMC passes (tools/profile_round.sh: FETCH_SIZE x2 + WRITE_SIZE, separate passes)
-        why = tsrc
-        tpath = os.environ.get("TRPO_TRAFFIC_JSON") or latest_traffic_json()
-        if tpath and os.path.exists(tpath):
-            traffic = json.load(open(tpath))["traffic_bytes"]
-            tsrc = {"measured": "profile file " + os.path.relpath(tpath, ROOT), "why_not_live": why}
 
     result = {
         "metric": "FVP samples/sec + 10-iter CG wall time, armDOF_0 policy",
@@ -832,7 +981,7 @@ def main():
                      "peak": PEAK_HBM_GBS if hbm_bound else PEAK_FP32_TFLOPS,
                      "unit": "GB/s" if hbm_bound else "TFLOP/s",
                      "frac": achieved_gbs / PEAK_HBM_GBS if hbm_bound else achieved_tflops / PEAK_FP32_TFLOPS,
-                     "traffic": traffic, "traffic_source": tsrc,
+                     "traffic": None, "traffic_source": None,
                      "kernel": "fvp_mlp3_kernel MODE 3 (CG-iteration kernel: fp64 CG step + cached-forward FVP)",
                      "kernel_ms": k3, "flops_per_launch": flops, "alg_bytes_per_launch": bytes_alg,
                      "fp32_tflops": achieved_tflops, "fp32_frac": achieved_tflops / PEAK_FP32_TFLOPS,
@@ -840,34 +989,118 @@ def main():
                      "full_recompute_equiv_tflops": flops_per_sample(ARM) * n_local / (k3 * 1e-3) / 1e12,
                      "secondary_fvp_kernel_mode2_ms": k2},
     }
-
     if extra is not None:
         result["extra"] = extra
+
+    if dist.world > 1 and not args.no_cpu_baseline:
+        # the sharded solve's step against the reference's CG over the WHOLE batch (rank 0 regenerates
+        # the seeded 50k observations; the other ranks wait at the agreement)
+        def parity():
+            if dist.rank == 0:
+                obs_all = synth.make_obs(N_TOTAL, ARM[0])
+                _, x_ref = cpu_reference_cg(theta, obs_all, b)
+                rel = float(np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref))
+                result["parity"] = {"cg_step_relL2_vs_cpu": rel, "tolerance": 1e-4,
+                                    "what": "x of the %d-rank sharded solve vs the reference CG on all %d samples"
+                                            % (dist.world, N_TOTAL)}
+        try:
+            agreed(dist, "parity", parity)
+        except Exception as e:                  # noqa: BLE001 -- recorded; the line still prints
+            result["parity"] = {"error": "%s: %s" % (type(e).__name__, e)}
+
+    # the headline is measured: from here the line is printed by the deadline whatever follows does
+    emitter.arm(result)
+
+    if extra is not None and dist.world > 1:
+        extras_multi(device, dist, b, x, args.comm, out=extra, lock=emitter.lock)
+        if not dist.broken:
+            with emitter.lock:
+                extra["C4_sweep"] = {}
+            sweep(device, dist, comm=args.comm, out=extra["C4_sweep"], lock=emitter.lock)
+
+    if dist.world == 1:
+        traffic, tsrc = None, None
+        if not args.no_pmc and os.environ.get("TRPO_TRAFFIC_JSON") is None:
+            traffic, tsrc = measure_traffic(device)
+        if traffic is None:
+            # fallback: HBM bytes per launch of this kernel at this workload from the newest committed
+            # rocprofv3 PMC passes (tools/profile_round.sh: FETCH_SIZE x2 + WRITE_SIZE, separate passes)
+            why = tsrc
+            tpath = os.environ.get("TRPO_TRAFFIC_JSON") or latest_traffic_json()
+            if tpath and os.path.exists(tpath):
+                traffic = json.load(open(tpath))["traffic_bytes"]
+                tsrc = {"measured": "profile file " + os.path.relpath(tpath, ROOT), "why_not_live": why}
+        with emitter.lock:
+            result["roofline"]["traffic"], result["roofline"]["traffic_source"] = traffic, tsrc
 
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
         threads_all = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
         head, rows, x_ref = cpu_rows(theta, obs_local, b, threads_all)
         head["rows"] = rows
-        result["cpu_baseline"] = head
         rel = float(np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref))
-        result["parity"] = {"cg_step_relL2_vs_cpu": rel, "tolerance": 1e-4}
-    elif dist.world > 1 and not args.no_cpu_baseline:
-        # the sharded solve's step against the reference's CG over the WHOLE batch (rank 0 regenerates
-        # the seeded 50k observations; the other ranks wait at the closing barrier)
-        if dist.rank == 0:
-            obs_all = synth.make_obs(N_TOTAL, ARM[0])
-            _, x_ref = cpu_reference_cg(theta, obs_all, b)
-            rel = float(np.linalg.norm(x - x_ref) / np.linalg.norm(x_ref))
-            result["parity"] = {"cg_step_relL2_vs_cpu": rel, "tolerance": 1e-4,
-                                "what": "x of the %d-rank sharded solve vs the reference CG on all %d samples"
-                                        % (dist.world, N_TOTAL)}
-        dist.barrier()
+        with emitter.lock:
+            result["cpu_baseline"] = head
+            result["parity"] = {"cg_step_relL2_vs_cpu": rel, "tolerance": 1e-4}
+
+    if dist.world > 1 and not dist.broken:
+        try:
+            dist.barrier()
+        except Exception:                       # noqa: BLE001 -- the line still prints
+            pass
+    if dist.broken:
+        ctx.comm_abort()                        # a rank may be stuck: do not wait on the collective
     ctx.close()
+    emitter.emit(result)
+    if dist.broken:
+        # a gloo collective timed out: tearing its process group down can abort in its destructor
+        # (std::terminate), so leave without interpreter teardown once the line is out
+        sys.stderr.flush()
+        os._exit(0)
     dist.close()
-    sys.stdout.flush()
-    with os.fdopen(json_fd, "w") as out:
-        if dist.rank == 0:
-            out.write(json.dumps(result) + "\n")
+
+
+class Emitter:
+    """Prints rank 0's one JSON line exactly once: from the main thread at the end, or -- once the
+    headline has been measured (arm) -- from a watchdog thread at the deadline, which then ends the
+    process (os._exit(0), on every rank) so that no secondary config, however it fails, can cost the
+    driver its headline line.  Deadline: TRPO_BENCH_DEADLINE_S (default 420) after the process started,
+    and at least TRPO_BENCH_GRACE_S (default 60) after the headline.  `lock` guards the result dict
+    against the watchdog's serialisation while the main thread adds secondary results."""
+
+    def __init__(self, fd, rank):
+        import threading
+        self.fd, self.rank, self.lock, self.done = fd, rank, threading.RLock(), False
+        self.t_start = time.monotonic()
+
+    def emit(self, result, note=None):
+        with self.lock:
+            if self.done:
+                return False
+            self.done = True
+            if note is not None:
+                result = dict(result, watchdog=note)
+            line = json.dumps(result) + "\n"
+        sys.stdout.flush()
+        if self.rank == 0:
+            os.write(self.fd, line.encode())
+        return True
+
+    def arm(self, result):
+        import threading
+        deadline = max(self.t_start + float(os.environ.get("TRPO_BENCH_DEADLINE_S", "420")),
+                       time.monotonic() + float(os.environ.get("TRPO_BENCH_GRACE_S", "60")))
+
+        def run():
+            while time.monotonic() < deadline:
+                time.sleep(min(1.0, max(0.0, deadline - time.monotonic())))
+            note = ("deadline reached after %.0f s: the line was printed by the watchdog; secondary configs "
+                    "still running were abandoned" % (time.monotonic() - self.t_start))
+            if self.emit(result, note):
+                print("bench.py: rank %d: %s" % (self.rank, note), file=sys.stderr)
+                sys.stderr.flush()
+                os._exit(0)
+
+        threading.Thread(target=run, name="bench-watchdog", daemon=True).start()
 
 
 if __name__ == "__main__":

@@ -1,0 +1,79 @@
+"""MI355X: the margin of the fp32 stall guard's threshold.  With the guard OFF
+(TRPO_RITZ_RERUN=0), every CG / update golden and every random-shape draw is solved in fp32 and its
+smallest relative Ritz residual (trpo_ctx_cg_status) is logged beside its error against the reference.
+Asserted: every solve whose fp32 step misses the 1e-4 bound has a Ritz residual below the library's
+default threshold (so the guard, ON, re-solves it in fp64), and the default threshold sits at least
+10x below the smallest Ritz residual of the solves that are within 1e-4 -- a false trigger only costs an
+fp64 re-solve, a missed one costs a 1e-3 step.  TRPO_RITZ_LOG=<file> writes the table (profiles/)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import cases
+import oracle
+import trpo_amd
+from trpo_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+DEFAULT_THRESHOLD = 1e-14            # csrc/trpo_host.c ritz_threshold()
+
+
+def _rows():
+    rows = []
+    for c in cases.manifest():
+        if c["kind"] == "cg":
+            x = cases.inputs(c)
+            with trpo_amd.Context(x["layers"], x["acfunc"], x["theta"], x["obs"], x["std"], x["damping"]) as ctx:
+                got = ctx.cg(x["vin"], c["maxiter"], c["resth"])
+                st = ctx.cg_status()
+            rows.append(dict(case=c["name"], ritz=st["ritz_residual"], err=cases.rel_l2(got, cases.expected(c))))
+        elif c["kind"] == "update":
+            x = cases.update_inputs(c)
+            with trpo_amd.Context(x["layers"], x["acfunc"], x["theta"], x["obs"], x["std"], x["damping"]) as ctx:
+                ctx.set_rollout(x["mean"], x["action"], x["adv"])
+                r = ctx.update()
+            exp = cases.expected(c)
+            rows.append(dict(case=c["name"], ritz=r["ritz_residual"],
+                             err=cases.rel_l2(r["theta"] - x["theta"], exp - x["theta"])))
+    from test_gpu_random_shapes import _draw
+    for seed in range(36):
+        layers, acts, n, std = _draw(seed)
+        th = synth.make_theta(layers, seed=100 + seed)
+        obs = synth.make_obs(n, layers[0], seed=200 + seed)
+        P = synth.num_params(layers)
+        b = synth.make_b(P, seed=400 + seed)
+        mean, action, adv = synth.make_rollout(layers, acts, th, obs, std, seed=500 + seed)
+        xr = oracle.cg(layers, acts, th, obs, std, b, 10, 0.0)["x"]
+        ref = oracle.update(layers, acts, th, obs, mean, action, adv, std, 0.1)
+        with trpo_amd.Context(layers, acts, th, obs, std, 0.1) as ctx:
+            x = ctx.cg(b, 10, 0.0)
+            rz = ctx.cg_status()["ritz_residual"]
+            ctx.set_rollout(mean, action, adv)
+            r = ctx.update()
+        rows.append(dict(case="draw%d cg" % seed, ritz=rz, err=cases.rel_l2(x, xr)))
+        rows.append(dict(case="draw%d update" % seed, ritz=r["ritz_residual"], err=cases.rel_l2(r["x"], ref["x"])))
+    return rows
+
+
+def test_stall_guard_threshold_margin(monkeypatch):
+    monkeypatch.setenv("TRPO_RITZ_RERUN", "0")
+    rows = _rows()
+    bad = [r for r in rows if r["err"] > 1e-4]
+    good = [r for r in rows if r["err"] <= 1e-4]
+    nearest = min((r for r in good if r["ritz"] >= DEFAULT_THRESHOLD), key=lambda r: r["ritz"])
+    out = {"threshold": DEFAULT_THRESHOLD, "missed_bound_fp32": bad, "nearest_within_bound_above_threshold": nearest,
+           "margin": nearest["ritz"] / DEFAULT_THRESHOLD,
+           "rows": sorted(rows, key=lambda r: r["ritz"])}
+    print(json.dumps({k: v for k, v in out.items() if k != "rows"}))
+    path = os.environ.get("TRPO_RITZ_LOG")
+    if path:
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+    assert bad, "expected draw 23's update to miss the bound without the guard"
+    for r in bad:
+        assert r["ritz"] < DEFAULT_THRESHOLD, r          # the guard catches every fp32 miss
+    assert out["margin"] >= 10.0, out                    # and stays clear of the solves that are fine
+    assert np.isfinite([r["ritz"] for r in rows]).all()

@@ -40,6 +40,7 @@ def test_past_convergence_solve_is_resolved_in_fp64(monkeypatch):
         got = ctx.cg(x["vin"], c["maxiter"], c["resth"])
         st = ctx.cg_status()
         rr, _, it = ctx.cg_history()
+        np.testing.assert_array_equal(ctx.download_x(), got)   # the device slot holds the returned x
     assert st["fp64_rerun"] and st["ritz_residual"] < 1e-15, st
     with _ctx(x, precision="fp64") as c64:
         want = c64.cg(x["vin"], c["maxiter"], c["resth"])

@@ -3,7 +3,9 @@ is 1.98e-3 off after the first repetition's in-process peer ranks ran.  Which st
 state behind?  usage: ... [torch|notorch] STAGE   (STAGE: none | create | handle | attach | fvp | update | threads |
 group | seqpeer)
   threads: the two contexts NOT attached, fvp + update concurrently from two threads
-  group:   attached to an in-process host group instead of peer windows, fvp + update concurrently"""
+  group:   attached to an in-process host group instead of peer windows, fvp + update concurrently
+optional 3rd argument "keep": the two contexts stay open while the later single context runs (round 5:
+does the later context go wrong only when it can reuse their freed memory?)"""
 import os
 import sys
 
@@ -83,7 +85,13 @@ if stage != "none":
             t.start()
         for t in ts:
             t.join()
-    for c in ctxs:
-        c.close()
+    keep = len(sys.argv) > 3 and sys.argv[3] == "keep"
+    if not keep:
+        for c in ctxs:
+            c.close()
 single("after %s" % stage)
 single("after %s, again" % stage)
+if stage != "none" and keep:
+    for c in ctxs:
+        c.close()
+    single("after %s, contexts closed" % stage)

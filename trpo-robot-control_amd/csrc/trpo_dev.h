@@ -43,6 +43,14 @@ int trpo_dev_set_comm(trpo_dev *d, int rank, int world, const void *id128, long 
 /* bounded self-check / wait / abort of the attached collective (trpo_kernels.hip) */
 int trpo_dev_comm_verify(trpo_dev *d, long timeout_ms, long *bad);
 int trpo_dev_wait(trpo_dev *d, long timeout_ms);
+// the closing wait of a synchronous call: hipStreamSynchronize on one rank, bounded (and the
+// collective's error reported) with a collective attached
+int trpo_dev_wait_done(trpo_dev *d);
+#define DSYNC(d)                                     \
+    do {                                             \
+        const int dsync_rc_ = trpo_dev_wait_done(d); \
+        if (dsync_rc_) return dsync_rc_;             \
+    } while (0)
 int trpo_dev_comm_abort(trpo_dev *d);
 /* in-process host-staged group of `world` contexts (one thread each): the sharded code path
  * without RCCL, for tests (trpo_kernels.hip) */

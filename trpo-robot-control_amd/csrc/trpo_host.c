@@ -87,7 +87,7 @@ struct trpo_ctx {
  * the Ritz residual is insensitive to it (the probe perturbs them: unchanged to 2 digits). */
 static double ritz_threshold(void) {
     const char *e = getenv("TRPO_RITZ_RERUN");
-    return e ? atof(e) : 1e-15;
+    return e ? atof(e) : 1e-14;
 }
 
 /* eigenvalues d[] of the symmetric tridiagonal matrix (diagonal d, e[i] = T[i][i+1] for i < n - 1) and
@@ -422,6 +422,8 @@ double trpo_ctx_cg(trpo_ctx *c, const double *b, size_t max_iter, double th, dou
             rc = trpo_dev_upload(t, TRPO_VEC_B, b);
             if (!rc) rc = trpo_dev_cg(t, max_iter, th);
             if (!rc) rc = trpo_dev_download(t, TRPO_VEC_X, x);
+            /* the context's own slot X then holds the x this call returns (trpo_ctx_download_x agrees) */
+            if (!rc) rc = trpo_dev_upload(c->dev, TRPO_VEC_X, x);
             if (!rc) {
                 c->last_rerun = 1;
                 hd = t;

@@ -3775,7 +3775,7 @@ static int hgroup_allreduce(trpo_dev *d, double *buf, size_t count) {
         hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv((long)count, 256)), dim3(256), 0, d->stream,
                            (const double *)d->gbuf_dev, buf, (int)count);
     HCHK(hipGetLastError());
-    HCHK(hipStreamSynchronize(d->stream));
+    DSYNC(d);
     return 0;
 }
 
@@ -3821,21 +3821,20 @@ static void bind_fast_no(trpo_dev *d) {
     name_fast(d);
 }
 
-static int g_force_prec = -1;        // trpo_dev_create_prec: -1 = TRPO_PRECISION, 0 fp32, 1 fp64
-extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, const char *ac, char *err,
-                                     size_t errlen);
-static pthread_mutex_t g_prec_mu = PTHREAD_MUTEX_INITIALIZER;
+// force_prec: -1 = TRPO_PRECISION from the environment, 0 fp32, 1 fp64 (trpo_dev_create_prec: the
+// fp64 twin of a context, built while other threads may create ordinary contexts)
+static trpo_dev *dev_create(int device, size_t nl, const size_t *ls, const char *ac, int force_prec, char *err,
+                            size_t errlen);
 extern "C" trpo_dev *trpo_dev_create_prec(int device, size_t nl, const size_t *ls, const char *ac, int f64,
                                           char *err, size_t errlen) {
-    pthread_mutex_lock(&g_prec_mu);
-    g_force_prec = f64 ? 1 : 0;
-    trpo_dev *d = trpo_dev_create(device, nl, ls, ac, err, errlen);
-    g_force_prec = -1;
-    pthread_mutex_unlock(&g_prec_mu);
-    return d;
+    return dev_create(device, nl, ls, ac, f64 ? 1 : 0, err, errlen);
 }
 extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, const char *ac, char *err,
                                      size_t errlen) {
+    return dev_create(device, nl, ls, ac, -1, err, errlen);
+}
+static trpo_dev *dev_create(int device, size_t nl, const size_t *ls, const char *ac, int force_prec, char *err,
+                            size_t errlen) {
 #define FAIL(...)                                      \
     do {                                               \
         if (err) snprintf(err, errlen, __VA_ARGS__);   \
@@ -3924,7 +3923,7 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
     {
         // precision mode: "fp64" runs the FVP in fp64 (v_mfma_f64_16x16x4_f64) -- the reference's
         // own precision -- through the cooperative kernel, which covers every tile-kernel shape
-        const char *ep = g_force_prec >= 0 ? (g_force_prec ? "fp64" : "fp32") : getenv("TRPO_PRECISION");
+        const char *ep = force_prec >= 0 ? (force_prec ? "fp64" : "fp32") : getenv("TRPO_PRECISION");
         d->f64 = ep && (strcmp(ep, "fp64") == 0 || strcmp(ep, "64") == 0 || strcmp(ep, "double") == 0);
         if (ep && !d->f64 && strcmp(ep, "fp32") != 0 && strcmp(ep, "32") != 0 && strcmp(ep, "float") != 0)
             FAIL("TRPO_PRECISION=%s: expected fp32 or fp64", ep);
@@ -4105,8 +4104,30 @@ extern "C" trpo_dev *trpo_dev_create(int device, size_t nl, const size_t *ls, co
 #undef DMALLOC
 }
 
+// Diagnostics (TRPO_DEBUG_ALLOC=1, stderr): the device address range of every buffer of the context, so
+// a probe can see whether a context's buffers reuse pages of an earlier context's freed peer window
+// (the peer-path wrong results under torch's runtime).
+static void dbg_dump(trpo_dev *d, const char *tag) {
+    if (!getenv("TRPO_DEBUG_ALLOC")) return;
+    const void *ptrs[] = {d->zbuf, d->dotsbuf, d->obs64, d->pg_d, d->pg_adv, d->pg_iv, d->st, d->pbuf[0], d->pbuf[1], d->rbuf[0], d->rbuf[1], d->accbuf, d->pacc, d->imap, d->tpack, d->vpack, d->tmap, d->vmap, d->pslot, d->islot, d->obs4, d->yc, d->gth, d->gv, d->giv, d->gobs, d->scratch,
+                          d->theta64, d->std64, d->r, d->zacc, d->slabs, d->ctl, d->hist, d->tscr, d->qbuf, d->qzero, d->zred, d->ptmp, d->pn, d->vec[0], d->vec[1], d->vec[2], d->vec[3], d->vec[4]};
+    const char *names[] = {"zbuf", "dotsbuf", "obs64", "pg_d", "pg_adv", "pg_iv", "st", "pbuf0", "pbuf1", "rbuf0", "rbuf1", "accbuf", "pacc", "imap", "tpack", "vpack", "tmap", "vmap", "pslot", "islot", "obs4", "yc", "gth", "gv", "giv", "gobs", "scratch",
+                           "theta64", "std64", "r", "zacc", "slabs", "ctl", "hist", "tscr", "qbuf", "qzero", "zred", "ptmp", "pn", "vec0", "vec1", "vec2", "vec3", "vec4"};
+    static_assert(sizeof(ptrs) / sizeof(ptrs[0]) == sizeof(names) / sizeof(names[0]), "names");
+    for (size_t i = 0; i < sizeof(ptrs) / sizeof(ptrs[0]); ++i) {
+        if (!ptrs[i]) continue;
+        void *base = NULL;
+        size_t sz = 0;
+        if (hipMemPtrGetInfo((void *)ptrs[i], &sz) != hipSuccess) (void)hipGetLastError();
+        base = (void *)ptrs[i];
+        fprintf(stderr, "[trpo_alloc] %s ctx=%p %s %p +%zu\n", tag, (void *)d, names[i], base, sz);
+    }
+    if (d->peer) fprintf(stderr, "[trpo_alloc] %s ctx=%p window %p\n", tag, (void *)d, trpo_peer_window(d->peer));
+}
+
 extern "C" void trpo_dev_destroy(trpo_dev *d) {
     if (!d) return;
+    dbg_dump(d, "destroy");
     if (d->stream) hipStreamSynchronize(d->stream);
     if (d->cg_exec) hipGraphExecDestroy(d->cg_exec);
     if (d->comm) ncclCommDestroy(d->comm);
@@ -4130,7 +4151,7 @@ static int sync_ctl_scalars(trpo_dev *d) {
     // damping and N live in the control block so captured graphs stay valid
     HCHK(hipMemcpyAsync(&d->ctl->damping, &d->damping, sizeof(double), hipMemcpyHostToDevice, d->stream));
     HCHK(hipMemcpyAsync(&d->ctl->n_total, &d->n_total, sizeof(double), hipMemcpyHostToDevice, d->stream));
-    HCHK(hipStreamSynchronize(d->stream));
+    DSYNC(d);
     return 0;
 }
 
@@ -4154,7 +4175,7 @@ extern "C" int trpo_dev_set_theta(trpo_dev *d, const double *theta) {
                            (long)d->P, d->f64);
     }
     HCHK(hipGetLastError());
-    HCHK(hipStreamSynchronize(d->stream));
+    DSYNC(d);
     return 0;
 }
 
@@ -4173,7 +4194,7 @@ extern "C" int trpo_dev_set_std(trpo_dev *d, const double *stdv) {
                            d->std64, d->net.A, d->net.A, d->f64);
     }
     HCHK(hipGetLastError());
-    HCHK(hipStreamSynchronize(d->stream));
+    DSYNC(d);
     return 0;
 }
 
@@ -4267,7 +4288,7 @@ extern "C" int trpo_dev_set_obs(trpo_dev *d, const double *obs, size_t n) {
         d->slab_blocks = d->grid;
     }
     HCHK(hipGetLastError());
-    HCHK(hipStreamSynchronize(d->stream));
+    DSYNC(d);
     if (d->obs64) hipFree(d->obs64);
     d->obs64 = tmp;                                    // kept in fp64 for the TRPO_Update path
     if (d->cg_exec) {     // geometry may have changed: recapture next time
@@ -4301,7 +4322,7 @@ static int choose_replicas(trpo_dev *d) {
         // a different prefix of each replica set is used from now on: start from all-zero sets
         HCHK(hipMemsetAsync(d->accbuf, 0, sizeof(double) * 3 * d->R * d->Ps, d->stream));
         HCHK(hipMemsetAsync(d->pacc, 0, sizeof(double) * 2 * d->R * d->Ps, d->stream));
-        HCHK(hipStreamSynchronize(d->stream));
+        DSYNC(d);
         d->Rc = rc;
         if (d->cg_exec) {
             hipGraphExecDestroy(d->cg_exec);
@@ -4516,9 +4537,13 @@ extern "C" int trpo_dev_set_comm(trpo_dev *d, int rank, int world, const void *i
 
 // Wait for everything enqueued on the context's stream, at most timeout_ms (<= 0: the default of
 // TRPO_COMM_TIMEOUT_MS / 120 s): 0 when it completed (or the collective's error), -6 on time-out.
-// spin: poll without sleeping (a timed region); otherwise 50 us between polls.
+// spin: poll without sleeping for the first WAIT_SPIN_MS (a timed region's closing wait must not add a
+// sleep quantum), then 50 us between polls, so a slow or hung collective does not hold a host core at
+// 100 % for the whole bound; otherwise 50 us between polls from the start.
+#define WAIT_SPIN_MS 250.0
 static int wait_stream(trpo_dev *d, long timeout_ms, bool spin) {
-    const double t_end = mono_ms() + (double)comm_timeout_ms(timeout_ms);
+    const double t0 = mono_ms();
+    const double t_end = t0 + (double)comm_timeout_ms(timeout_ms);
     for (;;) {
         const hipError_t e = hipStreamQuery(d->stream);
         if (e == hipSuccess) return 0;
@@ -4526,12 +4551,22 @@ static int wait_stream(trpo_dev *d, long timeout_ms, bool spin) {
             fprintf(stderr, "[trpo_mi355x] HIP error %s while waiting for the stream\n", hipGetErrorString(e));
             return -2;
         }
-        if (mono_ms() > t_end) return -6;
-        if (!spin) {
+        const double now = mono_ms();
+        if (now > t_end) return -6;
+        if (!spin || now - t0 > WAIT_SPIN_MS) {
             struct timespec ts = {0, 50000};
             nanosleep(&ts, NULL);
         }
     }
+}
+
+// The host's wait at the end of a synchronous call (update, FVP, surrogate, ...): a plain stream
+// synchronisation on one rank; with a collective attached a peer that never arrives must not hang the
+// caller, so the wait is bounded (TRPO_COMM_TIMEOUT_MS / 120 s) and reports -6 / the collective's error.
+extern "C" int trpo_dev_wait_done(trpo_dev *d) {
+    if (!has_collective(d)) return hipStreamSynchronize(d->stream) == hipSuccess ? 0 : -2;
+    const int rc = wait_stream(d, 0, true);
+    return rc ? rc : trpo_dev_comm_error(d);
 }
 
 extern "C" int trpo_dev_wait(trpo_dev *d, long timeout_ms) {
@@ -4573,7 +4608,12 @@ extern "C" int trpo_dev_comm_abort(trpo_dev *d) {
 static int comm_fault(const trpo_dev *d, const char *kind) {
     const char *e = getenv("TRPO_COMM_FAULT");
     const size_t k = strlen(kind);
-    return e && !strncmp(e, kind, k) && e[k] == ':' && atoi(e + k + 1) == d->rank;
+    const int hit = e && !strncmp(e, kind, k) && e[k] == ':' && atoi(e + k + 1) == d->rank;
+    if (hit)            // a test-only hook: never silent when it fires
+        fprintf(stderr, "[trpo_mi355x] WARNING: TRPO_COMM_FAULT=%s is set: rank %d %s its self-check "
+                        "all-reduce on purpose (fault injection for tests)\n", e, d->rank,
+                !strcmp(kind, "hang") ? "skips" : "corrupts");
+    return hit;
 }
 
 extern "C" int trpo_dev_comm_verify(trpo_dev *d, long timeout_ms, long *bad) {
@@ -4675,7 +4715,7 @@ extern "C" int trpo_dev_comm_error(const trpo_dev *d);
 extern "C" int trpo_dev_set_peers(trpo_dev *d, int rank, int world, const void *handles, void *const *local) {
     if (!d || !d->peer || world < 1 || world > PEER_WMAX || rank < 0 || rank >= world) return -1;
     HCHK(hipSetDevice(d->device));
-    HCHK(hipStreamSynchronize(d->stream));
+    DSYNC(d);
     const int rc = trpo_peer_connect(d->peer, rank, world, handles, local, d->stream);
     if (rc) return rc;
     if (d->comm) {
@@ -4731,7 +4771,7 @@ __global__ void vcopy64_kernel(const double *__restrict__ src, double *__restric
 // writers (downloads) are ordered after a pending upload's copy by the stream and need no wait
 static int ensure_hst(trpo_dev *d, size_t count, bool host_writes = false) {
     if (d->hst_pending && (host_writes || count > d->hst_cap || !d->hst)) {
-        HCHK(hipStreamSynchronize(d->stream));
+        DSYNC(d);
         d->hst_pending = 0;
     }
     if (count <= d->hst_cap && d->hst) return 0;
@@ -4765,7 +4805,7 @@ extern "C" int trpo_dev_download(trpo_dev *d, int slot, double *host) {
     hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, (const double *)d->vec[slot],
                        d->hst_dev, d->P);
     HCHK(hipGetLastError());
-    HCHK(hipStreamSynchronize(d->stream));
+    DSYNC(d);
     d->hst_pending = 0;
     memcpy(host, d->hst, sizeof(double) * d->P);
     return trpo_dev_comm_error(d);
@@ -4786,7 +4826,7 @@ extern "C" int trpo_dev_download_x_cg(trpo_dev *d, double *host, double *stats, 
     if (hw) hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv(hw, 256)), dim3(256), 0, d->stream,
                                (const double *)d->hist, d->hst_dev + d->P + cw, hw);
     HCHK(hipGetLastError());
-    HCHK(hipStreamSynchronize(d->stream));
+    DSYNC(d);
     d->hst_pending = 0;
     memcpy(host, d->hst, sizeof(double) * d->P);
     Ctl c;
@@ -4807,14 +4847,14 @@ extern "C" int trpo_dev_get_obs(trpo_dev *d, double *host) {
     if (!d->n) return 0;
     HCHK(hipSetDevice(d->device));
     HCHK(hipMemcpyAsync(host, d->obs64, sizeof(double) * d->n * d->net.L[0], hipMemcpyDeviceToHost, d->stream));
-    HCHK(hipStreamSynchronize(d->stream));
+    DSYNC(d);
     return 0;
 }
 extern "C" int trpo_dev_get_std(trpo_dev *d, double *host) {
     if (!d || !host) return -1;
     HCHK(hipSetDevice(d->device));
     HCHK(hipMemcpyAsync(host, d->std64, sizeof(double) * d->net.A, hipMemcpyDeviceToHost, d->stream));
-    HCHK(hipStreamSynchronize(d->stream));
+    DSYNC(d);
     return 0;
 }
 
@@ -4968,7 +5008,7 @@ extern "C" int trpo_dev_fvp_host(trpo_dev *d, double *host) {
     int rc = fvp_src(d, d->vec[TRPO_VEC_V], &zh);
     if (rc) return rc;
     if (!zh) return trpo_dev_download(d, TRPO_VEC_Z, host);
-    HCHK(hipStreamSynchronize(d->stream));
+    DSYNC(d);
     d->hst_pending = 0;
     memcpy(host, d->hst, sizeof(double) * d->P);
     return 0;
@@ -5335,7 +5375,7 @@ extern "C" int trpo_dev_cg_history(trpo_dev *d, double *rdotr, double *xnorm, si
     hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv(hw, 256)), dim3(256), 0, d->stream, (const double *)d->hist,
                        d->hst_dev + cw, hw);
     HCHK(hipGetLastError());
-    HCHK(hipStreamSynchronize(d->stream));
+    DSYNC(d);
     d->hst_pending = 0;
     Ctl c;
     memcpy(&c, d->hst, sizeof c);
@@ -5356,8 +5396,7 @@ extern "C" int trpo_dev_cg_history(trpo_dev *d, double *rdotr, double *xnorm, si
 extern "C" int trpo_dev_sync(trpo_dev *d) {
     if (!d) return -1;
     HCHK(hipSetDevice(d->device));
-    HCHK(hipStreamSynchronize(d->stream));
-    return trpo_dev_comm_error(d);
+    return trpo_dev_wait_done(d);
 }
 
 // Kernel-only timing of the fused CG-iteration kernel K_j (j >= 1: CG step j-1 -> j in the prologue,
@@ -5381,7 +5420,7 @@ static int cg_iter_kernel_only(trpo_dev *d, long j, bool init) {
         CgSt st;
         HCHK(hipMemcpyAsync(&c, d->ctl, sizeof c, hipMemcpyDeviceToHost, d->stream));
         HCHK(hipMemcpyAsync(&st, d->st, sizeof st, hipMemcpyDeviceToHost, d->stream));
-        HCHK(hipStreamSynchronize(d->stream));
+        DSYNC(d);
         c.maxiter = 1 << 30;
         c.resth = -1.0;
         c.done = 0;
@@ -5389,7 +5428,7 @@ static int cg_iter_kernel_only(trpo_dev *d, long j, bool init) {
         st.iter = 0;
         HCHK(hipMemcpyAsync(sctl, &c, sizeof c, hipMemcpyHostToDevice, d->stream));
         HCHK(hipMemcpyAsync(sst, &st, sizeof st, hipMemcpyHostToDevice, d->stream));
-        HCHK(hipStreamSynchronize(d->stream));
+        DSYNC(d);
     }
     IterArgs a = plain_args(d, &sctl->zero);
     a.update = 1;

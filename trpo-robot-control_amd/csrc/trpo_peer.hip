@@ -288,7 +288,9 @@ static void peer_free(trpo_peer *p) {
     hipSetDevice(p->device);
     for (int r = 0; r < PEER_WMAX; ++r)
         if (p->opened[r]) hipIpcCloseMemHandle(p->opened[r]);
-    if (p->win) hipFree(p->win);
+    // TRPO_PEER_KEEP_WINDOW=1 (diagnostics): leak the window instead of freeing it, so no later
+    // allocation of the process can reuse its pages
+    if (p->win && !getenv("TRPO_PEER_KEEP_WINDOW")) hipFree(p->win);
     if (p->dwins) hipFree(p->dwins);
     if (p->cnt) hipFree(p->cnt);
     if (p->err_h) hipHostFree(p->err_h);
@@ -316,6 +318,7 @@ trpo_peer *trpo_peer_create(int device, size_t S) {
         (void)hipGetLastError();
         p->win = NULL;
     }
+    if (getenv("TRPO_DEBUG_ALLOC")) fprintf(stderr, "[trpo_alloc] window %p +%zu\n", (void *)p->win, bytes);
     bool ok = p->win && hipMemset(p->win, 0, bytes) == hipSuccess &&
               hipMalloc((void **)&p->dwins, sizeof(double *) * PEER_WMAX) == hipSuccess &&
               hipMalloc((void **)&p->cnt, sizeof(unsigned long long) * PEER_WMAX) == hipSuccess &&

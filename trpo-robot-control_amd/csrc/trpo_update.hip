@@ -808,7 +808,7 @@ extern "C" int trpo_dev_set_rollout(trpo_dev *d, const double *mean, const doubl
     }
     int rc = ensure(&u->roll, &u->roll_cap, n * W, v.stream);
     if (!rc && n) rc = hipMemcpyAsync(u->roll, h, sizeof(double) * n * W, hipMemcpyHostToDevice, v.stream) ? -2 : 0;
-    if (!rc) rc = hipStreamSynchronize(v.stream) ? -2 : 0;
+    if (!rc) rc = trpo_dev_wait_done(d);
     free(h);
     if (rc) return rc;
     u->roll_n = n;
@@ -831,7 +831,7 @@ extern "C" int trpo_dev_get_rollout(trpo_dev *d, double *mean, double *action, d
     double *h = (double *)malloc(sizeof(double) * v.n * W);
     if (!h) return -3;
     int rc = hipMemcpyAsync(h, u->roll, sizeof(double) * v.n * W, hipMemcpyDeviceToHost, v.stream) ? -2 : 0;
-    if (!rc) rc = hipStreamSynchronize(v.stream) ? -2 : 0;
+    if (!rc) rc = trpo_dev_wait_done(d);
     if (!rc)
         for (size_t s = 0; s < v.n; ++s) {
             memcpy(mean + s * A, h + s * W, sizeof(double) * A);
@@ -898,7 +898,7 @@ extern "C" int trpo_dev_policy_gradient(trpo_dev *d, double *b_host, double *adv
     trpo_dev_get_view(d, &v);
     if (b_host) HCHK(hipMemcpyAsync(b_host, v.vec_b, sizeof(double) * v.net.P, hipMemcpyDeviceToHost, v.stream));
     if (adv_sum) HCHK(hipMemcpyAsync(adv_sum, adv_dev, sizeof(double), hipMemcpyDeviceToHost, v.stream));
-    HCHK(hipStreamSynchronize(v.stream));
+    DSYNC(d);
     return 0;
 }
 
@@ -955,7 +955,7 @@ extern "C" int trpo_dev_update_solve(trpo_dev *d, size_t maxiter, double resth, 
     // capture -- not kept)
     int rc = enqueue_update_device(d, maxiter, resth, max_kl, surr);
     if (rc) return rc;
-    HCHK(hipStreamSynchronize(v.stream));
+    DSYNC(d);
     if (surr0) *surr0 = u->hst[3 * P + 2 + H];
     if (stats) memcpy(stats, u->hst + 3 * P + 5 + H, sizeof(double) * TRPO_CG_STATS);
     if (shs_lm) {
@@ -1051,7 +1051,7 @@ extern "C" int trpo_dev_surrogate(trpo_dev *d, const double *fullstep, int k0, i
     if (rc) return rc;
     hipLaunchKernelGGL(copy64_kernel, dim3(1), dim3(64), 0, v.stream, (const double *)u->sums, u->hst_dev + P, nk);
     HCHK(hipGetLastError());
-    HCHK(hipStreamSynchronize(v.stream));
+    DSYNC(d);
     memcpy(surr_host, u->hst + P, sizeof(double) * nk);
     return 0;
 }
