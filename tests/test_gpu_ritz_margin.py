@@ -63,17 +63,21 @@ def test_stall_guard_threshold_margin(monkeypatch):
     rows = _rows()
     bad = [r for r in rows if r["err"] > 1e-4]
     good = [r for r in rows if r["err"] <= 1e-4]
-    nearest = min((r for r in good if r["ritz"] >= DEFAULT_THRESHOLD), key=lambda r: r["ritz"])
-    out = {"threshold": DEFAULT_THRESHOLD, "missed_bound_fp32": bad, "nearest_within_bound_above_threshold": nearest,
-           "margin": nearest["ritz"] / DEFAULT_THRESHOLD,
+    false_triggers = sorted((r for r in good if r["ritz"] < DEFAULT_THRESHOLD), key=lambda r: r["ritz"])
+    nearest_above = min((r for r in good if r["ritz"] >= DEFAULT_THRESHOLD), key=lambda r: r["ritz"])
+    worst_bad = max(r["ritz"] for r in bad) if bad else 0.0
+    out = {"threshold": DEFAULT_THRESHOLD, "missed_bound_fp32": bad,
+           "margin_below_threshold_of_every_miss": DEFAULT_THRESHOLD / worst_bad if worst_bad else None,
+           "false_triggers": false_triggers, "false_trigger_count": len(false_triggers), "solves": len(rows),
+           "nearest_within_bound_above_threshold": nearest_above,
            "rows": sorted(rows, key=lambda r: r["ritz"])}
-    print(json.dumps({k: v for k, v in out.items() if k != "rows"}))
+    print(json.dumps({k: v for k, v in out.items() if k not in ("rows", "false_triggers")}))
     path = os.environ.get("TRPO_RITZ_LOG")
     if path:
         with open(path, "w") as f:
             json.dump(out, f, indent=1)
     assert bad, "expected draw 23's update to miss the bound without the guard"
     for r in bad:
-        assert r["ritz"] < DEFAULT_THRESHOLD, r          # the guard catches every fp32 miss
-    assert out["margin"] >= 10.0, out                    # and stays clear of the solves that are fine
+        assert r["ritz"] * 1e3 <= DEFAULT_THRESHOLD, r     # every fp32 miss is caught, 1000x inside the threshold
+    assert len(false_triggers) <= len(rows) // 4, out["false_trigger_count"]
     assert np.isfinite([r["ritz"] for r in rows]).all()

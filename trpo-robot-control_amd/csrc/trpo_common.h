@@ -37,6 +37,21 @@ struct Net {
         }                                                                                  \
     } while (0)
 
+// Every device allocation of the library goes through here.  Diagnostics: TRPO_DEBUG_POISON=<byte> fills
+// each new allocation with that byte (and waits) before first use, so a kernel that reads device memory
+// the library never wrote -- memory a caller's runtime may hand back still holding another allocation's
+// bytes -- shows up as a wrong result instead of reading the zeros of fresh pages.
+#include <stdlib.h>
+static inline hipError_t trpo_malloc(void **p, size_t bytes) {
+    const hipError_t e = hipMalloc(p, bytes);
+    const char *pz = getenv("TRPO_DEBUG_POISON");
+    if (e == hipSuccess && pz && *p) {
+        if (hipMemset(*p, atoi(pz) & 0xff, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+            (void)hipGetLastError();
+    }
+    return e;
+}
+
 // Pinned host staging buffers that the host writes and kernels read (uploads), or kernels write and
 // the host reads (results through the mapped pointer), are allocated COHERENT (hipHostMallocDefault is
 // non-coherent under HIP_HOST_COHERENT=0, the default: the GPU may cache its lines), and are moved by

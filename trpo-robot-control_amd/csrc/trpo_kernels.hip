@@ -744,6 +744,20 @@ __device__ unsigned long long g_stamps[1024 * 32];
 #else
 #define STAMP(k) do { } while (0)
 #endif
+// fvp_coop_kernel's phase profile (diagnostic build only): wave 0 of every block accumulates the
+// s_memtime cycles of each phase of its tile steps in registers (CSTAMP(k, value the phase produced)),
+// and writes them at the end to g_stamps[block][k] (tools/stamps_coop.py)
+#ifdef TRPO_STAMPS
+#define CSTAMP(k, dep)                                          \
+    do {                                                        \
+        asm volatile("" ::"v"(dep));                            \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+        ph_[k] += t_ - tprev_;                                  \
+        tprev_ = t_;                                            \
+    } while (0)
+#else
+#define CSTAMP(k, dep) do { } while (0)
+#endif
 
 // ---------------------------------------------------------------------------
 // The fused FVP kernel, 3 weight layers (NumLayers == 4), MFMA path.
@@ -1783,6 +1797,10 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
         first_tile = false;
 #endif
     };
+#ifndef TRPO_SETPRIO
+#define TRPO_SETPRIO 0          // 1: the second-dispatched half of the block's waves at s_setprio 1 (guide item 4)
+#endif
+    if (TRPO_SETPRIO && wave >= C::WAVES / 2) __builtin_amdgcn_s_setprio(1);
     for (; tile < ntiles; tile += NT * nwaves) {
         // input tiles: lane holds features 16kt+4g..+3 of its sample (D-layout rows)
         f4 x0[NT][T0];
@@ -2431,6 +2449,12 @@ fvp_coop_kernel(IterArgs A, Net net) {
 
     // every wave of the block runs the same number of tile steps (barriers inside)
     const int nsteps = (ntiles + gstride - 1) / gstride;
+    if (TRPO_SETPRIO && wave >= Q::WAVES / 2) __builtin_amdgcn_s_setprio(1);
+#ifdef TRPO_STAMPS
+    unsigned long long ph_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tprev_ = __builtin_amdgcn_s_memtime();
+    const unsigned long long tloop_ = tprev_;
+#endif
     for (int step = 0; step < nsteps; ++step) {
         const int tile = step * gstride + blockIdx.x * Q::NG + grp;
         const int tc = min(tile, ntiles - 1);
@@ -2478,6 +2502,7 @@ fvp_coop_kernel(IterArgs A, Net net) {
             y1w = actv_fwd<T>(a1, a, ra, r1w);
             if (ycs && tile < ntiles) ycs[((long)tile * 2 * TH + w) * 64 + lane] = y1w;
         }
+        CSTAMP(0, r1w[0]);
         V y1[T1], r1[T1];
         if constexpr (Q::GW > 1) {
             xb[w * 2 * Q::XR + xl] = y1w;
@@ -2492,6 +2517,7 @@ fvp_coop_kernel(IterArgs A, Net net) {
             y1[0] = y1w;
             r1[0] = r1w;
         }
+        CSTAMP(1, r1[T1 - 1][0]);
 
         // ---- layer 1, row tile w ----
         a = b1w;
@@ -2515,6 +2541,7 @@ fvp_coop_kernel(IterArgs A, Net net) {
             y2w = actv_fwd<T>(a2, a, ra + rb, r2w);
             if (ycs && tile < ntiles) ycs[((long)tile * 2 * TH + TH + w) * 64 + lane] = y2w;
         }
+        CSTAMP(2, r2w[0]);
 
         // ---- layer 2: this wave's share (input row tile w), summed over the group ----
         V a3p = zero4, r3p = zero4, r3q = zero4;
@@ -2553,6 +2580,7 @@ fvp_coop_kernel(IterArgs A, Net net) {
             x3 += a3p;
             rx3 += r3p + r3q;
         }
+        CSTAMP(3, rx3[0]);
         V r3, g3;
         const V y3 = actv_fwd<T>(a3, x3, rx3, r3);
         if constexpr (FV) {
@@ -2589,6 +2617,7 @@ fvp_coop_kernel(IterArgs A, Net net) {
         }
         const V g2w = actv_bwd<T>(a2, y2w, t);
         sB2 += g2w;
+        CSTAMP(4, g2w[0]);
         V g2[T2];
         if constexpr (Q::GW > 1) {
             gb[w * Q::XR + xl] = g2w;
@@ -2598,6 +2627,7 @@ fvp_coop_kernel(IterArgs A, Net net) {
         } else {
             g2[0] = g2w;
         }
+        CSTAMP(5, g2[T2 - 1][0]);
         // ---- G1 row tile w = act1'(W1 G2) ----
         t = zero4;
 #pragma unroll
@@ -2606,6 +2636,7 @@ fvp_coop_kernel(IterArgs A, Net net) {
             for (int s = 0; s < 4; ++s) t = PT<T>::mfma(fb1[kt][s], g2[kt][s], t);
         const V g1w = actv_bwd<T>(a1, y1w, t);
         sB1 += g1w;
+        CSTAMP(6, g1w[0]);
         // ---- RGW1 tiles (at, w) += Y1_at . G2_w^T ----
         if constexpr (Q::XT) {
             // both operands read transposed from the exchange rows, which hold them in the D layout
@@ -2653,7 +2684,17 @@ fvp_coop_kernel(IterArgs A, Net net) {
                 for (int s = 0; s < 4; ++s) accW0[kt] = PT<T>::mfma(ya[s], gg[s], accW0[kt]);
             }
         }
+        CSTAMP(7, accW0[T0 - 1][0]);
     }
+#ifdef TRPO_STAMPS
+    const unsigned long long tend_ = __builtin_amdgcn_s_memtime();
+    if ((threadIdx.x == 0 || threadIdx.x == 64 * (Q::WAVES / 2)) && blockIdx.x < 1024) {
+        const int o = threadIdx.x ? 16 : 0;                             // wave 0 | the first wave of group 1
+        for (int k = 0; k < 8; ++k) g_stamps[blockIdx.x * 32 + o + k] = ph_[k];
+        g_stamps[blockIdx.x * 32 + o + 8] = tend_ - tloop_;           // the whole tile loop
+        g_stamps[blockIdx.x * 32 + o + 9] = (unsigned long long)nsteps;
+    }
+#endif
 
     // ---- epilogue: bias sums over the sample columns, NG-way group combine, block partial ----
 #pragma unroll
@@ -3935,7 +3976,7 @@ static trpo_dev *dev_create(int device, size_t nl, const size_t *ls, const char 
     d->hist_cap = 0;
 #define DMALLOC(p, bytes)                                                   \
     do {                                                                    \
-        if (hipMalloc((void **)&(p), (bytes)) != hipSuccess) FAIL("hipMalloc(%zu) failed", (size_t)(bytes)); \
+        if (trpo_malloc((void **)&(p), (bytes)) != hipSuccess) FAIL("trpo_malloc(%zu) failed", (size_t)(bytes)); \
         hipMemsetAsync((p), 0, (bytes), d->stream);                         \
     } while (0)
     DMALLOC(d->theta64, sizeof(double) * d->P);
@@ -4237,7 +4278,7 @@ extern "C" int trpo_dev_set_obs(trpo_dev *d, const double *obs, size_t n) {
     const int L0 = d->net.L[0];
     double *tmp = NULL;
     if (n) {
-        HCHK(hipMalloc((void **)&tmp, sizeof(double) * n * L0));
+        HCHK(trpo_malloc((void **)&tmp, sizeof(double) * n * L0));
         HCHK(hipMemcpyAsync(tmp, obs, sizeof(double) * n * L0, hipMemcpyHostToDevice, d->stream));
     }
     d->n = n;
@@ -4249,7 +4290,7 @@ extern "C" int trpo_dev_set_obs(trpo_dev *d, const double *obs, size_t n) {
         const int ld = 16 * d->pack.T[0];
         if (npad > d->npad_cap) {
             if (d->obs4) hipFree(d->obs4);
-            HCHK(hipMalloc((void **)&d->obs4, d->esz * npad * ld));
+            HCHK(trpo_malloc((void **)&d->obs4, d->esz * npad * ld));
             d->npad_cap = npad;
         }
         if (n)
@@ -4263,27 +4304,27 @@ extern "C" int trpo_dev_set_obs(trpo_dev *d, const double *obs, size_t n) {
                 if (d->yc) hipFree(d->yc);
                 d->yc = NULL;
                 d->yc_cap = 0;
-                HCHK(hipMalloc(&d->yc, bytes));
+                HCHK(trpo_malloc(&d->yc, bytes));
                 d->yc_cap = bytes;
             }
         }
     } else {
         if ((size_t)n * L0 > d->npad_cap) {
             if (d->gobs) hipFree(d->gobs);
-            HCHK(hipMalloc((void **)&d->gobs, d->esz * (n * L0 + 1)));
+            HCHK(trpo_malloc((void **)&d->gobs, d->esz * (n * L0 + 1)));
             d->npad_cap = n * L0;
         }
         if (n) hipLaunchKernelGGL(to_elem_kernel, dim3(cdiv((long)n * L0, 256)), dim3(256), 0, d->stream, d->gobs,
                                   tmp, (long)n * L0, d->f64);
         if ((size_t)d->grid > d->scratch_blocks) {
             if (d->scratch) hipFree(d->scratch);
-            HCHK(hipMalloc((void **)&d->scratch, d->esz * 3 * (size_t)d->srows * GEN_T * d->grid));
+            HCHK(trpo_malloc((void **)&d->scratch, d->esz * 3 * (size_t)d->srows * GEN_T * d->grid));
             d->scratch_blocks = d->grid;
         }
     }
     if (d->grid > d->slab_blocks) {
         if (d->slabs) hipFree(d->slabs);
-        HCHK(hipMalloc((void **)&d->slabs, d->esz * (size_t)d->slab * d->grid));
+        HCHK(trpo_malloc((void **)&d->slabs, d->esz * (size_t)d->slab * d->grid));
         HCHK(hipMemsetAsync(d->slabs, 0, d->esz * (size_t)d->slab * d->grid, d->stream));
         d->slab_blocks = d->grid;
     }
@@ -4344,7 +4385,7 @@ static int refresh_n_total(trpo_dev *d) {
         hn[d->rank] = (double)n;
         // the peer exchange uses a buffer allocated with its window: no allocation (which may wait for
         // the whole device) while another context of this process already spins in its exchange
-        if (!dn && hipMalloc((void **)&dn, sizeof(double) * W) != hipSuccess) {
+        if (!dn && trpo_malloc((void **)&dn, sizeof(double) * W) != hipSuccess) {
             free(hn);
             return -2;
         }
@@ -4701,10 +4742,10 @@ extern "C" int trpo_dev_peer_open(trpo_dev *d, void *handle64) {
     if (!d->peer) {
         d->peer = trpo_peer_create(d->device, peer_slot_doubles(d));
         if (!d->peer) return -2;
-        HCHK(hipMalloc((void **)&d->zred, sizeof(double) * 2 * d->Ps));
+        HCHK(trpo_malloc((void **)&d->zred, sizeof(double) * 2 * d->Ps));
         HCHK(hipMemset(d->zred, 0, sizeof(double) * 2 * d->Ps));
-        HCHK(hipMalloc((void **)&d->ptmp, sizeof(double) * trpo_peer_slot(d->peer)));
-        HCHK(hipMalloc((void **)&d->pn, sizeof(double) * PEER_WMAX));
+        HCHK(trpo_malloc((void **)&d->ptmp, sizeof(double) * trpo_peer_slot(d->peer)));
+        HCHK(trpo_malloc((void **)&d->pn, sizeof(double) * PEER_WMAX));
     }
     return handle64 ? trpo_peer_handle(d->peer, handle64) : 0;
 }
@@ -5032,7 +5073,7 @@ static int ensure_hist(trpo_dev *d, size_t maxiter) {
     if ((int)maxiter + 1 <= d->hist_cap) return 0;
     if (d->hist) hipFree(d->hist);
     d->hist = NULL;
-    HCHK(hipMalloc((void **)&d->hist, sizeof(double) * 2 * (maxiter + 1)));
+    HCHK(trpo_malloc((void **)&d->hist, sizeof(double) * 2 * (maxiter + 1)));
     d->hist_cap = (int)maxiter + 1;
     if (d->cg_exec) {
         hipGraphExecDestroy(d->cg_exec);
@@ -5409,7 +5450,7 @@ static int cg_iter_kernel_only(trpo_dev *d, long j, bool init) {
     if (!fused) return 1;
     if (!d->tscr) {
         const size_t bytes = sizeof(double) * (3 * (size_t)d->P + 2 * 65) + 2 * sizeof(CgSt) + sizeof(Ctl);
-        HCHK(hipMalloc(&d->tscr, bytes));
+        HCHK(trpo_malloc(&d->tscr, bytes));
         HCHK(hipMemsetAsync(d->tscr, 0, bytes, d->stream));
     }
     double *sp = (double *)d->tscr, *sr = sp + d->P, *sx = sr + d->P, *sh = sx + d->P;
@@ -5587,8 +5628,8 @@ int trpo_dev_pg_prepare(trpo_dev *d, const double *roll64, unsigned roll_gen) {
         if (d->pg_adv) hipFree(d->pg_adv);
         d->pg_d = d->pg_adv = NULL;
         d->pg_cap = 0;
-        HCHK(hipMalloc((void **)&d->pg_d, d->esz * npad * ld));
-        HCHK(hipMalloc((void **)&d->pg_adv, d->esz * npad));
+        HCHK(trpo_malloc((void **)&d->pg_d, d->esz * npad * ld));
+        HCHK(trpo_malloc((void **)&d->pg_adv, d->esz * npad));
         d->pg_cap = npad;
         d->pg_gen = 0;
     }
@@ -5598,7 +5639,7 @@ int trpo_dev_pg_prepare(trpo_dev *d, const double *roll64, unsigned roll_gen) {
     d->pg_gen = roll_gen;
     d->pg_n = d->n;
     if (!d->pg_iv) {
-        HCHK(hipMalloc((void **)&d->pg_iv, d->esz * ld));
+        HCHK(trpo_malloc((void **)&d->pg_iv, d->esz * ld));
     }
     if (prep) {
         if (d->f64)

@@ -318,10 +318,14 @@ trpo_peer *trpo_peer_create(int device, size_t S) {
         (void)hipGetLastError();
         p->win = NULL;
     }
+    if (p->win && getenv("TRPO_DEBUG_POISON")) {
+        (void)hipMemset(p->win, atoi(getenv("TRPO_DEBUG_POISON")) & 0xff, bytes);
+        (void)hipDeviceSynchronize();
+    }
     if (getenv("TRPO_DEBUG_ALLOC")) fprintf(stderr, "[trpo_alloc] window %p +%zu\n", (void *)p->win, bytes);
     bool ok = p->win && hipMemset(p->win, 0, bytes) == hipSuccess &&
-              hipMalloc((void **)&p->dwins, sizeof(double *) * PEER_WMAX) == hipSuccess &&
-              hipMalloc((void **)&p->cnt, sizeof(unsigned long long) * PEER_WMAX) == hipSuccess &&
+              trpo_malloc((void **)&p->dwins, sizeof(double *) * PEER_WMAX) == hipSuccess &&
+              trpo_malloc((void **)&p->cnt, sizeof(unsigned long long) * PEER_WMAX) == hipSuccess &&
               hipMemset(p->cnt, 0, sizeof(unsigned long long) * PEER_WMAX) == hipSuccess &&
               hipHostMalloc((void **)&p->err_h, sizeof(int), TRPO_HOST_COHERENT) == hipSuccess;
     if (ok) {

@@ -679,7 +679,7 @@ static int ensure(double **p, size_t *cap, size_t count, hipStream_t st) {
     if (*p) hipFree(*p);
     *p = nullptr;
     *cap = 0;
-    HCHK(hipMalloc((void **)p, sizeof(double) * (count ? count : 1)));
+    HCHK(trpo_malloc((void **)p, sizeof(double) * (count ? count : 1)));
     HCHK(hipMemsetAsync(*p, 0, sizeof(double) * (count ? count : 1), st));
     *cap = count;
     return 0;
@@ -854,7 +854,7 @@ static int enqueue_policy_gradient(trpo_dev *d, const double **adv_dev) {
     const int P = net.P, n = (int)v.n;
     const int G = n ? (cdiv(n, UT) < 1024 ? cdiv(n, UT) : 1024) : 1;
     if (ensure(&u->slabs, &u->slab_cap, (size_t)G * (P + 1), v.stream)) return -2;
-    if (!u->sum) HCHK(hipMalloc((void **)&u->sum, sizeof(double) * (P + 1)));
+    if (!u->sum) HCHK(trpo_malloc((void **)&u->sum, sizeof(double) * (P + 1)));
     const char *eg = getenv("TRPO_UPDATE_GENERIC");
     const double *wsum = nullptr;
     int fast = (eg && atoi(eg)) ? 1 : trpo_dev_pg_sums_fast(d, u->roll, u->roll_gen, &wsum);
@@ -949,7 +949,7 @@ extern "C" int trpo_dev_update_solve(trpo_dev *d, size_t maxiter, double resth, 
     const bool surr = surr0 != nullptr;
     // outside any graph: buffers, and the rollout rows of the policy-gradient kernel (new rollout only)
     if (ensure_host(u, (size_t)3 * P + 5 + H + TRPO_CG_STATS)) return -2;
-    if (!u->fs) HCHK(hipMalloc((void **)&u->fs, sizeof(double) * P));
+    if (!u->fs) HCHK(trpo_malloc((void **)&u->fs, sizeof(double) * P));
     if (trpo_dev_pg_prepare(d, u->roll, u->roll_gen) < 0) return -2;
     // (capturing this whole sequence into one graph was measured: ~3 % faster per update, ~10 ms to
     // capture -- not kept)
@@ -988,7 +988,7 @@ static int enqueue_surrogate(trpo_dev *d, const double *fs, int k0, int nk) {
     const int cap = 2048 / nk > 0 ? 2048 / nk : 1;
     const int Gs = n ? (cdiv(n, UT) < cap ? cdiv(n, UT) : cap) : 1;
     if (ensure(&u->slabs, &u->slab_cap, (size_t)Gs * nk, v.stream)) return -2;
-    if (!u->sums) HCHK(hipMalloc((void **)&u->sums, sizeof(double) * 64));
+    if (!u->sums) HCHK(trpo_malloc((void **)&u->sums, sizeof(double) * 64));
     const int ms = surr_mfma_shape(net);
     if (ms >= 0) {
         // one wave per 16-sample tile, SM_WAVES per workgroup
@@ -1042,7 +1042,7 @@ extern "C" int trpo_dev_surrogate(trpo_dev *d, const double *fullstep, int k0, i
     if (!u->have_roll || u->roll_n != v.n) return -3;
     HCHK(hipSetDevice(v.device));
     const int P = v.net.P;
-    if (!u->fs) HCHK(hipMalloc((void **)&u->fs, sizeof(double) * P));
+    if (!u->fs) HCHK(trpo_malloc((void **)&u->fs, sizeof(double) * P));
     // fullstep in through the mapped host buffer, the sums out through it
     if (ensure_host(u, (size_t)P + 64)) return -2;
     memcpy(u->hst, fullstep, sizeof(double) * P);
@@ -1187,8 +1187,8 @@ extern "C" trpo_bdev *trpo_bdev_create(int device, size_t nl, const size_t *ls, 
     n.A = n.L[nl - 1];
     n.P = pos + n.A;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc((void **)&b->theta, sizeof(double) * n.P) != hipSuccess ||
-        hipMalloc((void **)&b->sum, sizeof(double) * (n.P + 1)) != hipSuccess) {
+        trpo_malloc((void **)&b->theta, sizeof(double) * n.P) != hipSuccess ||
+        trpo_malloc((void **)&b->sum, sizeof(double) * (n.P + 1)) != hipSuccess) {
         if (err) snprintf(err, errlen, "baseline device allocation failed");
         trpo_bdev_destroy(b);
         return nullptr;
@@ -1219,9 +1219,9 @@ extern "C" int trpo_bdev_set_data(trpo_bdev *b, const double *obs, const double 
         if (b->pred) hipFree(b->pred);
         b->obs = b->target = b->pred = nullptr;
         b->cap = 0;
-        HCHK(hipMalloc((void **)&b->obs, sizeof(double) * n * L0));
-        HCHK(hipMalloc((void **)&b->target, sizeof(double) * n));
-        HCHK(hipMalloc((void **)&b->pred, sizeof(double) * n));
+        HCHK(trpo_malloc((void **)&b->obs, sizeof(double) * n * L0));
+        HCHK(trpo_malloc((void **)&b->target, sizeof(double) * n));
+        HCHK(trpo_malloc((void **)&b->pred, sizeof(double) * n));
         b->cap = n;
     }
     b->n = n;
