@@ -213,17 +213,19 @@ double trpo_ctx_cg(trpo_ctx *ctx, const double *b, size_t max_iter, double resid
 int trpo_ctx_cg_history(const trpo_ctx *ctx, double *rdotr, double *xnorm, size_t cap, size_t *iters);
 /* The fp32 stall guard of the last trpo_ctx_cg / trpo_ctx_update (and the file entry points), DESIGN §3:
  * ritz_residual = the smallest relative Ritz residual of the solve's Lanczos matrix (from its CG
- * coefficients); below $TRPO_RITZ_RERUN (default 1e-15) the reference's fp64 CG loses orthogonality and
+ * coefficients); below $TRPO_RITZ_RERUN (default 1e-14) the reference's fp64 CG loses orthogonality and
  * its step is its rounding's, so the solve was repeated in fp64 (*fp64_rerun = 1; one-rank contexts; a
  * "[WARN]" line on stderr).  orth_loss = the largest fraction of a new residual the fp32 path's
  * reorthogonalisation removed.  Any pointer may be NULL.  No reference counterpart. */
 int trpo_ctx_cg_status(const trpo_ctx *ctx, double *ritz_residual, double *orth_loss, int *fp64_rerun);
 
-/* Device-resident benchmarking hooks: b stays in HBM, no host round trip. */
+/* Device-resident benchmarking hooks: b stays in HBM, no host round trip.  trpo_ctx_enqueue_cg is the
+ * plain device solve: the fp32 stall guard (trpo_ctx_cg_status) never re-solves it.  After a
+ * trpo_ctx_cg that the guard re-solved in fp64, slot X (trpo_ctx_download_x) holds the returned fp64 x. */
 int trpo_ctx_upload_b(trpo_ctx *ctx, const double *b);
 int trpo_ctx_upload_v(trpo_ctx *ctx, const double *v);
 int trpo_ctx_enqueue_fvp(trpo_ctx *ctx);                                  /* z = F v */
-int trpo_ctx_enqueue_cg(trpo_ctx *ctx, size_t max_iter, double residual_th); /* graph replay */
+int trpo_ctx_enqueue_cg(trpo_ctx *ctx, size_t max_iter, double residual_th); /* eager, or a graph under RCCL */
 int trpo_ctx_enqueue_fvp_kernel_only(trpo_ctx *ctx);                      /* dominant kernel */
 int trpo_ctx_synchronize(trpo_ctx *ctx);
 /* Average duration (ms) of `reps` back-to-back launches of `what`

@@ -1,9 +1,10 @@
 """Phase profile of the cooperative kernel (fvp_coop_kernel, 2x64 policies) from the stamps build
 (make -C trpo-robot-control_amd stamps): wave 0 and wave 4 (the first waves of the two lane groups) of
 every block accumulate the shader-clock cycles
-(s_memtime) of each phase of its tile steps.  Phases: 0 layer 0 (incl. the wait for the tile's inputs),
-1 exchange y1/r1 (barrier + reads), 2 layer 1, 3 layer 2 + partial-sum exchange, 4 G3 + RGW2 + G2,
-5 exchange g2, 6 G1, 7 RGW1 + RGW0; 8 = the whole tile loop.  Prints the median over blocks of the
+(s_memtime) of each phase of its tile steps.  Phases (round 5, the segments of
+fvp_coop_kernel's tile step): 0 S0 layer 0 (incl. the wait for the tile's inputs), 1 the barrier wait
+before S1, 2 S1 (y1/r1 rows read, layer 1, the layer-2 partial), 3 the wait before S2, 4 S2 (partials
+summed, G3, RGW2, G2), 5 the wait before S3, 6 S3's G1, 7 S3's RGW1 + RGW0; 8 = the whole tile loop.  Prints the median over blocks of the
 cycles per tile step.   usage: python tools/stamps_coop.py [N ...]"""
 import ctypes as C
 import os
@@ -20,7 +21,7 @@ from trpo_amd import synth  # noqa: E402
 L = trpo_amd.lib()
 L.trpo_dev_read_stamps.restype = C.c_int
 L.trpo_dev_read_stamps.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
-NAMES = ["layer0", "xchg y1", "layer1", "layer2+xchg", "g3/RGW2/G2", "xchg g2", "G1", "RGW1+RGW0"]
+NAMES = ["S0 layer0", "wait > S1", "S1 layer1+2", "wait > S2", "S2 g3/RGW2/G2", "wait > S3", "S3 G1", "S3 RGW1+0"]
 layers = [15, 64, 64, 3]
 for n in [int(a) for a in sys.argv[1:]] or [4096, 50000]:
     th = synth.make_theta(layers)
@@ -45,4 +46,7 @@ for n in [int(a) for a in sys.argv[1:]] or [4096, 50000]:
             print("  %-12s %7.0f  (%4.1f %%) | %7.0f  (%4.1f %%)" % (NAMES[k], meds[0][k], 100 * meds[0][k] / meds[0][8],
                                                               meds[1][k], 100 * meds[1][k] / meds[1][8]))
         print("  %-12s %7.0f | %7.0f" % ("loop", meds[0][8], meds[1][8]))
+        pro, epi = np.median(full[:, 10]), np.median(full[:, 11])
+        print("  prologue (entry -> loop) %.0f cycles, epilogue (loop -> slab stored) %.0f cycles, loop total %.0f"
+              % (pro, epi, np.median(full[:, 8])))
         print("  kernel_us(events) %.2f" % (ctx.time_ms(0, 50) * 1e3))

@@ -2214,8 +2214,13 @@ fvp_coop_kernel(IterArgs A, Net net) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     T *ldsT = reinterpret_cast<T *>(lds);
     V *LV = reinterpret_cast<V *>(lds);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // wave index as a wave-uniform (scalar) value: branches on the lane group are then uniform, so a
+    // wave runs only its own group's schedule (the rotated one below) with its own barriers
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int c = lane & 15, g = lane >> 4, grp = wave / Q::GW, w = wave % Q::GW;
+#ifdef TRPO_STAMPS
+    const unsigned long long tentry_ = __builtin_amdgcn_s_memtime();
+#endif
     T *scr = ldsT + 4 * Q::MAIN_V + wave * Q::SCR;
     const int ntiles = A.ntiles, n = A.n;
     const V *obs4 = reinterpret_cast<const V *>(A.obs4);
@@ -2449,25 +2454,29 @@ fvp_coop_kernel(IterArgs A, Net net) {
 
     // every wave of the block runs the same number of tile steps (barriers inside)
     const int nsteps = (ntiles + gstride - 1) / gstride;
-    if (TRPO_SETPRIO && wave >= Q::WAVES / 2) __builtin_amdgcn_s_setprio(1);
+#ifndef TRPO_COOP_PRIO
+#define TRPO_COOP_PRIO TRPO_SETPRIO   // the second lane group (waves WAVES/2 ..) at s_setprio 1
+#endif
+    if (TRPO_COOP_PRIO && wave >= Q::WAVES / 2) __builtin_amdgcn_s_setprio(1);
 #ifdef TRPO_STAMPS
     unsigned long long ph_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long tprev_ = __builtin_amdgcn_s_memtime();
     const unsigned long long tloop_ = tprev_;
 #endif
-    for (int step = 0; step < nsteps; ++step) {
+    // One tile step is four segments separated by the group's three LDS exchanges (block barriers):
+    //   S0 layer 0 (R chain) -> [y1/r1 rows] -> S1 layer 1, the layer-2 partial over this row tile ->
+    //   [layer-2 partials] -> S2 G3, RGW2, G2 -> [g2 rows] -> S3 G1, RGW1, RGW0.
+    // (Round 5 measured running the second lane group one barrier later, so that the two waves of a
+    // SIMD would pair a heavy segment with a light one: slower -- 451 vs 444 us per 2x64 solve at 50k --
+    // and it is not kept; profiles/HISTORY.md.)
+    [[maybe_unused]] V x0[T0], yc1, yc2, y1w, r1w, y1[T1], r1[T1], y2w, r2w, a3p, r3p, r3q, g2w;
+    auto seg0 = [&](int step) __attribute__((always_inline)) {
         const int tile = step * gstride + blockIdx.x * Q::NG + grp;
-        const int tc = min(tile, ntiles - 1);
-        const bool live = tile < ntiles && tc * 16 + c < n;
         const int par = step & 1;
         V *xb = LV + Q::XB + ((par * Q::NG + grp) * TH) * 2 * Q::XR;   // [row tile][2][64 (+4 pad)]
-        V *pb = LV + Q::PB + ((par * Q::NG + grp) * TH) * 128;
-        V *gb = LV + Q::GB + ((par * Q::NG + grp) * TH) * Q::XR;        // [row tile][64 (+4 pad)]
         const int xl = Q::XT ? lane + (lane >> 4) : lane;               // this lane's V in such a row
-        V x0[T0];
 #pragma unroll
         for (int kt = 0; kt < T0; ++kt) x0[kt] = xn[kt];
-        [[maybe_unused]] V yc1, yc2;
         if constexpr (YC) {
             yc1 = yn1;
             yc2 = yn2;
@@ -2484,7 +2493,6 @@ fvp_coop_kernel(IterArgs A, Net net) {
             __builtin_amdgcn_sched_barrier(0);             // keep the prefetch here (see fvp_mlp3_kernel)
 #endif
         }
-
         // ---- layer 0, row tile w ----
         V a = b0w, ra = vb0w;
 #pragma unroll
@@ -2494,7 +2502,6 @@ fvp_coop_kernel(IterArgs A, Net net) {
                 if constexpr (!YC) a = PT<T>::mfma(fa0[kt][s], x0[kt][s], a);
                 if constexpr (FV) ra = PT<T>::mfma(vfa0[kt][s], x0[kt][s], ra);
             }
-        V r1w, y1w;
         if constexpr (YC) {
             y1w = yc1;
             r1w = actv_r<T>(a1, y1w, ra);
@@ -2502,12 +2509,19 @@ fvp_coop_kernel(IterArgs A, Net net) {
             y1w = actv_fwd<T>(a1, a, ra, r1w);
             if (ycs && tile < ntiles) ycs[((long)tile * 2 * TH + w) * 64 + lane] = y1w;
         }
-        CSTAMP(0, r1w[0]);
-        V y1[T1], r1[T1];
         if constexpr (Q::GW > 1) {
             xb[w * 2 * Q::XR + xl] = y1w;
             if constexpr (FV) xb[w * 2 * Q::XR + Q::XR + xl] = r1w;
-            __syncthreads();
+        }
+        CSTAMP(0, r1w[0]);
+    };
+    auto seg1 = [&](int step) __attribute__((always_inline)) {
+        const int tile = step * gstride + blockIdx.x * Q::NG + grp;
+        const int par = step & 1;
+        V *xb = LV + Q::XB + ((par * Q::NG + grp) * TH) * 2 * Q::XR;
+        V *pb = LV + Q::PB + ((par * Q::NG + grp) * TH) * 128;
+        const int xl = Q::XT ? lane + (lane >> 4) : lane;
+        if constexpr (Q::GW > 1) {
 #pragma unroll
             for (int kt = 0; kt < T1; ++kt) {
                 y1[kt] = xb[kt * 2 * Q::XR + xl];
@@ -2517,12 +2531,8 @@ fvp_coop_kernel(IterArgs A, Net net) {
             y1[0] = y1w;
             r1[0] = r1w;
         }
-        CSTAMP(1, r1[T1 - 1][0]);
-
         // ---- layer 1, row tile w ----
-        a = b1w;
-        ra = vb1w;
-        V rb = zero4;
+        V a = b1w, ra = vb1w, rb = zero4;
 #pragma unroll
         for (int kt = 0; kt < T1; ++kt)
 #pragma unroll
@@ -2533,7 +2543,6 @@ fvp_coop_kernel(IterArgs A, Net net) {
                     rb = PT<T>::mfma(vfa1[kt][s], y1[kt][s], rb);
                 }
             }
-        V r2w, y2w;
         if constexpr (YC) {
             y2w = yc2;
             r2w = actv_r<T>(a2, y2w, ra + rb);
@@ -2541,10 +2550,10 @@ fvp_coop_kernel(IterArgs A, Net net) {
             y2w = actv_fwd<T>(a2, a, ra + rb, r2w);
             if (ycs && tile < ntiles) ycs[((long)tile * 2 * TH + TH + w) * 64 + lane] = y2w;
         }
-        CSTAMP(2, r2w[0]);
-
-        // ---- layer 2: this wave's share (input row tile w), summed over the group ----
-        V a3p = zero4, r3p = zero4, r3q = zero4;
+        // ---- layer 2: this wave's share (input row tile w), summed over the group in S2 ----
+        a3p = zero4;
+        r3p = zero4;
+        r3q = zero4;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             if constexpr (NO) {
@@ -2566,11 +2575,22 @@ fvp_coop_kernel(IterArgs A, Net net) {
             r3p = FV ? rowgroup_sum4(r3p + r3q) : zero4;
             r3q = zero4;
         }
-        V x3 = b2, rx3 = vb2;
         if constexpr (Q::GW > 1) {
             pb[w * 128 + lane] = a3p;
             pb[w * 128 + 64 + lane] = r3p + r3q;
-            __syncthreads();
+        }
+        CSTAMP(2, r3p[0]);
+    };
+    auto seg2 = [&](int step) __attribute__((always_inline)) {
+        const int tile = step * gstride + blockIdx.x * Q::NG + grp;
+        const int tc = min(tile, ntiles - 1);
+        const bool live = tile < ntiles && tc * 16 + c < n;
+        const int par = step & 1;
+        V *pb = LV + Q::PB + ((par * Q::NG + grp) * TH) * 128;
+        V *gb = LV + Q::GB + ((par * Q::NG + grp) * TH) * Q::XR;        // [row tile][64 (+4 pad)]
+        const int xl = Q::XT ? lane + (lane >> 4) : lane;
+        V x3 = b2, rx3 = vb2;
+        if constexpr (Q::GW > 1) {
 #pragma unroll
             for (int kt = 0; kt < TH; ++kt) {              // fixed order
                 x3 += pb[kt * 128 + lane];
@@ -2580,7 +2600,6 @@ fvp_coop_kernel(IterArgs A, Net net) {
             x3 += a3p;
             rx3 += r3p + r3q;
         }
-        CSTAMP(3, rx3[0]);
         V r3, g3;
         const V y3 = actv_fwd<T>(a3, x3, rx3, r3);
         if constexpr (FV) {
@@ -2594,7 +2613,6 @@ fvp_coop_kernel(IterArgs A, Net net) {
         // NO: every lane group holds outputs 0..3; the contractions below want rows 4g + r
         const V g3m = (NO && g != 0) ? zero4 : g3;
         if (w == 0) sB3 += g3m;
-
         // ---- RGW2 tile (w, 0) += Y2_w . G3^T ----
         scr_put_t<T>(scr, 0, y2w, c, g);
         scr_put_t<T>(scr, 16, g3m, c, g);
@@ -2615,21 +2633,25 @@ fvp_coop_kernel(IterArgs A, Net net) {
 #pragma unroll
             for (int s = 0; s < 4; ++s) t = PT<T>::mfma(fb2[s], g3[s], t);
         }
-        const V g2w = actv_bwd<T>(a2, y2w, t);
+        g2w = actv_bwd<T>(a2, y2w, t);
         sB2 += g2w;
+        if constexpr (Q::GW > 1) gb[w * Q::XR + xl] = g2w;
         CSTAMP(4, g2w[0]);
+    };
+    auto seg3 = [&](int step) __attribute__((always_inline)) {
+        const int par = step & 1;
+        V *xb = LV + Q::XB + ((par * Q::NG + grp) * TH) * 2 * Q::XR;
+        V *gb = LV + Q::GB + ((par * Q::NG + grp) * TH) * Q::XR;
+        const int xl = Q::XT ? lane + (lane >> 4) : lane;
         V g2[T2];
         if constexpr (Q::GW > 1) {
-            gb[w * Q::XR + xl] = g2w;
-            __syncthreads();
 #pragma unroll
             for (int kt = 0; kt < T2; ++kt) g2[kt] = gb[kt * Q::XR + xl];
         } else {
             g2[0] = g2w;
         }
-        CSTAMP(5, g2[T2 - 1][0]);
         // ---- G1 row tile w = act1'(W1 G2) ----
-        t = zero4;
+        V t = zero4;
 #pragma unroll
         for (int kt = 0; kt < T2; ++kt)
 #pragma unroll
@@ -2659,17 +2681,17 @@ fvp_coop_kernel(IterArgs A, Net net) {
             }
         } else {
 #pragma unroll
-        for (int at = 0; at < T1; ++at) scr_put_t<T>(scr, 16 * at, y1[at], c, g);
-        scr_put_t<T>(scr, 16 * T1, g2w, c, g);
-        {
-            const V gg = scr_get_t<T>(scr, 16 * T1, c, g);
+            for (int at = 0; at < T1; ++at) scr_put_t<T>(scr, 16 * at, y1[at], c, g);
+            scr_put_t<T>(scr, 16 * T1, g2w, c, g);
+            {
+                const V gg = scr_get_t<T>(scr, 16 * T1, c, g);
 #pragma unroll
-            for (int at = 0; at < T1; ++at) {
-                const V ya = scr_get_t<T>(scr, 16 * at, c, g);
+                for (int at = 0; at < T1; ++at) {
+                    const V ya = scr_get_t<T>(scr, 16 * at, c, g);
 #pragma unroll
-                for (int s = 0; s < 4; ++s) accW1[at] = PT<T>::mfma(ya[s], gg[s], accW1[at]);
+                    for (int s = 0; s < 4; ++s) accW1[at] = PT<T>::mfma(ya[s], gg[s], accW1[at]);
+                }
             }
-        }
         }
         // ---- RGW0 tiles (kt0, w) += X0_kt0 . G1_w^T ----
 #pragma unroll
@@ -2685,6 +2707,22 @@ fvp_coop_kernel(IterArgs A, Net net) {
             }
         }
         CSTAMP(7, accW0[T0 - 1][0]);
+    };
+    // the group exchanges' barrier (none with one wave per group)
+    auto xsync = [&]() __attribute__((always_inline)) {
+        if constexpr (Q::GW > 1) __syncthreads();
+    };
+    for (int step = 0; step < nsteps; ++step) {
+        seg0(step);
+        xsync();
+        CSTAMP(1, r1w[0]);
+        seg1(step);
+        xsync();
+        CSTAMP(3, y2w[0]);
+        seg2(step);
+        xsync();
+        CSTAMP(5, g2w[0]);
+        seg3(step);
     }
 #ifdef TRPO_STAMPS
     const unsigned long long tend_ = __builtin_amdgcn_s_memtime();
@@ -2693,6 +2731,7 @@ fvp_coop_kernel(IterArgs A, Net net) {
         for (int k = 0; k < 8; ++k) g_stamps[blockIdx.x * 32 + o + k] = ph_[k];
         g_stamps[blockIdx.x * 32 + o + 8] = tend_ - tloop_;           // the whole tile loop
         g_stamps[blockIdx.x * 32 + o + 9] = (unsigned long long)nsteps;
+        g_stamps[blockIdx.x * 32 + o + 10] = tloop_ - tentry_;        // prologue: entry -> tile loop
     }
 #endif
 
@@ -2741,6 +2780,12 @@ fvp_coop_kernel(IterArgs A, Net net) {
             V *slab4 = reinterpret_cast<V *>(reinterpret_cast<T *>(A.slabs) + (long)blockIdx.x * Q::SLAB);
 #pragma unroll
             for (int k = 0; k < Q::NW; ++k) slab4[(w * Q::NW + k) * 64 + lane] = acc[k];
+#ifdef TRPO_STAMPS
+            if (threadIdx.x == 0 && blockIdx.x < 1024) {        // epilogue: tile loop end -> slab stored
+                asm volatile("" ::"v"(acc[0][0]));
+                g_stamps[blockIdx.x * 32 + 11] = __builtin_amdgcn_s_memtime() - tend_;
+            }
+#endif
         }
     }
 }

@@ -43,6 +43,7 @@
 // barrier.  TRPO_PEER_FENCE=0 restores the fence-free form for A/B.
 #include <hip/hip_runtime.h>
 
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -283,14 +284,56 @@ peer_granule_kernel(const double *__restrict__ in, int R, int Rstride, int count
     if (tid == 0) cnt[t] = e;
 }
 
+// Uncached windows are process-lifetime memory (round 5): a destroyed context's window goes to
+// this pool and the next peer context of the process with the same window size takes it back, instead of
+// returning it to the HIP runtime.  Under the ROCm 7.0 runtime a PyTorch wheel bundles, hipFree of an
+// uncached window left every LATER context of the process computing a wrong first FVP (the same 4.3e-5
+// every run with the granule exchange, 2e-3 .. 5e-3 after peer updates); the probes in
+// profiles/r05_peer_diag/ show it needs the free: leaking the window (TRPO_PEER_KEEP_WINDOW) or keeping
+// the contexts alive removes it, while none of the later context's own buffers lands in the freed range
+// (TRPO_DEBUG_ALLOC) and poisoning every allocation does not change it (TRPO_DEBUG_POISON).
+constexpr int WIN_POOL = 16;
+struct WinSlot {
+    void *p;
+    size_t bytes;
+    int device;
+};
+static pthread_mutex_t g_win_mu = PTHREAD_MUTEX_INITIALIZER;
+static WinSlot g_win_pool[WIN_POOL];
+static int g_win_n = 0;
+
+static void *win_take(int device, size_t bytes) {
+    void *p = NULL;
+    pthread_mutex_lock(&g_win_mu);
+    for (int i = 0; i < g_win_n; ++i)
+        if (g_win_pool[i].device == device && g_win_pool[i].bytes == bytes) {
+            p = g_win_pool[i].p;
+            g_win_pool[i] = g_win_pool[--g_win_n];
+            break;
+        }
+    pthread_mutex_unlock(&g_win_mu);
+    return p;
+}
+
+static void win_give(void *p, size_t bytes, int device) {
+    pthread_mutex_lock(&g_win_mu);
+    const bool kept = g_win_n < WIN_POOL;
+    if (kept) g_win_pool[g_win_n++] = WinSlot{p, bytes, device};
+    pthread_mutex_unlock(&g_win_mu);
+    if (!kept) hipFree(p);              // more than WIN_POOL windows parked at once: give the oldest shape back
+}
+
 static void peer_free(trpo_peer *p) {
     if (!p) return;
     hipSetDevice(p->device);
     for (int r = 0; r < PEER_WMAX; ++r)
         if (p->opened[r]) hipIpcCloseMemHandle(p->opened[r]);
-    // TRPO_PEER_KEEP_WINDOW=1 (diagnostics): leak the window instead of freeing it, so no later
-    // allocation of the process can reuse its pages
-    if (p->win && !getenv("TRPO_PEER_KEEP_WINDOW")) hipFree(p->win);
+    // TRPO_PEER_KEEP_WINDOW=1 (diagnostics): leak the window; TRPO_PEER_FREE_WINDOW=1 (diagnostics): return
+    // it to the runtime as rounds 2-4 did; default: park it in the window pool
+    if (p->win && !getenv("TRPO_PEER_KEEP_WINDOW")) {
+        if (getenv("TRPO_PEER_FREE_WINDOW")) hipFree(p->win);
+        else win_give(p->win, sizeof(double) * win_doubles(p->S), p->device);
+    }
     if (p->dwins) hipFree(p->dwins);
     if (p->cnt) hipFree(p->cnt);
     if (p->err_h) hipHostFree(p->err_h);
@@ -314,7 +357,8 @@ trpo_peer *trpo_peer_create(int device, size_t S) {
     p->fence = !(ef && atoi(ef) == 0);
     const char *eb = getenv("TRPO_PEER_PROTO");
     p->proto = eb ? atoi(eb) : 1;
-    if (hipExtMallocWithFlags((void **)&p->win, bytes, hipDeviceMallocUncached) != hipSuccess) {
+    p->win = (double *)win_take(device, bytes);
+    if (!p->win && hipExtMallocWithFlags((void **)&p->win, bytes, hipDeviceMallocUncached) != hipSuccess) {
         (void)hipGetLastError();
         p->win = NULL;
     }
