@@ -1,10 +1,11 @@
-"""Child process of tests/test_gpu_peer.py::test_peer_slab_paths_torch_runtime_first:
-torch is imported FIRST, so its bundled libamdhip64 serves libtrpo_mi355x.so as well.  Under that runtime a
-peer-attached FVP left later contexts computing wrong FVPs (round-4 bisection), so the library
-refuses the peer exchange there: this script checks that opening a peer window fails with an error (no
-silent wrong result) and that ordinary single contexts stay correct.  With argument "any" and
-TRPO_PEER_ANY_RUNTIME=1 it instead runs the slab-path peer test (the reproduction).
-Exit status 0 = every check passed; prints the runtime in use."""
+"""Child process of tests/test_gpu_peer.py::test_peer_slab_paths_torch_runtime_first: torch is imported
+FIRST, so its bundled libamdhip64 (ROCm 7.0) serves libtrpo_mi355x.so as well.  Under that runtime, in rounds
+2-4, contexts created after peer-attached contexts had been destroyed computed wrong FVPs; round 5 traced it
+to returning the uncached peer window to that runtime (hipFree) and keeps the windows for the life of the
+process instead (profiles/r05_peer_diag/).  This script repeats the round-4 reproduction -- the
+slab-path peer test (2x64 fp32 and fp64: two in-process ranks through peer windows, FVP and the full
+TRPO update against the oracle) twice -- and then checks a fresh single context's FVP.
+Exit status 0 = every check passed; prints the runtime in use and one "ok" line per check."""
 import os
 import sys
 
@@ -29,26 +30,17 @@ import oracle  # noqa: E402
 import test_gpu_peer  # noqa: E402
 from trpo_amd import synth  # noqa: E402
 
-if len(sys.argv) > 1 and sys.argv[1] == "any":
-    for r in range(2):
-        for kind in ("2x64", "fp64"):
-            test_gpu_peer.test_peer_fvp_and_update_slab_paths(kind)
-            print("ok", r, kind, flush=True)
-    raise SystemExit(0)
+for r in range(2):
+    for kind in ("2x64", "fp64"):
+        test_gpu_peer.test_peer_fvp_and_update_slab_paths(kind)
+        print("ok", r, kind, flush=True)
 layers = [15, 64, 64, 3]
 th, obs = synth.make_theta(layers), synth.make_obs(3000, layers[0])
 std = np.ones(3)
 v = synth.make_v(synth.num_params(layers))
 zor, _ = oracle.fvp(layers, "lttl", th, obs, std, v)
-refused = 0
-for r in range(2):
-    with trpo_amd.Context(layers, "lttl", th, obs, std, 0.1) as c:
+with trpo_amd.Context(layers, "lttl", th, obs, std, 0.1) as c:
+    for k in range(2):                      # the first FVP (forward pass recomputed) and a cached one
         e = float(np.linalg.norm(c.fvp(v) - zor) / np.linalg.norm(zor))
         assert e <= 1e-5, e
-        try:
-            c.peer_handle()
-        except trpo_amd.TRPOError as err:
-            refused += 1
-            print("refused:", err, flush=True)
-    print("ok", r, "single-context fvp %.2e" % e, flush=True)
-assert refused == 2 or trpo_amd.runtime_is_built_one(), refused
+        print("ok single-context fvp %d %.2e" % (k, e), flush=True)

@@ -3368,7 +3368,8 @@ cg_axpy_kernel(const double *__restrict__ dots, int G, const double *__restrict_
                const double *__restrict__ p_in, const double *__restrict__ r_in, double *__restrict__ p_out,
                double *__restrict__ r_out, double *__restrict__ x, void *qbuf_v, const void *qz_v, int nq, int reorth,
                int P, int Ps, Ctl *__restrict__ ctl, const CgSt *__restrict__ st_in, CgSt *__restrict__ st_out,
-               double *__restrict__ hist, const int *__restrict__ skip) {
+               double *__restrict__ hist, const int *__restrict__ skip, float *__restrict__ vpk = nullptr,
+               const int *__restrict__ pslot = nullptr) {
 #pragma clang fp contract(off)
     __shared__ double tot[CGS_K];
     QT *Q = reinterpret_cast<QT *>(qbuf_v);
@@ -3401,6 +3402,9 @@ cg_axpy_kernel(const double *__restrict__ dots, int G, const double *__restrict_
     }
     const double2 p2 = reinterpret_cast<const double2 *>(p_in)[tc], r2 = reinterpret_cast<const double2 *>(r_in)[tc];
     const double2 x2 = reinterpret_cast<const double2 *>(x)[tc], z2 = reinterpret_cast<const double2 *>(zbuf)[tc];
+    // vpk: p' also into the fp32 fragment-order direction pack of the next FVP (slots pslot[q], -1 for
+    // LogStd), so its cooperative kernel loads the pack coalesced instead of gathering p' itself
+    const int2 ps2 = vpk ? reinterpret_cast<const int2 *>(pslot)[tc] : make_int2(-1, -1);
     double qv[QCAP][2];
     typedef typename V2T<QT>::type QV2;
 #pragma unroll
@@ -3471,6 +3475,10 @@ cg_axpy_kernel(const double *__restrict__ dots, int G, const double *__restrict_
         x[2 * t] = xo[0];
         r_out[2 * t] = ro2[0];
         p_out[2 * t] = po[0];
+    }
+    if (vpk) {
+        if (2 * t < P && ps2.x >= 0) vpk[ps2.x] = (float)po[0];
+        if (2 * t + 1 < P && ps2.y >= 0) vpk[ps2.y] = (float)po[1];
     }
     if (reorth && it < QCAP) {                            // q_it = r' / |r'|
         const double inv = nr > 0.0 ? 1.0 / sqrt(nr) : 0.0;
@@ -3670,6 +3678,7 @@ struct trpo_dev {
     int coop;
     int coop_fused;             // CG step fused into the cooperative FVP kernel (MODE 2)
     int coop_dist;              // cooperative path: the CG step over slices (cg_dots / cg_axpy), TRPO_COOP_DIST
+    int coop_pk;                // ... cg_axpy also writes p' into the fp32 direction pack (TRPO_COOP_PK, round 5)
     int cinit;                  // cooperative CG start inside the first FVP launch (TRPO_COOP_CINIT, default 1)
     double *zbuf, *dotsbuf;     // its z (natural order, Ps) and per-block partial dots
     fast_launch_fn k_fvp, k_pg; // the tile kernel serving this shape, FVP and policy-gradient modes
@@ -4134,6 +4143,10 @@ static trpo_dev *dev_create(int device, size_t nl, const size_t *ls, const char 
             // mode keeps the fused cooperative step with its direct |r'|^2 reduction
             const char *ed = getenv("TRPO_COOP_DIST");
             d->coop_dist = !d->f64 && !(ed && atoi(ed) == 0);
+            // the FVP after each distributed step loads p' from the fragment-order pack cg_axpy scattered it
+            // into (coalesced) instead of gathering it element by element in every block's prologue
+            const char *epk = getenv("TRPO_COOP_PK");
+            d->coop_pk = d->coop_dist && !(epk && atoi(epk) == 0);
             const char *eci = getenv("TRPO_COOP_CINIT");
             d->cinit = !(eci && atoi(eci) == 0);         // (read for both cooperative CG forms)
             DMALLOC(d->zbuf, sizeof(double) * d->Ps);
@@ -4749,40 +4762,15 @@ static size_t peer_slot_doubles(const trpo_dev *d) {
     return s;
 }
 
-// The peer exchange runs only on the HIP runtime the library was built and rpath-linked against
-// (TRPO_HIP_LIBDIR).  Under the copy a PyTorch wheel bundles (ROCm 7.0's, loaded first by a process that
-// imports torch before this library) one in-process peer-attached FVP left every LATER context of the
-// process computing wrong FVPs (2e-3 .. 5e-3 relative, varying run to run), bisected in round 4
-// (tools/diag/torch_first_bisect.py: two contexts attached through peer windows, one standalone FVP
-// each, then a fresh single context; not with the system runtime, not with the host group, not with the
-// same two contexts driven concurrently unattached, not after plain allocate/free of uncached memory).
-// The cause is not found, so the exchange is refused there instead of risking silent wrong results.
-static int peer_runtime_ok(char *msg, size_t len) {
-#ifdef TRPO_HIP_LIBDIR
-    Dl_info info;
-    char a[4096], b[4096];
-    if (!dladdr(reinterpret_cast<void *>(&hipGetDeviceCount), &info) || !info.dli_fname) return 1;
-    if (!realpath(info.dli_fname, a) || !realpath(TRPO_HIP_LIBDIR, b)) return 1;
-    char *slash = strrchr(a, '/');
-    if (slash) *slash = 0;
-    if (strcmp(a, b) != 0) {
-        snprintf(msg, len, "peer exchange refused: this process runs the HIP runtime in %s, the library was built and "
-                 "validated against %s (load libtrpo_mi355x.so before importing torch)", a, b);
-        return 0;
-    }
-#endif
-    (void)msg;
-    (void)len;
-    return 1;
-}
-
+// Round 4 refused the peer exchange under any HIP runtime but the one the library was built against: under
+// the ROCm 7.0 copy a PyTorch wheel bundles, contexts created AFTER peer-attached contexts had run and been
+// destroyed computed wrong FVPs.  Round 5 found the trigger -- returning the uncached peer window to that
+// runtime (hipFree); none of the later contexts' own buffers reuses the freed range and no kernel reads
+// memory the library never wrote (profiles/r05_peer_diag/) -- and trpo_peer.hip now keeps uncached windows
+// for the life of the process (a pool reused by later peer contexts), so the exchange runs under either
+// runtime (tests/test_gpu_peer.py::test_peer_slab_paths_torch_runtime_first).
 extern "C" int trpo_dev_peer_open(trpo_dev *d, void *handle64) {
     if (!d) return -1;
-    char why[640];
-    if (!getenv("TRPO_PEER_ANY_RUNTIME") && !peer_runtime_ok(why, sizeof why)) {
-        fprintf(stderr, "[trpo_mi355x] %s\n", why);
-        return -4;
-    }
     HCHK(hipSetDevice(d->device));
     if (!d->peer) {
         d->peer = trpo_peer_create(d->device, peer_slot_doubles(d));
@@ -5284,6 +5272,8 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
                 a.reorth = d->reorth;
                 a.q = d->reorth ? d->qbuf : nullptr;
             }
+            // fp32: K_j (j >= 1) reads p_j from the fragment-order pack the previous cg_axpy wrote (PK)
+            if (j > 0 && !d->f64 && d->coop_pk) a.v_nat = nullptr;
             if (d->yc_on) a.yc = reinterpret_cast<float4 *>(d->yc);
             (j > 0 && d->yc_on ? d->k_fvp_yc : d->k_fvp)(dim3(d->grid), d->k_lds, d->stream, a, d->net);
             const int nq = cg_step_nq(d, j);
@@ -5306,7 +5296,8 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
                 hipLaunchKernelGGL(cg_axpy_kernel<float>, dim3(G), dim3(CGS_T), 0, d->stream, d->dotsbuf, G, d->zbuf,
                                    d->pbuf[cur], d->rbuf[cur], d->pbuf[nxt], d->rbuf[nxt], x, qb,
                                    (const void *)d->qzero, d->reorth ? nq : 0, d->reorth, d->P, d->Ps, d->ctl,
-                                   d->st + cur, d->st + nxt, d->hist, done);
+                                   d->st + cur, d->st + nxt, d->hist, done,
+                                   d->coop_pk ? (float *)d->vpack : (float *)nullptr, (const int *)d->pslot);
             }
         }
     } else if (d->coop_fused) {
