@@ -34,6 +34,8 @@ for sname in os.environ.get("SHAPES", "arm,2x64").split(","):
     for r in range(int(os.environ.get("ROUNDS", "5"))):
         for i, c in enumerate(ctxs):
             res[i]["cg"].append(c.time_ms(2, 20, 10, 0.0) * 1e3)
+            c.upload_v(v)          # a CG rewrites the cooperative kernel's direction pack: the FVP rows below
+                                   # time v as its upload packed it (the bench's C2 sequence)
             res[i]["k"].append(c.time_ms(0, 50) * 1e3)
             res[i]["f"].append(c.time_ms(1, 50) * 1e3)
             if sname == "arm":

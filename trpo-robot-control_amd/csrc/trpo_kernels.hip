@@ -2159,6 +2159,22 @@ struct CoopCfg {
     static_assert(LDS_BYTES <= 160 * 1024, "LDS");
 };
 
+// Block-partial (slab) layout of the cooperative kernel.  fp64: the accumulator order in full, NW = T0 + TH + 4
+// vectors of 64 lanes per wave.  fp32 (round 5, COMPACT): the RGW0 / RGW1 tiles in full; the RGW2 tile in
+// full or, with the narrow output layer (NO, <= 4 outputs), only its 16 lanes of output columns c < 4; the
+// three bias rows only from the 4 lanes with c == 0 (after the 16-column sums every other lane holds
+// padding) -- 40 % fewer bytes for the FVP epilogue to store and the slab reduce to read (2x64).
+#ifndef TRPO_COOP_COMPACT
+#define TRPO_COOP_COMPACT 1
+#endif
+template <typename T, int T0, int TH, int NO>
+struct CoopSlab {
+    static constexpr bool COMPACT = sizeof(T) == 4 && TRPO_COOP_COMPACT;
+    static constexpr int A2 = NO ? 16 : 64;                           // V of the RGW2 tile
+    static constexpr int WV = COMPACT ? (T0 + TH) * 64 + A2 + 12 : (T0 + TH + 4) * 64;   // V per wave
+    static constexpr int SLAB = ((TH * WV * 4 + 31) / 32) * 32;      // T per block (reduce: multiple of RS_POS)
+};
+
 // slab position -> natural parameter (or -1) for the cooperative kernel's accumulator order
 // [wave w][k][lane][r], k over RGW0 tiles (kt0, w), RGW1 tiles (at, w), RGW2 tile (w, 0),
 // B1 tile w, B2 tile w, B3 (wave 0 only); p64: the fp64 row permutation.
@@ -2180,9 +2196,33 @@ __device__ __forceinline__ int imap_coop_at(const Net &n, int T0, int TH, int j,
     return (a < n.L[i] && b < n.L[i + 1]) ? n.woff[i] + a * n.L[i + 1] + b : -1;
 }
 
-__global__ void build_imap_coop_kernel(Net n, int T0, int TH, int p64, int *imap, int len) {
+// the same for the fp32 compact slab layout (CoopSlab): position j -> (wave, vector, lane, r) of the full
+// accumulator order, then imap_coop_at
+__device__ __forceinline__ int imap_coop_slab(const Net &n, int T0, int TH, int no, int j, bool p64) {
+    if (p64 || !TRPO_COOP_COMPACT) return imap_coop_at(n, T0, TH, j, p64);
+    const int A2 = no ? 16 : 64, WV = (T0 + TH) * 64 + A2 + 12, NW = T0 + TH + 4;
+    const int w = j / (4 * WV), rem = j % (4 * WV);
+    if (w >= TH) return -1;                               // the block slab's padding
+    const int vi = rem >> 2, r = rem & 3;
+    int k, lane;
+    if (vi < (T0 + TH) * 64) {
+        k = vi >> 6;
+        lane = vi & 63;
+    } else if (vi < (T0 + TH) * 64 + A2) {
+        const int li = vi - (T0 + TH) * 64;
+        k = T0 + TH;
+        lane = no ? (li >> 2) * 16 + (li & 3) : li;        // (g, c < 4)
+    } else {
+        const int li = vi - (T0 + TH) * 64 - A2;
+        k = T0 + TH + 1 + (li >> 2);                      // B1, B2, B3
+        lane = (li & 3) * 16;                             // (g, c = 0)
+    }
+    return imap_coop_at(n, T0, TH, (w * NW + k) * 256 + lane * 4 + r, false);
+}
+
+__global__ void build_imap_coop_kernel(Net n, int T0, int TH, int p64, int no, int *imap, int len) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j < len) imap[j] = imap_coop_at(n, T0, TH, j, p64 != 0);
+    if (j < len) imap[j] = imap_coop_slab(n, T0, TH, no, j, p64 != 0);
 }
 
 // direction-pack element e of the cooperative kernel's tile shape, from a natural-order vector
@@ -2470,6 +2510,20 @@ fvp_coop_kernel(IterArgs A, Net net) {
     // SIMD would pair a heavy segment with a light one: slower -- 451 vs 444 us per 2x64 solve at 50k --
     // and it is not kept; profiles/HISTORY.md.)
     [[maybe_unused]] V x0[T0], yc1, yc2, y1w, r1w, y1[T1], r1[T1], y2w, r2w, a3p, r3p, r3q, g2w;
+    // NOV (round 5, fp32 narrow output): RGW2 as per-lane VALU partials over the lane's own sample column
+    // (hidden 16w + 4g + r x output o), summed over the 16 columns once in the epilogue -- 16 FMAs per tile
+    // instead of two LDS transposes and 4 MFMAs whose 16 columns carried <= 4 outputs
+#ifndef TRPO_COOP_NOV
+#define TRPO_COOP_NOV 1
+#endif
+    constexpr bool NOV = NO != 0 && sizeof(T) == 4 && TRPO_COOP_NOV;
+    [[maybe_unused]] float acc2v[4][NO > 0 ? NO : 1];
+    if constexpr (NOV) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int o = 0; o < (NO > 0 ? NO : 1); ++o) acc2v[r][o] = 0.0f;
+    }
     auto seg0 = [&](int step) __attribute__((always_inline)) {
         const int tile = step * gstride + blockIdx.x * Q::NG + grp;
         const int par = step & 1;
@@ -2614,9 +2668,14 @@ fvp_coop_kernel(IterArgs A, Net net) {
         const V g3m = (NO && g != 0) ? zero4 : g3;
         if (w == 0) sB3 += g3m;
         // ---- RGW2 tile (w, 0) += Y2_w . G3^T ----
-        scr_put_t<T>(scr, 0, y2w, c, g);
-        scr_put_t<T>(scr, 16, g3m, c, g);
-        {
+        if constexpr (NOV) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int o = 0; o < (NO > 0 ? NO : 1); ++o) acc2v[r][o] = fmaf((float)y2w[r], (float)g3[o], acc2v[r][o]);
+        } else {
+            scr_put_t<T>(scr, 0, y2w, c, g);
+            scr_put_t<T>(scr, 16, g3m, c, g);
             const V ya = scr_get_t<T>(scr, 0, c, g), gg = scr_get_t<T>(scr, 16, c, g);
 #pragma unroll
             for (int s = 0; s < 4; ++s) accW2 = PT<T>::mfma(ya[s], gg[s], accW2);
@@ -2742,6 +2801,20 @@ fvp_coop_kernel(IterArgs A, Net net) {
         sB2[r] = PT<T>::rsum16(sB2[r]);
         sB3[r] = PT<T>::rsum16(sB3[r]);
     }
+    if constexpr (NOV) {
+        // the 16 sample columns of each RGW2 partial summed (every lane of the row gets the total); lane
+        // (c, g) keeps output o = c in register r, the accumulator layout of the MFMA form
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            float v = 0.0f;
+#pragma unroll
+            for (int o = 0; o < (NO > 0 ? NO : 1); ++o) {
+                const float t = rowsum16(acc2v[r][o]);
+                v = c == o ? t : v;
+            }
+            accW2[r] = v;
+        }
+    }
     V acc[Q::NW];
     {
         int k = 0;
@@ -2777,9 +2850,25 @@ fvp_coop_kernel(IterArgs A, Net net) {
                     if (m >= 0) unsafeAtomicAdd(dst + m, (double)acc[k][r]);
                 }
         } else {
-            V *slab4 = reinterpret_cast<V *>(reinterpret_cast<T *>(A.slabs) + (long)blockIdx.x * Q::SLAB);
+            using SL = CoopSlab<T, T0, TH, NO>;
+            V *slab4 = reinterpret_cast<V *>(reinterpret_cast<T *>(A.slabs) + (long)blockIdx.x * SL::SLAB);
+            if constexpr (SL::COMPACT) {
+                V *base = slab4 + w * SL::WV;
 #pragma unroll
-            for (int k = 0; k < Q::NW; ++k) slab4[(w * Q::NW + k) * 64 + lane] = acc[k];
+                for (int k = 0; k < T0 + TH; ++k) base[k * 64 + lane] = acc[k];
+                if constexpr (NO != 0) {
+                    if (c < 4) base[(T0 + TH) * 64 + g * 4 + c] = acc[T0 + TH];
+                } else {
+                    base[(T0 + TH) * 64 + lane] = acc[T0 + TH];
+                }
+                if (c == 0) {
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) base[(T0 + TH) * 64 + SL::A2 + i * 4 + g] = acc[T0 + TH + 1 + i];
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < Q::NW; ++k) slab4[(w * Q::NW + k) * 64 + lane] = acc[k];
+            }
 #ifdef TRPO_STAMPS
             if (threadIdx.x == 0 && blockIdx.x < 1024) {        // epilogue: tile loop end -> slab stored
                 asm volatile("" ::"v"(acc[0][0]));
@@ -3651,7 +3740,7 @@ struct CoopEntry {
     {sizeof(T) == 8, t0, th, act, no, coop_launch<T, t0, th, act, 0, no>, coop_launch<T, t0, th, act, 1, no>,     \
      coop_launch<T, t0, th, act, 2, no>, coop_yc_launch<T, t0, th, act, 3, no>(),                                \
      coop_yc_launch<T, t0, th, act, 4, no>(), coop_attr<T, t0, th, act, no>, CoopCfg<T, t0, th>::LDS_BYTES,      \
-     CoopCfg<T, t0, th>::SLAB, CoopCfg<T, t0, th>::NG, CoopCfg<T, t0, th>::THREADS, CoopCfg<T, t0, th>::MAIN_BYTES}
+     CoopSlab<T, t0, th, no>::SLAB, CoopCfg<T, t0, th>::NG, CoopCfg<T, t0, th>::THREADS, CoopCfg<T, t0, th>::MAIN_BYTES}
 #define COOP_ENTRY(T, t0, th, act) COOP_ENTRY_NO(T, t0, th, act, 0)
 #define COOP_SHAPE(T, t0, th) COOP_ENTRY(T, t0, th, ACT_TTL), COOP_ENTRY(T, t0, th, -1)
 #define COOP_SHAPE_NO(t0, th) COOP_ENTRY_NO(float, t0, th, ACT_TTL, 4), COOP_ENTRY_NO(float, t0, th, -1, 4)
@@ -3679,6 +3768,8 @@ struct trpo_dev {
     int coop_fused;             // CG step fused into the cooperative FVP kernel (MODE 2)
     int coop_dist;              // cooperative path: the CG step over slices (cg_dots / cg_axpy), TRPO_COOP_DIST
     int coop_pk;                // ... cg_axpy also writes p' into the fp32 direction pack (TRPO_COOP_PK, round 5)
+    int vpack_v;                // the fp32 direction pack holds slot V (written by its upload; any other
+                                // writer of the pack -- a CG, a gathered FVP -- clears it)
     int cinit;                  // cooperative CG start inside the first FVP launch (TRPO_COOP_CINIT, default 1)
     double *zbuf, *dotsbuf;     // its z (natural order, Ps) and per-block partial dots
     fast_launch_fn k_fvp, k_pg; // the tile kernel serving this shape, FVP and policy-gradient modes
@@ -4153,7 +4244,7 @@ static trpo_dev *dev_create(int device, size_t nl, const size_t *ls, const char 
             DMALLOC(d->dotsbuf, sizeof(double) * CGS_K * cdiv(d->Ps / 2, CGS_T));
             DMALLOC(d->imap, sizeof(int) * d->slab);
             hipLaunchKernelGGL(build_imap_coop_kernel, dim3(cdiv(d->slab, 256)), dim3(256), 0, d->stream, n, T[0],
-                               T[1], d->f64, d->imap, d->slab);
+                               T[1], d->f64, d->coop_e->no, d->imap, d->slab);
         } else {
             DMALLOC(d->imap, sizeof(int) * d->slab);
             hipLaunchKernelGGL(build_imap_kernel, dim3(cdiv(d->slab, 256)), dim3(256), 0, d->stream, n, pk, d->imap,
@@ -4841,6 +4932,19 @@ __global__ void vcopy64_kernel(const double *__restrict__ src, double *__restric
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) dst[i] = src[i];
 }
+// the upload of a direction for the cooperative kernel: the natural-order copy, and the same values in the
+// fp32 fragment-order pack (slot pslot[i], -1 for LogStd), so the FVP loads the pack coalesced instead of
+// every block gathering it (round 5; the CG's cg_axpy does the same for p')
+__global__ void vcopy_pack_kernel(const double *__restrict__ src, double *__restrict__ dst, int n,
+                                  float *__restrict__ vpk, const int *__restrict__ pslot) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const double v = src[i];
+        dst[i] = v;
+        const int s = pslot[i];
+        if (s >= 0) vpk[s] = (float)v;
+    }
+}
 // host_writes: the caller is about to write the buffer from the host (an upload); device-side
 // writers (downloads) are ordered after a pending upload's copy by the stream and need no wait
 static int ensure_hst(trpo_dev *d, size_t count, bool host_writes = false) {
@@ -4863,8 +4967,14 @@ extern "C" int trpo_dev_upload(trpo_dev *d, int slot, const double *host) {
     HCHK(hipSetDevice(d->device));
     if (ensure_hst(d, (size_t)d->P + 2 * (size_t)(d->hist_cap + 8), true)) return -2;
     memcpy(d->hst, host, sizeof(double) * d->P);
-    hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, (const double *)d->hst_dev,
-                       d->vec[slot], d->P);
+    if (slot == TRPO_VEC_V && d->coop_pk) {
+        hipLaunchKernelGGL(vcopy_pack_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream,
+                           (const double *)d->hst_dev, d->vec[slot], d->P, (float *)d->vpack, (const int *)d->pslot);
+        d->vpack_v = 1;
+    } else {
+        hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, (const double *)d->hst_dev,
+                           d->vec[slot], d->P);
+    }
     HCHK(hipGetLastError());
     // no wait here: the stream orders the copy before every later kernel, and the next host-side
     // write to the staging buffer (ensure_hst) waits for it
@@ -5040,7 +5150,7 @@ static int fvp_src(trpo_dev *d, const double *src, double **zh) {
         // two launches: the tile kernel gathers its direction fragments from v itself, then the
         // atomic-replica or slab reduce applies the epilogue (under RCCL after the all-reduce)
         IterArgs a = plain_args(d, &d->ctl->zero);
-        a.v_nat = src;
+        a.v_nat = (d->coop_pk && d->vpack_v && src == d->vec[TRPO_VEC_V]) ? nullptr : src;   // packed at upload
         double *acc = launch_fvp_plain(d, a);
         if (acc) {
             if (allreduce(d, acc, (size_t)d->Rc * d->Ps)) return -4;
@@ -5054,9 +5164,11 @@ static int fvp_src(trpo_dev *d, const double *src, double **zh) {
         HCHK(hipGetLastError());
         return 0;
     }
-    if (d->fast)
+    if (d->fast) {
         hipLaunchKernelGGL(gather_pack_kernel, dim3(cdiv(d->pack.vlen, 256)), dim3(256), 0, d->stream, d->vpack,
                            src, d->vmap, d->pack.vlen, d->f64);
+        d->vpack_v = src == d->vec[TRPO_VEC_V];
+    }
     int rc = enqueue_fvp_core(d, src, &d->ctl->zero);
     if (rc) return rc;
     hipLaunchKernelGGL(fvp_epilogue_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, d->zacc,
@@ -5093,7 +5205,7 @@ extern "C" int trpo_dev_fvp_kernel(trpo_dev *d) {
     HCHK(hipSetDevice(d->device));
     if (d->fast) {
         IterArgs a = plain_args(d, &d->ctl->zero);
-        a.v_nat = d->vec[TRPO_VEC_V];                  // the same launch as the FVP call's
+        a.v_nat = (d->coop_pk && d->vpack_v) ? nullptr : d->vec[TRPO_VEC_V];   // as the FVP call's launch
         launch_fvp_plain(d, a, true);                  // no epilogue follows: accumulate into the sink
     } else {
         launch_generic(d, &d->ctl->zero);
@@ -5157,6 +5269,7 @@ static int cg_step_nq(const trpo_dev *d, long sin_iter) {
 // CG(maxiter) as a straight-line launch sequence (captured into a hipGraph by trpo_dev_cg).
 // Fast path: init, K_0 .. K_{M-1} (K_j fuses CG step j-1 -> j with FVP j), final step.
 static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
+    d->vpack_v = 0;                                    // the CG kernels write the direction pack
     double *x = d->vec[TRPO_VEC_X], *b = d->vec[TRPO_VEC_B];
     const int E = cg_E(d->P);
     const int vlen = d->fast ? d->pack.vlen : 0;
