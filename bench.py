@@ -44,7 +44,9 @@ DAMPING = 0.1
 PEAK_FP32_TFLOPS = 157.3     # MI355X dense FP32 (vector = matrix), MI355X_MICROARCH.md
 PEAK_FP64_TFLOPS = 78.6      # MI355X dense fp64 matrix (AMD spec sheet; the guide lists fp32/bf16 only)
 PEAK_HBM_GBS = 8000.0
-SWEEP_N = (500_000, 4_000_000)   # the latency crossover of the sharded solve
+# the latency crossover of the sharded solve; 6 250 and 500 000 are the per-rank shards of
+# the 50k headline and of 4M at 8 GPUs (the one-GPU inputs of DESIGN §6.1's 8-GPU model)
+SWEEP_N = (6_250, 500_000, 4_000_000)
 
 
 def parse_args():
