@@ -134,6 +134,7 @@ struct IterArgs {
     void *q;                      // QT [QCAP][P]: float (fp32 kernels) or double (fp64 mode)
     const void *qz;
     int nq, reorth;
+    int gmaj;                     // cooperative kernel: group-major tile order (TRPO_COOP_GMAJ)
 };
 
 // fixed-order block-wide fp64 sum (every thread gets the result)
@@ -2271,12 +2272,16 @@ fvp_coop_kernel(IterArgs A, Net net) {
     // the first tile's observations are issued with the prologue loads; later tiles are
     // prefetched one step ahead (clamped: every load unconditional)
     const int gstride = gridDim.x * Q::NG;
+    // this group's first tile: block-major (blocks 0, 1, .. take NG consecutive tiles) or, with A.gmaj,
+    // group-major (every block's group 0 first): at fewer tiles than groups the busy groups then sit
+    // one per block, one wave per SIMD, instead of two per block on half the CUs (round 5)
+    const int gbase = A.gmaj ? grp * (int)gridDim.x + (int)blockIdx.x : (int)blockIdx.x * Q::NG + grp;
     V xn[T0];
     [[maybe_unused]] V yn1, yn2;                          // cached y1, y2 row tiles of the next tile
     const V *ycl = reinterpret_cast<const V *>(A.yc);
     V *ycs = MODE == 0 ? reinterpret_cast<V *>(A.yc) : nullptr;   // cache writer
     {
-        const int tc0 = min(blockIdx.x * Q::NG + grp, ntiles - 1);
+        const int tc0 = min(gbase, ntiles - 1);
 #pragma unroll
         for (int kt = 0; kt < T0; ++kt) xn[kt] = obs4[(long)(tc0 * 16 + c) * (4 * T0) + kt * 4 + g];
         if constexpr (YC) {
@@ -2525,7 +2530,7 @@ fvp_coop_kernel(IterArgs A, Net net) {
             for (int o = 0; o < (NO > 0 ? NO : 1); ++o) acc2v[r][o] = 0.0f;
     }
     auto seg0 = [&](int step) __attribute__((always_inline)) {
-        const int tile = step * gstride + blockIdx.x * Q::NG + grp;
+        const int tile = step * gstride + gbase;
         const int par = step & 1;
         V *xb = LV + Q::XB + ((par * Q::NG + grp) * TH) * 2 * Q::XR;   // [row tile][2][64 (+4 pad)]
         const int xl = Q::XT ? lane + (lane >> 4) : lane;               // this lane's V in such a row
@@ -2570,7 +2575,7 @@ fvp_coop_kernel(IterArgs A, Net net) {
         CSTAMP(0, r1w[0]);
     };
     auto seg1 = [&](int step) __attribute__((always_inline)) {
-        const int tile = step * gstride + blockIdx.x * Q::NG + grp;
+        const int tile = step * gstride + gbase;
         const int par = step & 1;
         V *xb = LV + Q::XB + ((par * Q::NG + grp) * TH) * 2 * Q::XR;
         V *pb = LV + Q::PB + ((par * Q::NG + grp) * TH) * 128;
@@ -2636,7 +2641,7 @@ fvp_coop_kernel(IterArgs A, Net net) {
         CSTAMP(2, r3p[0]);
     };
     auto seg2 = [&](int step) __attribute__((always_inline)) {
-        const int tile = step * gstride + blockIdx.x * Q::NG + grp;
+        const int tile = step * gstride + gbase;
         const int tc = min(tile, ntiles - 1);
         const bool live = tile < ntiles && tc * 16 + c < n;
         const int par = step & 1;
@@ -2772,16 +2777,19 @@ fvp_coop_kernel(IterArgs A, Net net) {
         if constexpr (Q::GW > 1) __syncthreads();
     };
     for (int step = 0; step < nsteps; ++step) {
-        seg0(step);
+        // a group past the last tile skips its segments (wave-uniform; it still joins the block's
+        // barriers): its masked products would add exact zeros, so only its SIMD partner's time changes
+        const bool act = step * gstride + gbase < ntiles;
+        if (act) seg0(step);
         xsync();
         CSTAMP(1, r1w[0]);
-        seg1(step);
+        if (act) seg1(step);
         xsync();
         CSTAMP(3, y2w[0]);
-        seg2(step);
+        if (act) seg2(step);
         xsync();
         CSTAMP(5, g2w[0]);
-        seg3(step);
+        if (act) seg3(step);
     }
 #ifdef TRPO_STAMPS
     const unsigned long long tend_ = __builtin_amdgcn_s_memtime();
@@ -3451,6 +3459,102 @@ cg_dots_kernel(const double *__restrict__ zacc, const double *__restrict__ p, co
     }
 }
 
+// One rank (no all-reduce between the slab reduce and the step): reduce_slabs_kernel<float> and
+// cg_dots_kernel in ONE launch (round 5; TRPO_COOP_RDOTS=0 keeps the two).  Block b reduces its RS_POS
+// slab positions exactly as reduce_slabs_kernel does (same loads, same fixed order, the same zacc
+// bits), then its threads t < RS_POS that hold a parameter (m = imap[.] >= 0) and, in block 0, the
+// threads RS_POS + k (k < P - nw) that hold the log-std entries form z = a / N + lambda p (2p + lambda p)
+// as cg_dots_kernel does, store it to zbuf and contribute the partial dots p.z, r.z, z.z, x.p, p.p,
+// q_i.z -> dots[b][CGS_K] (cg_axpy_kernel sums the slab/RS_POS partials in block order).  The gathers
+// of p, r, x and the basis at the block's natural indices are issued between the slab loads and
+// their sums, so they add no round trip.  Only the dots' partition differs from the two-kernel form.
+template <typename QT>
+__global__ void __launch_bounds__(RS_THREADS)
+reduce_dots_kernel(const float *__restrict__ slabs, int G, int slab, const int *__restrict__ imap,
+                   double *__restrict__ zacc, const double *__restrict__ p, const double *__restrict__ r,
+                   const double *__restrict__ x, double *__restrict__ zbuf, double *__restrict__ dots,
+                   const void *qbuf_v, const void *qz_v, int nq, int P, int Ps, int nw,
+                   const Ctl *__restrict__ ctl, const int *__restrict__ skip) {
+#pragma clang fp contract(off)
+    constexpr int VE = 4, LP = RS_POS / VE, SG = RS_THREADS / LP, NLD = 256 / SG;
+    typedef float VT __attribute__((ext_vector_type(VE)));
+    __shared__ double part[SG][RS_POS + 1];
+    __shared__ double sh[32 * (RS_THREADS / 64)];
+    const QT *Q = reinterpret_cast<const QT *>(qbuf_v);
+    const QT *qz = reinterpret_cast<const QT *>(qz_v);
+    const int t = threadIdx.x, lp = t % LP, sg = t / LP;
+    const int j0 = blockIdx.x * RS_POS + lp * VE;
+    const int m = t < RS_POS ? imap[blockIdx.x * RS_POS + t] : -1;
+    // this thread's parameter: a slab position's, a log-std entry (block 0), or none (-1)
+    const int kls = t - RS_POS;
+    if (*skip) return;                                    // grid-uniform
+    VT v[NLD];
+#pragma unroll
+    for (int k = 0; k < NLD; ++k) {                       // the first load round (all of it for G <= 256)
+        const int b = sg + SG * k;
+        v[k] = b < G ? *reinterpret_cast<const VT *>(slabs + (long)b * slab + j0) : (VT)0;
+    }
+    const int q = t < RS_POS ? m : (blockIdx.x == 0 && kls >= 0 && kls < P - nw ? nw + kls : -1);
+    const int qc = min(max(q, 0), P - 1);
+    const double p0 = p[qc], r0 = r[qc], x0 = x[qc];
+    double qv[QCAP];
+#pragma unroll
+    for (int i = 0; i < QCAP; ++i) {
+        const bool ok = i < nq;
+        const QT qq = ok ? Q[(long)i * Ps + qc] : qz[t & 7];
+        qv[i] = ok ? (double)qq : 0.0;
+    }
+    double s[VE];
+#pragma unroll
+    for (int e = 0; e < VE; ++e) s[e] = 0.0;
+#pragma unroll
+    for (int k = 0; k < NLD; ++k)
+#pragma unroll
+        for (int e = 0; e < VE; ++e) s[e] += (double)v[k][e];
+    for (int b0 = sg + SG * NLD; b0 < G; b0 += SG * NLD) {   // G > 256 block partials
+#pragma unroll
+        for (int k = 0; k < NLD; ++k) {
+            const int b = b0 + SG * k;
+            v[k] = b < G ? *reinterpret_cast<const VT *>(slabs + (long)b * slab + j0) : (VT)0;
+        }
+#pragma unroll
+        for (int k = 0; k < NLD; ++k)
+#pragma unroll
+            for (int e = 0; e < VE; ++e) s[e] += (double)v[k][e];
+    }
+#pragma unroll
+    for (int e = 0; e < VE; ++e) part[sg][lp * VE + e] = s[e];
+    __syncthreads();
+    double a = 0.0;
+    if (t < RS_POS) {
+#pragma unroll 8
+        for (int k = 0; k < SG; ++k) a += part[k][t];
+        if (m >= 0) zacc[m] = a;
+    }
+    const double cn = ctl->n_total, lam = ctl->damping;
+    double red[CGS_K];
+#pragma unroll
+    for (int k = 0; k < CGS_K; ++k) red[k] = 0.0;
+    if (q >= 0) {
+        const double zv = __builtin_fma(lam, p0, q < nw ? a / cn : 2.0 * p0);
+        zbuf[q] = zv;
+        red[0] = p0 * zv;
+        red[1] = r0 * zv;
+        red[2] = zv * zv;
+        red[3] = x0 * p0;
+        red[4] = p0 * p0;
+#pragma unroll
+        for (int i = 0; i < QCAP; ++i) red[5 + i] = qv[i] * zv;
+    }
+    block_sums_dpp<CGS_K, RS_THREADS / 64>(red, sh);
+    if (t < CGS_K) {
+        double o = red[0];
+#pragma unroll
+        for (int k = 1; k < CGS_K; ++k) o = t == k ? red[k] : o;
+        dots[(long)blockIdx.x * CGS_K + t] = o;
+    }
+}
+
 template <typename QT>
 __global__ void __launch_bounds__(CGS_T)
 cg_axpy_kernel(const double *__restrict__ dots, int G, const double *__restrict__ zbuf,
@@ -3768,6 +3872,9 @@ struct trpo_dev {
     int coop_fused;             // CG step fused into the cooperative FVP kernel (MODE 2)
     int coop_dist;              // cooperative path: the CG step over slices (cg_dots / cg_axpy), TRPO_COOP_DIST
     int coop_pk;                // ... cg_axpy also writes p' into the fp32 direction pack (TRPO_COOP_PK, round 5)
+    int coop_rdots;             // ... one rank: slab reduce + dots in one launch (TRPO_COOP_RDOTS, round 5)
+    int coop_gmaj;              // cooperative kernel: group-major tile order (TRPO_COOP_GMAJ: 1 on, 0 off, unset auto)
+    int gmaj_on;                // ... in effect for the current sample count (choose_grid)
     int vpack_v;                // the fp32 direction pack holds slot V (written by its upload; any other
                                 // writer of the pack -- a CG, a gathered FVP -- clears it)
     int cinit;                  // cooperative CG start inside the first FVP launch (TRPO_COOP_CINIT, default 1)
@@ -4241,7 +4348,14 @@ static trpo_dev *dev_create(int device, size_t nl, const size_t *ls, const char 
             const char *eci = getenv("TRPO_COOP_CINIT");
             d->cinit = !(eci && atoi(eci) == 0);         // (read for both cooperative CG forms)
             DMALLOC(d->zbuf, sizeof(double) * d->Ps);
-            DMALLOC(d->dotsbuf, sizeof(double) * CGS_K * cdiv(d->Ps / 2, CGS_T));
+            const char *egm = getenv("TRPO_COOP_GMAJ");
+            d->coop_gmaj = egm ? (atoi(egm) != 0) : -1;
+            const char *erd = getenv("TRPO_COOP_RDOTS");
+            d->coop_rdots = d->coop_dist && !(erd && atoi(erd) == 0) && d->P - d->nw <= RS_THREADS - RS_POS;
+            {
+                const int gd = cdiv(d->Ps / 2, CGS_T), gr = d->slab / RS_POS;   // cg_dots / reduce_dots partials
+                DMALLOC(d->dotsbuf, sizeof(double) * CGS_K * (gd > gr ? gd : gr));
+            }
             DMALLOC(d->imap, sizeof(int) * d->slab);
             hipLaunchKernelGGL(build_imap_coop_kernel, dim3(cdiv(d->slab, 256)), dim3(256), 0, d->stream, n, T[0],
                                T[1], d->f64, d->coop_e->no, d->imap, d->slab);
@@ -4407,7 +4521,13 @@ static int choose_grid(trpo_dev *d) {
     const char *e = getenv("TRPO_FVP_BLOCKS");
     if (d->fast) {
         const int ntiles = cdiv((long)d->n, 16);
-        int g = cdiv(ntiles, d->k_tiles);
+        // cooperative kernel, group-major tiles (A.gmaj): by default only when the grid is full either
+        // way (ntiles >= groups of a full grid) -- below that, group-major spreads the busy groups one per
+        // block over up to twice the blocks: 2x64 N = 4 096 kernel 8.47 -> 7.65 us, but the slab reduce
+        // then reads twice the block partials and the FVP call / CG get slower (11.93 -> 12.25 us,
+        // 205.8 -> 208.7 us; profiles/r05_ab_coop.log); TRPO_COOP_GMAJ=1 / 0 forces it on / off
+        d->gmaj_on = d->coop && (d->coop_gmaj > 0 || (d->coop_gmaj < 0 && ntiles >= d->k_tiles * cus));
+        int g = cdiv(ntiles, d->gmaj_on ? 1 : d->k_tiles);
         if (g > cus) g = cus;
         if (e && atoi(e) > 0) g = atoi(e);
         return g < 1 ? 1 : g;
@@ -5061,6 +5181,7 @@ static IterArgs plain_args(trpo_dev *d, const int *skip) {
     a.skip = skip;
     a.R_out = 1;
     a.R_in = 1;
+    a.gmaj = d->gmaj_on;
     return a;
 }
 
@@ -5262,6 +5383,9 @@ static fast_launch_fn cg_iter_kernel(trpo_dev *d, const IterArgs &a) {
     return d->k_cg_yc_q[qb_index(a.nq)];
 }
 // arguments of the last CG step (after FVP M-1) and of every step of the unfused paths
+// the distributed cooperative step with no collective attached: reduce_dots_kernel replaces the slab
+// reduce + cg_dots pair (with a collective the all-reduce sits between them)
+static bool coop_rdots(const trpo_dev *d) { return d->coop_rdots && !d->comm && !d->group && !d->peer_on; }
 static int cg_step_nq(const trpo_dev *d, long sin_iter) {
     return d->reorth ? (int)(sin_iter < QCAP ? sin_iter : QCAP) : 0;
 }
@@ -5391,6 +5515,19 @@ static int enqueue_cg_body(trpo_dev *d, size_t maxiter, double resth) {
             (j > 0 && d->yc_on ? d->k_fvp_yc : d->k_fvp)(dim3(d->grid), d->k_lds, d->stream, a, d->net);
             const int nq = cg_step_nq(d, j);
             void *qb = d->reorth ? d->qbuf : (void *)d->qzero;
+            if (coop_rdots(d)) {                            // one rank: the reduce and the dots in one launch
+                const int GR = d->slab / RS_POS;
+                hipLaunchKernelGGL(reduce_dots_kernel<float>, dim3(GR), dim3(RS_THREADS), 0, d->stream,
+                                   (const float *)d->slabs, d->grid, d->slab, d->imap, d->zacc, d->pbuf[cur],
+                                   d->rbuf[cur], x, d->zbuf, d->dotsbuf, (const void *)qb, (const void *)d->qzero,
+                                   d->reorth ? nq : 0, d->P, d->Ps, d->nw, d->ctl, done);
+                hipLaunchKernelGGL(cg_axpy_kernel<float>, dim3(G), dim3(CGS_T), 0, d->stream, d->dotsbuf, GR, d->zbuf,
+                                   d->pbuf[cur], d->rbuf[cur], d->pbuf[nxt], d->rbuf[nxt], x, qb,
+                                   (const void *)d->qzero, d->reorth ? nq : 0, d->reorth, d->P, d->Ps, d->ctl,
+                                   d->st + cur, d->st + nxt, d->hist, done,
+                                   d->coop_pk ? (float *)d->vpack : (float *)nullptr, (const int *)d->pslot);
+                continue;
+            }
             launch_reduce(d, done);
             int rc = allreduce(d, d->zacc, d->nw);
             if (rc) return rc;
