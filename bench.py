@@ -644,7 +644,7 @@ def extras_single(device, dist, reps, lock=None):
                 # per-iteration tile kernel is the standalone cached-forward FVP kernel (MODE 3)
                 ctx.upload_v(synth.make_v(num_params(L)))
                 k3 = ctx.time_ms(0, 50)
-                kdesc = " (FVP kernel, cached forward; per iteration + slab reduce + cg_dots + cg_axpy)"
+                kdesc = " (FVP kernel, cached forward; per iteration + slab reduce with the CG dots (one rank) + cg_axpy)"
             else:
                 k3 = ctx.time_ms(3, 10, CG_ITERS)
                 kdesc = " (CG-iteration kernel, cached forward)"

@@ -3306,7 +3306,7 @@ cg_update_kernel(const double *__restrict__ acc, int R_in, const double *__restr
 // basis streamed twice) re-reads ~(4 + 2 nq) P-vectors per block -- at P = 5 443 that is 0.2-0.6 MB
 // per CU per iteration.  Here the step is split over natural-order slices instead:
 //   cg_dots_kernel : z = zacc / N + lambda p (log-std block 2p + lambda p) for its slice, and the
-//                    slice's partial dots p.z, r.z, z.z, x.p, p.p, q_i.z (i < nq) -> dots[block][21]
+//                    slice's partial dots p.z, r.z, z.z, x.p, p.p, q_i.z (i < nq) -> dots (DOTS_AT)
 //   cg_axpy_kernel : every block sums the partial dots over the blocks in block order (fixed order:
 //                    every block gets the same bits), forms alpha, the reorthogonalisation
 //                    coefficients, |r'|^2 and beta as in the fused step, and updates its slice:
@@ -3405,6 +3405,13 @@ cg_last_kernel(const double *__restrict__ acc, int R_in, const double *__restric
 #define TRPO_CGS_T 256
 #endif
 constexpr int CGS_T = TRPO_CGS_T, CGS_K = 5 + QCAP;
+// layout of the per-block partial dots (value k of block b of G): block-major [b][CGS_K] (default) or
+// value-major [k][G] (TRPO_DOTS_VMAJ=1: cg_axpy's loads coalesced, but each producer block's 21 values
+// land on 21 lines shared with other blocks)
+#ifndef TRPO_DOTS_VMAJ
+#define TRPO_DOTS_VMAJ 0
+#endif
+#define DOTS_AT(k, b, G) (TRPO_DOTS_VMAJ ? (long)(k) * (G) + (b) : (long)(b) * CGS_K + (k))
 template <typename QT>
 __global__ void __launch_bounds__(CGS_T)
 cg_dots_kernel(const double *__restrict__ zacc, const double *__restrict__ p, const double *__restrict__ r,
@@ -3455,7 +3462,7 @@ cg_dots_kernel(const double *__restrict__ zacc, const double *__restrict__ p, co
         double v = red[0];
 #pragma unroll
         for (int k = 1; k < CGS_K; ++k) v = tid == k ? red[k] : v;
-        dots[(long)blockIdx.x * CGS_K + tid] = v;
+        dots[DOTS_AT(tid, blockIdx.x, gridDim.x)] = v;
     }
 }
 
@@ -3465,7 +3472,7 @@ cg_dots_kernel(const double *__restrict__ zacc, const double *__restrict__ p, co
 // bits), then its threads t < RS_POS that hold a parameter (m = imap[.] >= 0) and, in block 0, the
 // threads RS_POS + k (k < P - nw) that hold the log-std entries form z = a / N + lambda p (2p + lambda p)
 // as cg_dots_kernel does, store it to zbuf and contribute the partial dots p.z, r.z, z.z, x.p, p.p,
-// q_i.z -> dots[b][CGS_K] (cg_axpy_kernel sums the slab/RS_POS partials in block order).  The gathers
+// q_i.z -> dots (DOTS_AT; cg_axpy_kernel sums the slab/RS_POS partials in block order).  The gathers
 // of p, r, x and the basis at the block's natural indices are issued between the slab loads and
 // their sums, so they add no round trip.  Only the dots' partition differs from the two-kernel form.
 template <typename QT>
@@ -3551,7 +3558,7 @@ reduce_dots_kernel(const float *__restrict__ slabs, int G, int slab, const int *
         double o = red[0];
 #pragma unroll
         for (int k = 1; k < CGS_K; ++k) o = t == k ? red[k] : o;
-        dots[(long)blockIdx.x * CGS_K + t] = o;
+        dots[DOTS_AT(t, blockIdx.x, gridDim.x)] = o;
     }
 }
 
@@ -3569,8 +3576,8 @@ cg_axpy_kernel(const double *__restrict__ dots, int G, const double *__restrict_
     const QT *qz = reinterpret_cast<const QT *>(qz_v);
     const int tid = threadIdx.x, t = blockIdx.x * CGS_T + tid;
     const int tc = min(t, (Ps >> 1) - 1);
-    // the partial dots of the G producer blocks: wave w sums values k = w, w + 4, ...; lane l takes
-    // partials l, l + 64, l + 128, l + 192 (all loads issued together, unconditional), then the
+    // the partial dots of the G producer blocks (DOTS_AT): wave w sums values k = w,
+    // w + 4, ...; lane l takes partials l, l + 64, l + 128, l + 192 (all loads issued together, unconditional), then the
     // fixed-order wave tree (a serial chain of G dependent loads by one thread was measured ~100 us
     // at G = 176 partials)
     constexpr int NW = CGS_T / 64, NI = (CGS_K + NW - 1) / NW, NJ = 4;
@@ -3583,13 +3590,13 @@ cg_axpy_kernel(const double *__restrict__ dots, int G, const double *__restrict_
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
                 const int k = w + NW * i, b = lane + 64 * j;
-                const double d = dots[(long)min(b, G - 1) * CGS_K + min(k, CGS_K - 1)];
+                const double d = dots[DOTS_AT(min(k, CGS_K - 1), min(b, G - 1), G)];
                 v[i][j] = (k < CGS_K && b < G) ? d : 0.0;
             }
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
             double a = (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
-            for (int b = lane + 64 * NJ; b < G; b += 64) a += dots[(long)b * CGS_K + min(w + NW * i, CGS_K - 1)];
+            for (int b = lane + 64 * NJ; b < G; b += 64) a += dots[DOTS_AT(min(w + NW * i, CGS_K - 1), b, G)];
             pv_[i] = wave_tree_sum(a);
         }
     }
@@ -5038,7 +5045,7 @@ extern "C" const char *trpo_dev_comm_backend(const trpo_dev *d) {
     if (!d) return "";
     if (d->comm_aborted) return "aborted";
     if (d->peer_on)
-        return trpo_peer_proto(d->peer) == 2 ? "peer-xgmi (uncached window, tagged granules)"
+        return trpo_peer_proto(d->peer) >= 2 ? "peer-xgmi (uncached window, tagged granules)"
                : trpo_peer_fenced(d->peer)   ? "peer-xgmi (uncached window, fenced hand-off)"
                                              : "peer-xgmi (uncached window)";
     if (d->comm) return "rccl";

@@ -28,7 +28,8 @@
 // steps 1 and 5 go out in rounds with every load of a round in flight (round 4: the per-element loops
 // cost one trip per element and replica; tools/peer_floor.py on one GPU, the exchange of the rank that
 // arrives second: 9.9 -> 7.3 us, profiles/r04_peer_exchange_floor_1gpu.txt).  TRPO_PEER_PROTO selects
-// 1 (this form, default), 0 (the round-3 loops) or 2 (peer_granule_kernel below: no flag at all).
+// 1 (this form, default), 0 (the round-3 loops), 2 (peer_granule_kernel below: no flag at all) or 3
+// (peer_granule_w_kernel: the granules with a compile-time world and unconditional loads, round 5).
 //
 // Memory ordering (round 4).  The window is allocated uncached, and every exchanged byte is stored and
 // loaded at system scope, so on the system ROCm no cache can hold a stale line of it.  That property
@@ -64,7 +65,7 @@ struct trpo_peer {
     int rank, world;
     int connected;                   // windows carry the exchange numbering: one connect per window
     int fence;                       // release / acquire around the flag hand-off (TRPO_PEER_FENCE, default 1)
-    int proto;                       // TRPO_PEER_PROTO: 1 flag + batched loads (default), 2 tagged granules, 0 the round-3 loops
+    int proto;                       // TRPO_PEER_PROTO: 1 flag + batched loads (default), 2 / 3 tagged granules, 0 the round-3 loops
 };
 
 static size_t flag_doubles(size_t S) { return 2 * (size_t)PEER_WMAX * S + (size_t)PEER_WMAX * FLAG_STRIDE; }
@@ -284,6 +285,133 @@ peer_granule_kernel(const double *__restrict__ in, int R, int Rstride, int count
     if (tid == 0) cnt[t] = e;
 }
 
+// The granule exchange for a compile-time world W (TRPO_PEER_PROTO=3, round 5).  peer_granule_kernel's
+// poll loads are guarded by `r < world` (run-time): hipcc branches around each of them and drains vmcnt
+// between them, so one poll costs several serialised round trips (its ISA: `s_cbranch_vccnz` around every
+// `global_load_dwordx2 … sc0 sc1`, `s_waitcnt vmcnt(0)` after each pair).  Here the rank loop is W long and
+// every load is unconditional, and the own rank's contribution never travels: workgroup t sums this
+// rank's replicas for its slice itself (in registers, issued with the first poll) and pushes only to the
+// W - 1 peers; workgroup `rank` pushes nothing.  So no workgroup waits on a sibling of its own rank.  The
+// rank-order sum and its bits are those of the other forms.  Two sets as there.
+template <int W>
+__global__ void __launch_bounds__(PEER_T)
+peer_granule_w_kernel(const double *__restrict__ in, int R, int Rstride, int count, double *const *wins, int rank,
+                      int S, double *__restrict__ out, unsigned long long *cnt, int *err, const int *done,
+                      size_t goff) {
+    const int t = blockIdx.x, tid = threadIdx.x;
+    const unsigned long long e = cnt[t] + 1;
+    const unsigned int tg = (unsigned int)(e & 0xffffffffULL);
+    const unsigned long long tag = (unsigned long long)tg << 32;
+    const int set = (int)(e & 1);
+    const int dn = done ? *done : 0;
+    // 1: local replica sum (replica order) pushed as tagged granules into slot `rank` of peer t's window
+    if (t != rank) {                                   // grid-uniform per workgroup
+        unsigned long long *dst =
+            reinterpret_cast<unsigned long long *>(wins[t] + goff) + 2 * ((size_t)set * PEER_WMAX + rank) * S;
+        for (int i0 = 0; i0 < count; i0 += PE * PEER_T) {
+            double v[PE][PE_R];
+#pragma unroll
+            for (int k = 0; k < PE; ++k)
+#pragma unroll
+                for (int r = 0; r < PE_R; ++r)
+                    v[k][r] = in[(long)min(r, R - 1) * Rstride + min(i0 + tid + k * PEER_T, count - 1)];
+            if (dn) return;                           // (grid-uniform) after the loads were issued
+#pragma unroll
+            for (int k = 0; k < PE; ++k) {
+                const int i = i0 + tid + k * PEER_T;
+                double s = v[k][0];
+#pragma unroll
+                for (int r = 1; r < PE_R; ++r) s += r < R ? v[k][r] : 0.0;
+                if (i < count) {
+                    const unsigned long long b = (unsigned long long)__double_as_longlong(s);
+                    st_sys64(dst + 2 * i, tag | (b & 0xffffffffULL));
+                    st_sys64(dst + 2 * i + 1, tag | (b >> 32));
+                }
+            }
+        }
+    } else if (dn) {
+        return;
+    }
+    // 2: slice t: the own replicas summed here, the W - 1 peers' granules polled in the OWN window until
+    // every tag reads e, then the rank-order sum
+    const int per = (count + W - 1) / W, lo = t * per, hi = min(count, lo + per);
+    const unsigned long long *src =
+        reinterpret_cast<const unsigned long long *>(wins[rank] + goff) + 2 * (size_t)set * PEER_WMAX * S;
+    constexpr int PE5 = 2;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    int failed = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    int nap = 0;                                       // poll backoff: every thread of the workgroup polls,
+                                                       // so a rank that arrives first backs off (1, 2, 4 ..
+                                                       // 32 x 64 cycles) instead of flooding the window lines
+    for (int i0 = lo; i0 < hi; i0 += PE5 * PEER_T) {
+        double own[PE5];
+#pragma unroll
+        for (int k = 0; k < PE5; ++k) {
+            const int ic = max(min(i0 + tid + k * PEER_T, hi - 1), 0);
+            double rv[PE_R];
+#pragma unroll
+            for (int r = 0; r < PE_R; ++r) rv[r] = in[(long)min(r, R - 1) * Rstride + ic];
+            double s = rv[0];
+#pragma unroll
+            for (int r = 1; r < PE_R; ++r) s += r < R ? rv[r] : 0.0;
+            own[k] = s;
+        }
+        unsigned long long g[PE5][W][2];
+        for (;;) {
+            bool ok = true;
+#pragma unroll
+            for (int k = 0; k < PE5; ++k)
+#pragma unroll
+                for (int r = 0; r < W; ++r) {
+                    const size_t a = 2 * ((size_t)r * S + max(min(i0 + tid + k * PEER_T, hi - 1), 0));
+                    g[k][r][0] = ld_sys64(src + a);
+                    g[k][r][1] = ld_sys64(src + a + 1);
+                }
+#pragma unroll
+            for (int k = 0; k < PE5; ++k)
+#pragma unroll
+                for (int r = 0; r < W; ++r)
+                    ok = ok && (r == rank || ((unsigned int)(g[k][r][0] >> 32) == tg &&
+                                              (unsigned int)(g[k][r][1] >> 32) == tg));
+            if (ok || failed) break;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > WAIT_TICKS) {
+                __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                failed = 1;
+#ifdef TRPO_PEER_DIAG
+                for (int r = 0; r < W; ++r)
+                    if ((tid & 63) == 0 && r != rank && (unsigned int)(g[0][r][0] >> 32) != tg)
+                        printf("[peer3] rank %d wg %d e %u: slot %d element %d tag %u\n", rank, t, tg, r,
+                               i0 + tid, (unsigned int)(g[0][r][0] >> 32));
+#endif
+                break;
+            }
+            // s_sleep takes an immediate: the backoff steps are unrolled
+            if (nap == 0) __builtin_amdgcn_s_sleep(1);
+            else if (nap == 1) __builtin_amdgcn_s_sleep(2);
+            else if (nap == 2) __builtin_amdgcn_s_sleep(4);
+            else if (nap == 3) __builtin_amdgcn_s_sleep(8);
+            else if (nap == 4) __builtin_amdgcn_s_sleep(16);
+            else __builtin_amdgcn_s_sleep(32);
+            nap = nap < 5 ? nap + 1 : 5;
+        }
+#pragma unroll
+        for (int k = 0; k < PE5; ++k) {
+            const int i = i0 + tid + k * PEER_T;
+            double s = 0.0;
+#pragma unroll
+            for (int r = 0; r < W; ++r) {
+                const double x = r == rank ? own[k]
+                                           : __longlong_as_double((long long)((g[k][r][0] & 0xffffffffULL) |
+                                                                              ((g[k][r][1] & 0xffffffffULL) << 32)));
+                s = r == 0 ? x : s + x;
+            }
+            if (i < hi) out[i] = s;
+        }
+    }
+    __syncthreads();                                  // every wave's reads of set e & 1 are done
+    if (tid == 0) cnt[t] = e;
+}
+
 // Uncached windows are process-lifetime memory (round 5): a destroyed context's window goes to
 // this pool and the next peer context of the process with the same window size takes it back, instead of
 // returning it to the HIP runtime.  Under the ROCm 7.0 runtime a PyTorch wheel bundles, hipFree of an
@@ -450,7 +578,18 @@ int trpo_peer_allreduce(trpo_peer *p, hipStream_t st, const double *in, int R, i
                         const int *done) {
     if (!p || count < 0 || (size_t)count > p->S || R < 1 || in == out) return -1;
     if (count == 0) return 0;
-    if (p->proto == 2)
+    if (p->proto == 3 && p->world <= 8 && R <= PE_R) {
+        const size_t go = flag_doubles(p->S);
+#define PEER_GW(W)                                                                                                   \
+    case W:                                                                                                          \
+        hipLaunchKernelGGL(peer_granule_w_kernel<W>, dim3(W), dim3(PEER_T), 0, st, in, R, Rstride, count, p->dwins,   \
+                           p->rank, (int)p->S, out, p->cnt, p->err_d, done, go);                                    \
+        break;
+        switch (p->world) {
+            PEER_GW(1) PEER_GW(2) PEER_GW(3) PEER_GW(4) PEER_GW(5) PEER_GW(6) PEER_GW(7) PEER_GW(8)
+        }
+#undef PEER_GW
+    } else if (p->proto == 2 || p->proto == 3)
         hipLaunchKernelGGL(peer_granule_kernel, dim3(p->world), dim3(PEER_T), 0, st, in, R, Rstride, count, p->dwins,
                            p->rank, p->world, (int)p->S, out, p->cnt, p->err_d, done, flag_doubles(p->S));
     else if (p->proto == 1)
