@@ -671,15 +671,16 @@ def extras_single(device, dist, reps, lock=None):
 
 def extras_multi(device, dist, b, x_ref, comm="rccl", out=None, lock=None):
     """N > 1, measured AFTER the headline: the same sharded solve with the other collectives in place of
-    the headline's (A/B on the driver's multi-GPU node): RCCL or the peer-window exchange (flag hand-off),
-    and the peer exchange in its tagged-granule form (TRPO_PEER_PROTO=2: the data is its own flag, one
-    xGMI trip fewer per exchange); and one sharded TRPO update (config C5) under the headline's collective.
+    the headline's (A/B on the driver's multi-GPU node): RCCL or the peer-window exchange (tagged granules,
+    the default form since round 5), and the peer exchange in its flag hand-off form (TRPO_PEER_PROTO=1,
+    the default through round 4: one more xGMI trip per exchange); and one sharded TRPO update (config C5)
+    under the headline's collective.
     Every one goes through run_secondary (agreed setup, agreed steps, abort + close in `finally`);
     results go into `out` as they complete (under `lock`: the watchdog may serialise it meanwhile)."""
     out = {} if out is None else out
     other = "rccl" if comm == "peer" else "peer"
     runs = (("C4_%s_exchange" % other, "other", other, _solve_body(dist, b, x_ref), None),
-            ("C4_peer_granule_exchange", "granule", "peer", _solve_body(dist, b, x_ref), {"TRPO_PEER_PROTO": "2"}),
+            ("C4_peer_flag_exchange", "flag", "peer", _solve_body(dist, b, x_ref), {"TRPO_PEER_PROTO": "1"}),
             ("C5_update_armDOF_0_N50000", "update", comm, _update_body(dist), None))
     for key, tag, backend, body, env in runs:
         if dist.broken:                          # a gloo bound expired: the ranks may be out of step

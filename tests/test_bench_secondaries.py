@@ -62,7 +62,7 @@ def _ok(row):
 def test_secondaries_all_run_without_faults():
     d, _, _ = _run2()
     ex = d["extra"]
-    for k in ("C4_peer_exchange", "C4_peer_granule_exchange", "C5_update_armDOF_0_N50000"):
+    for k in ("C4_peer_exchange", "C4_peer_flag_exchange", "C5_update_armDOF_0_N50000"):
         assert _ok(ex[k]), (k, ex[k])
     assert ex["C4_peer_exchange"]["verify"]["x_identical_on_all_ranks"]
     sw = ex["C4_sweep"]
@@ -119,8 +119,8 @@ def test_hung_rank_in_a_secondary_is_bounded():
 def test_hung_rank0_prints_by_watchdog():
     """Rank 0 itself blocks inside a secondary: its watchdog prints the headline line (marked) at the
     deadline and ends the process with exit 0."""
-    d, wall, _ = _run2("granule.hang:0")
+    d, wall, _ = _run2("flag.hang:0")
     assert "deadline reached" in d["watchdog"]
     assert _ok(d["extra"]["C4_peer_exchange"])
-    assert "C4_peer_granule_exchange" not in d["extra"]
+    assert "C4_peer_flag_exchange" not in d["extra"]
     assert wall < 90

@@ -28,8 +28,9 @@
 // steps 1 and 5 go out in rounds with every load of a round in flight (round 4: the per-element loops
 // cost one trip per element and replica; tools/peer_floor.py on one GPU, the exchange of the rank that
 // arrives second: 9.9 -> 7.3 us, profiles/r04_peer_exchange_floor_1gpu.txt).  TRPO_PEER_PROTO selects
-// 1 (this form, default), 0 (the round-3 loops), 2 (peer_granule_kernel below: no flag at all) or 3
-// (peer_granule_w_kernel: the granules with a compile-time world and unconditional loads, round 5).
+// 1 (this form; the default through round 4), 0 (the round-3 loops), 2 (peer_granule_kernel below: no
+// flag at all) or 3 (peer_granule_w_kernel: the granules with a compile-time world and unconditional loads,
+// the default since round 5; more than 8 ranks or replicas fall back to 2).
 //
 // Memory ordering (round 4).  The window is allocated uncached, and every exchanged byte is stored and
 // loaded at system scope, so on the system ROCm no cache can hold a stale line of it.  That property
@@ -65,7 +66,7 @@ struct trpo_peer {
     int rank, world;
     int connected;                   // windows carry the exchange numbering: one connect per window
     int fence;                       // release / acquire around the flag hand-off (TRPO_PEER_FENCE, default 1)
-    int proto;                       // TRPO_PEER_PROTO: 1 flag + batched loads (default), 2 / 3 tagged granules, 0 the round-3 loops
+    int proto;                       // TRPO_PEER_PROTO: 3 granules on a compile-time world (default), 2 granules, 1 flag + batched loads, 0 the round-3 loops
 };
 
 static size_t flag_doubles(size_t S) { return 2 * (size_t)PEER_WMAX * S + (size_t)PEER_WMAX * FLAG_STRIDE; }
@@ -484,7 +485,7 @@ trpo_peer *trpo_peer_create(int device, size_t S) {
     const char *ef = getenv("TRPO_PEER_FENCE");
     p->fence = !(ef && atoi(ef) == 0);
     const char *eb = getenv("TRPO_PEER_PROTO");
-    p->proto = eb ? atoi(eb) : 1;
+    p->proto = eb ? atoi(eb) : 3;
     p->win = (double *)win_take(device, bytes);
     if (!p->win && hipExtMallocWithFlags((void **)&p->win, bytes, hipDeviceMallocUncached) != hipSuccess) {
         (void)hipGetLastError();
