@@ -93,7 +93,7 @@ def test_peer_cg_lockstep_and_golden(bounds):
     assert cases.rel_l2(x0, cases.expected(c)) <= CG_TOL
 
 
-@pytest.mark.parametrize("proto", ["0", "1", "2", "3"])
+@pytest.mark.parametrize("proto", ["0", "1", "2", "3", "4"])
 def test_peer_exchange_forms_agree(proto, monkeypatch):
     """The four forms of the exchange kernel (TRPO_PEER_PROTO, read when the window is created):
     0 the round-3 per-element loops, 1 the batched load rounds (default), 2 the flagless tagged
@@ -120,7 +120,7 @@ def test_peer_exchange_forms_agree(proto, monkeypatch):
     for r in range(len(bounds)):
         np.testing.assert_array_equal(got[r][0], ref[0][0])     # CG: lockstep and equal to form 1
         np.testing.assert_array_equal(got[r][1], ref[0][1])     # standalone FVP (in-place exchange)
-        assert ("tagged granules" in got[r][2]) == (proto in ("2", "3")), got[r][2]
+        assert ("tagged granules" in got[r][2]) == (proto in ("2", "3", "4")), got[r][2]
     assert cases.rel_l2(got[0][0], cases.expected(c)) <= CG_TOL
 
     # a long message: the 2x64 policy's FVP (P = 5 443 > one load round of 4 x 256 elements; slices

@@ -29,8 +29,9 @@
 // cost one trip per element and replica; tools/peer_floor.py on one GPU, the exchange of the rank that
 // arrives second: 9.9 -> 7.3 us, profiles/r04_peer_exchange_floor_1gpu.txt).  TRPO_PEER_PROTO selects
 // 1 (this form; the default through round 4), 0 (the round-3 loops), 2 (peer_granule_kernel below: no
-// flag at all) or 3 (peer_granule_w_kernel: the granules with a compile-time world and unconditional loads,
-// the default since round 5; more than 8 ranks or replicas fall back to 2).
+// flag at all), 3 (peer_granule_w_kernel: the granules with a compile-time world and unconditional loads)
+// or 4 (the same with separate pushing and polling workgroups: the default since round 5; more than 8 ranks
+// or replicas fall back to 2).
 //
 // Memory ordering (round 4).  The window is allocated uncached, and every exchanged byte is stored and
 // loaded at system scope, so on the system ROCm no cache can hold a stale line of it.  That property
@@ -60,13 +61,15 @@ struct trpo_peer {
     size_t S;                        // slot length (fp64)
     double *win;                     // own window (device)
     double **dwins;                  // device array [world] of the windows as mapped in this process
+    double *hwins[PEER_WMAX];        // the same pointers on the host (kernel arguments of the granule forms)
     void *opened[PEER_WMAX];         // IPC-opened peer windows (closed at destroy)
     unsigned long long *cnt;         // [PEER_WMAX] per-workgroup exchange counters
     int *err_h, *err_d;              // pinned host error word and its device view
+    int *zero_d;                     // a device word that stays 0 (the granule forms' `done` when none is given)
     int rank, world;
     int connected;                   // windows carry the exchange numbering: one connect per window
     int fence;                       // release / acquire around the flag hand-off (TRPO_PEER_FENCE, default 1)
-    int proto;                       // TRPO_PEER_PROTO: 3 granules on a compile-time world (default), 2 granules, 1 flag + batched loads, 0 the round-3 loops
+    int proto;                       // TRPO_PEER_PROTO: 4 split granule form (default), 3 granules on a compile-time world, 2 granules, 1 flag + batched loads, 0 the round-3 loops
 };
 
 static size_t flag_doubles(size_t S) { return 2 * (size_t)PEER_WMAX * S + (size_t)PEER_WMAX * FLAG_STRIDE; }
@@ -294,21 +297,34 @@ peer_granule_kernel(const double *__restrict__ in, int R, int Rstride, int count
 // rank's replicas for its slice itself (in registers, issued with the first poll) and pushes only to the
 // W - 1 peers; workgroup `rank` pushes nothing.  So no workgroup waits on a sibling of its own rank.  The
 // rank-order sum and its bits are those of the other forms.  Two sets as there.
-template <int W>
+// SPLIT (TRPO_PEER_PROTO=4): 2W workgroups, the first W only push (to peer t), the last W only poll and sum
+// (slice t - W), so the rank that arrives second finishes after ONE dependent memory round trip (its
+// pollers find every peer's granules at the first poll while its pushers load the replicas) instead of
+// two (replica loads, then the poll).  The two-set argument holds unchanged: every polling workgroup of
+// exchange e + 1 waits for every peer's e + 1 push, so a rank starts e + 2 only after every peer started
+// e + 1, i.e. finished e.
+// The window pointers travel by value (kernel arguments), and each role issues its first loads (the
+// replicas; the own replicas and BOTH granule sets of its first slice round, whose addresses need no e)
+// before it loads the exchange counter and the done flag, so a poller's first poll is not queued behind a
+// counter round trip (the loads return together; a compiler barrier keeps that order).
+template <int W> struct PeerWins { double *w[W]; };
+template <int W, bool SPLIT = false>
 __global__ void __launch_bounds__(PEER_T)
-peer_granule_w_kernel(const double *__restrict__ in, int R, int Rstride, int count, double *const *wins, int rank,
+peer_granule_w_kernel(const double *__restrict__ in, int R, int Rstride, int count, PeerWins<W> wins, int rank,
                       int S, double *__restrict__ out, unsigned long long *cnt, int *err, const int *done,
                       size_t goff) {
     const int t = blockIdx.x, tid = threadIdx.x;
-    const unsigned long long e = cnt[t] + 1;
-    const unsigned int tg = (unsigned int)(e & 0xffffffffULL);
-    const unsigned long long tag = (unsigned long long)tg << 32;
-    const int set = (int)(e & 1);
-    const int dn = done ? *done : 0;
+    const bool pusher = !SPLIT || t < W, poller = !SPLIT || t >= W;   // grid-uniform per workgroup
+    const int ts = SPLIT ? t - W : t;                                 // the slice this workgroup sums
+    unsigned long long e = 0;
+    int dn = 0;
+    auto load_state = [&]() __attribute__((always_inline)) {
+        __builtin_amdgcn_sched_barrier(0);
+        e = __hip_atomic_load(cnt + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+        dn = __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // never null (zero word)
+    };
     // 1: local replica sum (replica order) pushed as tagged granules into slot `rank` of peer t's window
-    if (t != rank) {                                   // grid-uniform per workgroup
-        unsigned long long *dst =
-            reinterpret_cast<unsigned long long *>(wins[t] + goff) + 2 * ((size_t)set * PEER_WMAX + rank) * S;
+    if (pusher && t != rank) {                         // grid-uniform per workgroup
         for (int i0 = 0; i0 < count; i0 += PE * PEER_T) {
             double v[PE][PE_R];
 #pragma unroll
@@ -316,7 +332,11 @@ peer_granule_w_kernel(const double *__restrict__ in, int R, int Rstride, int cou
 #pragma unroll
                 for (int r = 0; r < PE_R; ++r)
                     v[k][r] = in[(long)min(r, R - 1) * Rstride + min(i0 + tid + k * PEER_T, count - 1)];
+            if (i0 == 0) load_state();
             if (dn) return;                           // (grid-uniform) after the loads were issued
+            const unsigned long long tag = (e & 0xffffffffULL) << 32;
+            unsigned long long *dst = reinterpret_cast<unsigned long long *>(wins.w[t] + goff) +
+                                      2 * ((size_t)(e & 1) * PEER_WMAX + rank) * S;
 #pragma unroll
             for (int k = 0; k < PE; ++k) {
                 const int i = i0 + tid + k * PEER_T;
@@ -330,44 +350,73 @@ peer_granule_w_kernel(const double *__restrict__ in, int R, int Rstride, int cou
                 }
             }
         }
-    } else if (dn) {
+        if (!poller) {                                 // SPLIT pusher: done once its stores are issued
+            if (tid == 0) cnt[t] = e;
+            return;
+        }
+    } else if (!poller) {
+        load_state();
+        if (!dn && tid == 0) cnt[t] = e;
         return;
     }
-    // 2: slice t: the own replicas summed here, the W - 1 peers' granules polled in the OWN window until
+    // 2: slice ts: the own replicas summed here, the W - 1 peers' granules polled in the OWN window until
     // every tag reads e, then the rank-order sum
-    const int per = (count + W - 1) / W, lo = t * per, hi = min(count, lo + per);
-    const unsigned long long *src =
-        reinterpret_cast<const unsigned long long *>(wins[rank] + goff) + 2 * (size_t)set * PEER_WMAX * S;
-    constexpr int PE5 = 2;
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    int failed = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    int nap = 0;                                       // poll backoff: every thread of the workgroup polls,
+    const int per = (count + W - 1) / W, lo = ts * per, hi = min(count, lo + per);
+    const unsigned long long *src0 = reinterpret_cast<const unsigned long long *>(wins.w[rank] + goff);
+    const size_t s1 = 2 * (size_t)PEER_WMAX * S;       // set 1 - set 0
+    constexpr int PE5 = W <= 4 ? 2 : 1;
+    bool errchk = false;
+    int failed = 0, nap = 0;                           // poll backoff: every thread of the workgroup polls,
                                                        // so a rank that arrives first backs off (1, 2, 4 ..
                                                        // 32 x 64 cycles) instead of flooding the window lines
+    unsigned long long t0 = 0;
+    bool state = SPLIT ? false : true;                 // e / dn loaded (by the pusher part when not SPLIT)
+    if (!SPLIT && t == rank) state = false;
+    if (lo >= hi && !state) {                          // empty slice
+        load_state();
+        state = true;
+    }
     for (int i0 = lo; i0 < hi; i0 += PE5 * PEER_T) {
         double own[PE5];
+        unsigned long long h[PE5][W][2][2];            // [k][rank][set][granule]
 #pragma unroll
         for (int k = 0; k < PE5; ++k) {
             const int ic = max(min(i0 + tid + k * PEER_T, hi - 1), 0);
             double rv[PE_R];
 #pragma unroll
             for (int r = 0; r < PE_R; ++r) rv[r] = in[(long)min(r, R - 1) * Rstride + ic];
+#pragma unroll
+            for (int r = 0; r < W; ++r) {
+                const size_t a = 2 * ((size_t)r * S + ic);
+                h[k][r][0][0] = ld_sys64(src0 + a);
+                h[k][r][0][1] = ld_sys64(src0 + a + 1);
+                h[k][r][1][0] = ld_sys64(src0 + s1 + a);
+                h[k][r][1][1] = ld_sys64(src0 + s1 + a + 1);
+            }
             double s = rv[0];
 #pragma unroll
             for (int r = 1; r < PE_R; ++r) s += r < R ? rv[r] : 0.0;
             own[k] = s;
         }
+        if (!state) {
+            load_state();
+            state = true;
+        }
+        if (dn) return;                                // (grid-uniform) a converged CG skips the exchange
+        if (i0 == lo) t0 = __builtin_amdgcn_s_memrealtime();
+        const unsigned int tg = (unsigned int)(e & 0xffffffffULL);
+        const int set = (int)(e & 1);
+        const unsigned long long *src = src0 + (set ? s1 : 0);
         unsigned long long g[PE5][W][2];
+#pragma unroll
+        for (int k = 0; k < PE5; ++k)
+#pragma unroll
+            for (int r = 0; r < W; ++r) {
+                g[k][r][0] = set ? h[k][r][1][0] : h[k][r][0][0];
+                g[k][r][1] = set ? h[k][r][1][1] : h[k][r][0][1];
+            }
         for (;;) {
             bool ok = true;
-#pragma unroll
-            for (int k = 0; k < PE5; ++k)
-#pragma unroll
-                for (int r = 0; r < W; ++r) {
-                    const size_t a = 2 * ((size_t)r * S + max(min(i0 + tid + k * PEER_T, hi - 1), 0));
-                    g[k][r][0] = ld_sys64(src + a);
-                    g[k][r][1] = ld_sys64(src + a + 1);
-                }
 #pragma unroll
             for (int k = 0; k < PE5; ++k)
 #pragma unroll
@@ -375,6 +424,11 @@ peer_granule_w_kernel(const double *__restrict__ in, int R, int Rstride, int cou
                     ok = ok && (r == rank || ((unsigned int)(g[k][r][0] >> 32) == tg &&
                                               (unsigned int)(g[k][r][1] >> 32) == tg));
             if (ok || failed) break;
+            if (!errchk) {                             // an earlier exchange gave up: do not wait (the error
+                errchk = true;                         // word is host memory, so read only off the fast path)
+                failed = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (failed) break;
+            }
             if (__builtin_amdgcn_s_memrealtime() - t0 > WAIT_TICKS) {
                 __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 failed = 1;
@@ -394,6 +448,14 @@ peer_granule_w_kernel(const double *__restrict__ in, int R, int Rstride, int cou
             else if (nap == 4) __builtin_amdgcn_s_sleep(16);
             else __builtin_amdgcn_s_sleep(32);
             nap = nap < 5 ? nap + 1 : 5;
+#pragma unroll
+            for (int k = 0; k < PE5; ++k)
+#pragma unroll
+                for (int r = 0; r < W; ++r) {
+                    const size_t a = 2 * ((size_t)r * S + max(min(i0 + tid + k * PEER_T, hi - 1), 0));
+                    g[k][r][0] = ld_sys64(src + a);
+                    g[k][r][1] = ld_sys64(src + a + 1);
+                }
         }
 #pragma unroll
         for (int k = 0; k < PE5; ++k) {
@@ -409,6 +471,7 @@ peer_granule_w_kernel(const double *__restrict__ in, int R, int Rstride, int cou
             if (i < hi) out[i] = s;
         }
     }
+    if (dn) return;
     __syncthreads();                                  // every wave's reads of set e & 1 are done
     if (tid == 0) cnt[t] = e;
 }
@@ -465,6 +528,7 @@ static void peer_free(trpo_peer *p) {
     }
     if (p->dwins) hipFree(p->dwins);
     if (p->cnt) hipFree(p->cnt);
+    if (p->zero_d) hipFree(p->zero_d);
     if (p->err_h) hipHostFree(p->err_h);
     free(p);
 }
@@ -485,7 +549,7 @@ trpo_peer *trpo_peer_create(int device, size_t S) {
     const char *ef = getenv("TRPO_PEER_FENCE");
     p->fence = !(ef && atoi(ef) == 0);
     const char *eb = getenv("TRPO_PEER_PROTO");
-    p->proto = eb ? atoi(eb) : 3;
+    p->proto = eb ? atoi(eb) : 4;
     p->win = (double *)win_take(device, bytes);
     if (!p->win && hipExtMallocWithFlags((void **)&p->win, bytes, hipDeviceMallocUncached) != hipSuccess) {
         (void)hipGetLastError();
@@ -500,6 +564,8 @@ trpo_peer *trpo_peer_create(int device, size_t S) {
               trpo_malloc((void **)&p->dwins, sizeof(double *) * PEER_WMAX) == hipSuccess &&
               trpo_malloc((void **)&p->cnt, sizeof(unsigned long long) * PEER_WMAX) == hipSuccess &&
               hipMemset(p->cnt, 0, sizeof(unsigned long long) * PEER_WMAX) == hipSuccess &&
+              trpo_malloc((void **)&p->zero_d, sizeof(int)) == hipSuccess &&
+              hipMemset(p->zero_d, 0, sizeof(int)) == hipSuccess &&
               hipHostMalloc((void **)&p->err_h, sizeof(int), TRPO_HOST_COHERENT) == hipSuccess;
     if (ok) {
         *p->err_h = 0;
@@ -565,6 +631,7 @@ int trpo_peer_connect(trpo_peer *p, int rank, int world, const void *handles, vo
         if (!w[r]) return -1;
     }
     HCHK(hipMemcpyAsync(p->dwins, w, sizeof(double *) * world, hipMemcpyHostToDevice, st));
+    for (int r = 0; r < PEER_WMAX; ++r) p->hwins[r] = r < world ? w[r] : NULL;
     HCHK(hipStreamSynchronize(st));
     __atomic_store_n(p->err_h, 0, __ATOMIC_RELEASE);
     p->connected = 1;
@@ -579,18 +646,27 @@ int trpo_peer_allreduce(trpo_peer *p, hipStream_t st, const double *in, int R, i
                         const int *done) {
     if (!p || count < 0 || (size_t)count > p->S || R < 1 || in == out) return -1;
     if (count == 0) return 0;
-    if (p->proto == 3 && p->world <= 8 && R <= PE_R) {
+    if ((p->proto == 3 || p->proto == 4) && p->world <= 8 && R <= PE_R) {
         const size_t go = flag_doubles(p->S);
+        const bool split = p->proto == 4;
+        const int *dz = done ? done : p->zero_d;
 #define PEER_GW(W)                                                                                                   \
-    case W:                                                                                                          \
-        hipLaunchKernelGGL(peer_granule_w_kernel<W>, dim3(W), dim3(PEER_T), 0, st, in, R, Rstride, count, p->dwins,   \
-                           p->rank, (int)p->S, out, p->cnt, p->err_d, done, go);                                    \
-        break;
+    case W: {                                                                                                        \
+        PeerWins<W> pw;                                                                                              \
+        for (int r = 0; r < W; ++r) pw.w[r] = p->hwins[r];                                                           \
+        if (split)                                                                                                   \
+            hipLaunchKernelGGL((peer_granule_w_kernel<W, true>), dim3(2 * W), dim3(PEER_T), 0, st, in, R, Rstride,    \
+                               count, pw, p->rank, (int)p->S, out, p->cnt, p->err_d, dz, go);                       \
+        else                                                                                                         \
+            hipLaunchKernelGGL((peer_granule_w_kernel<W, false>), dim3(W), dim3(PEER_T), 0, st, in, R, Rstride,       \
+                               count, pw, p->rank, (int)p->S, out, p->cnt, p->err_d, dz, go);                       \
+        break;                                                                                                       \
+    }
         switch (p->world) {
             PEER_GW(1) PEER_GW(2) PEER_GW(3) PEER_GW(4) PEER_GW(5) PEER_GW(6) PEER_GW(7) PEER_GW(8)
         }
 #undef PEER_GW
-    } else if (p->proto == 2 || p->proto == 3)
+    } else if (p->proto >= 2)
         hipLaunchKernelGGL(peer_granule_kernel, dim3(p->world), dim3(PEER_T), 0, st, in, R, Rstride, count, p->dwins,
                            p->rank, p->world, (int)p->S, out, p->cnt, p->err_d, done, flag_doubles(p->S));
     else if (p->proto == 1)
