@@ -3002,13 +3002,19 @@ reduce_slabs_kernel(const ST *__restrict__ slabs, int G, int slab, const int *__
     double s[VE];
 #pragma unroll
     for (int e = 0; e < VE; ++e) s[e] = 0.0;
-    for (int b0 = sg; b0 < G; b0 += SG * NLD) {
+    // the FVP epilogue's direction value vin[m] is gathered between the first slab loads and their sums (one
+    // round trip, not two); slab loads clamped and masked by a multiply (+-0 adds nothing), so the compiler
+    // can count them instead of draining exec-masked loads (round 5, as reduce_dots_kernel)
+    // (the first round runs in every thread, also where sg >= G, so that every thread gathers its vin[m])
+    double vm = 0.0;
+    for (int b0 = sg, r0 = 1; r0 || b0 < G; b0 += SG * NLD, r0 = 0) {
         VT v[NLD];
 #pragma unroll
         for (int k = 0; k < NLD; ++k) {
             const int b = b0 + SG * k;
-            v[k] = b < G ? *reinterpret_cast<const VT *>(slabs + (long)b * slab + j0) : (VT)0;
+            v[k] = *reinterpret_cast<const VT *>(slabs + (long)min(b, G - 1) * slab + j0) * (ST)(b < G ? 1 : 0);
         }
+        if (r0 && zout) vm = vin[max(m, 0)];
 #pragma unroll
         for (int k = 0; k < NLD; ++k)
 #pragma unroll
@@ -3022,7 +3028,7 @@ reduce_slabs_kernel(const ST *__restrict__ slabs, int G, int slab, const int *__
 #pragma unroll 8
         for (int k = 0; k < SG; ++k) a += part[k][t];
         if (zout) {                                    // fused FVP epilogue
-            const double z = a / ctl->n_total + ctl->damping * vin[m];
+            const double z = a / ctl->n_total + ctl->damping * vm;
             zout[m] = z;
             if (zh) zh[m] = z;                         // also into the caller's mapped host buffer
         } else {
@@ -3343,14 +3349,24 @@ cg_last_kernel(const double *__restrict__ acc, int R_in, const double *__restric
         return;
     }
     const double pe[2] = {p2.x, p2.y}, re[2] = {r2.x, r2.y}, xe[2] = {x2.x, x2.y};
+    // the replica values pinned in registers here: z is only used for q < nw, and with the fp64 division
+    // behind it hipcc turned that select into a branch and sank half the replica loads into it (issued
+    // after the first round had drained: a second round trip, round 5)
+    double zr[2][RMAX];
+#pragma unroll
+    for (int k = 0; k < RMAX; ++k) {
+        zr[0][k] = za[k].x;
+        zr[1][k] = za[k].y;
+        asm volatile("" : "+v"(zr[0][k]), "+v"(zr[1][k]));
+    }
     double pv[2], rv[2], xv[2], zv[2];
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
         const int q = 2 * tid + e;
         const bool in = q < P;
-        double z = e ? za[0].y : za[0].x;
+        double z = zr[e][0];
 #pragma unroll
-        for (int k = 1; k < RMAX; ++k) z += k < R_in ? (e ? za[k].y : za[k].x) : 0.0;
+        for (int k = 1; k < RMAX; ++k) z += k < R_in ? zr[e][k] : 0.0;
         pv[e] = in ? pe[e] : 0.0;
         rv[e] = in ? re[e] : 0.0;
         xv[e] = in ? xe[e] : 0.0;
@@ -3498,8 +3514,10 @@ reduce_dots_kernel(const float *__restrict__ slabs, int G, int slab, const int *
     VT v[NLD];
 #pragma unroll
     for (int k = 0; k < NLD; ++k) {                       // the first load round (all of it for G <= 256)
+        // clamped and masked by a multiply (+-0 adds nothing): a `b < G ? load : 0` became exec-masked
+        // loads the compiler cannot count, so it drained them all (vmcnt(0)) before the gathers below
         const int b = sg + SG * k;
-        v[k] = b < G ? *reinterpret_cast<const VT *>(slabs + (long)b * slab + j0) : (VT)0;
+        v[k] = *reinterpret_cast<const VT *>(slabs + (long)min(b, G - 1) * slab + j0) * (b < G ? 1.0f : 0.0f);
     }
     const int q = t < RS_POS ? m : (blockIdx.x == 0 && kls >= 0 && kls < P - nw ? nw + kls : -1);
     const int qc = min(max(q, 0), P - 1);
@@ -3580,26 +3598,7 @@ cg_axpy_kernel(const double *__restrict__ dots, int G, const double *__restrict_
     // w + 4, ...; lane l takes partials l, l + 64, l + 128, l + 192 (all loads issued together, unconditional), then the
     // fixed-order wave tree (a serial chain of G dependent loads by one thread was measured ~100 us
     // at G = 176 partials)
-    constexpr int NW = CGS_T / 64, NI = (CGS_K + NW - 1) / NW, NJ = 4;
-    const int lane = tid & 63, w = tid >> 6;
-    double pv_[NI];
-    {
-        double v[NI][NJ];
-#pragma unroll
-        for (int i = 0; i < NI; ++i)
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                const int k = w + NW * i, b = lane + 64 * j;
-                const double d = dots[DOTS_AT(min(k, CGS_K - 1), min(b, G - 1), G)];
-                v[i][j] = (k < CGS_K && b < G) ? d : 0.0;
-            }
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
-            double a = (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
-            for (int b = lane + 64 * NJ; b < G; b += 64) a += dots[DOTS_AT(min(w + NW * i, CGS_K - 1), b, G)];
-            pv_[i] = wave_tree_sum(a);
-        }
-    }
+    // this slice's vectors first (independent of the dots: their round trip overlaps the dots')
     const double2 p2 = reinterpret_cast<const double2 *>(p_in)[tc], r2 = reinterpret_cast<const double2 *>(r_in)[tc];
     const double2 x2 = reinterpret_cast<const double2 *>(x)[tc], z2 = reinterpret_cast<const double2 *>(zbuf)[tc];
     // vpk: p' also into the fp32 fragment-order direction pack of the next FVP (slots pslot[q], -1 for
@@ -3615,6 +3614,28 @@ cg_axpy_kernel(const double *__restrict__ dots, int G, const double *__restrict_
         const QV2 v = *src;
         qv[i][0] = ok ? (double)v.x : 0.0;
         qv[i][1] = ok ? (double)v.y : 0.0;
+    }
+    constexpr int NW = CGS_T / 64, NI = (CGS_K + NW - 1) / NW, NJ = 4;
+    const int lane = tid & 63, w = tid >> 6;
+    double pv_[NI];
+    {
+        double v[NI][NJ];
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int k = w + NW * i, b = lane + 64 * j;
+                const double d = dots[DOTS_AT(min(k, CGS_K - 1), min(b, G - 1), G)];
+                // a multiply, not a select: with `cond ? d : 0` hipcc sank the loads under the condition
+                // (exec-masked, one vmcnt(0) drain each: 16 serialised round trips, round 5)
+                v[i][j] = d * ((k < CGS_K && b < G) ? 1.0 : 0.0);
+            }
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            double a = (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
+            for (int b = lane + 64 * NJ; b < G; b += 64) a += dots[DOTS_AT(min(w + NW * i, CGS_K - 1), b, G)];
+            pv_[i] = wave_tree_sum(a);
+        }
     }
     const CgSt sin = *st_in;
     const double cth = ctl->resth;
