@@ -4549,12 +4549,14 @@ static int choose_grid(trpo_dev *d) {
     const char *e = getenv("TRPO_FVP_BLOCKS");
     if (d->fast) {
         const int ntiles = cdiv((long)d->n, 16);
-        // cooperative kernel, group-major tiles (A.gmaj): by default only when the grid is full either
-        // way (ntiles >= groups of a full grid) -- below that, group-major spreads the busy groups one per
-        // block over up to twice the blocks: 2x64 N = 4 096 kernel 8.47 -> 7.65 us, but the slab reduce
-        // then reads twice the block partials and the FVP call / CG get slower (11.93 -> 12.25 us,
-        // 205.8 -> 208.7 us; profiles/r05_ab_coop.log); TRPO_COOP_GMAJ=1 / 0 forces it on / off
-        d->gmaj_on = d->coop && (d->coop_gmaj > 0 || (d->coop_gmaj < 0 && ntiles >= d->k_tiles * cus));
+        // cooperative kernel, group-major tiles (A.gmaj): by default when the grid is full either way
+        // (ntiles >= groups of a full grid), and at <= cus / 2 tiles.  In between group-major spreads the
+        // busy groups one per block over up to twice the blocks and the slab reduce reads twice the block
+        // partials: 2x64 N = 4 096 (256 tiles) kernel 8.44 -> 7.73 us but FVP call 11.75 -> 12.18 us and CG
+        // 197.0 -> 202.0 us, while at N = 2 048 (128 tiles) kernel 8.31 -> 7.16 us, call 11.21 -> 10.59 us,
+        // CG 192.0 -> 185.8 us (profiles/r05_ab_coop.log); TRPO_COOP_GMAJ=1 / 0 forces it on / off
+        d->gmaj_on = d->coop && (d->coop_gmaj > 0 ||
+                                 (d->coop_gmaj < 0 && (ntiles >= d->k_tiles * cus || 2 * ntiles <= cus)));
         int g = cdiv(ntiles, d->gmaj_on ? 1 : d->k_tiles);
         if (g > cus) g = cus;
         if (e && atoi(e) > 0) g = atoi(e);
