@@ -789,6 +789,9 @@ constexpr int SCR_LD3 = TRPO_SCR_LD3;  // fvp_mlp3_kernel's transpose scratch (T
 #ifndef TRPO_RGS4_T
 #define TRPO_RGS4_T 1                   // rowgroup_sum4 as a transposed reduction (same bits, half the swaps)
 #endif
+#ifndef TRPO_NO_PF
+#define TRPO_NO_PF 0                    // experiment builds only: no register prefetch of the next tile
+#endif
 #ifndef TRPO_DIAG_NOLOAD
 #define TRPO_DIAG_NOLOAD 0              // diagnostic builds only: every tile reuses the first tile's inputs
 #endif                                  // (1: all of them, 2: the observations only, 3: the cached y only)
@@ -1806,6 +1809,29 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
         // input tiles: lane holds features 16kt+4g..+3 of its sample (D-layout rows)
         f4 x0[NT][T0];
         [[maybe_unused]] f4 ycur[YC ? NYC : 1];
+#if TRPO_NO_PF
+        // experiment (round 5): no register prefetch -- the trip's own inputs loaded at its top (12 VGPRs
+        // fewer, for more waves per SIMD to hide the latency instead)
+        {
+            const int tc = min(tile, ntiles - 1);
+            const auto rx = __builtin_amdgcn_make_buffer_rsrc((void *)(obs4 + (long)tc * (16 * 4 * T0)), 0,
+                                                              16 * 64 * T0, 0x00020000);
+#pragma unroll
+            for (int kt = 0; kt < T0; ++kt)
+                xn[kt] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rx, pf_xoff + kt * 64, 0, 0));
+            if constexpr (YC) {
+                const auto ry = __builtin_amdgcn_make_buffer_rsrc((void *)(yc4 + (long)tc * (NYC * 64)), 0, NYC * 1024,
+                                                                  0x00020000);
+#pragma unroll
+                for (int k = 0; k < T1 + T2; ++k)
+                    yn[k] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ry, pf_yoff + k * 1024, 0, 0));
+                if (y3_needed)
+#pragma unroll
+                    for (int k = T1 + T2; k < NYC; ++k)
+                        yn[k] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ry, pf_yoff + k * 1024, 0, 0));
+            }
+        }
+#endif
         if constexpr (YC) {
 #pragma unroll
             for (int k = 0; k < NYC; ++k) ycur[k] = yn[k];
@@ -1824,7 +1850,7 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
                 for (int kt = 0; kt < T0; ++kt) x0[t][kt] = obs4[(long)(tc * 16 + c) * (4 * T0) + kt * 4 + g];
             }
         }
-        if constexpr (TRPO_DIAG_NOLOAD != 1) {   // unconditional (clamped) prefetch of the next trip's first tile
+        if constexpr (TRPO_DIAG_NOLOAD != 1 && !TRPO_NO_PF) {   // unconditional (clamped) prefetch of the next trip's first tile
             const int tn = min(tile + NT * nwaves, ntiles - 1);
 #if TRPO_BUF_PF
             // buffer loads off per-trip descriptors of the tile's records: the wave-uniform part of the
