@@ -121,7 +121,7 @@ __device__ void forward64(const Net &net, const TH &th, const double *__restrict
             double x[FWD_JB];
 #pragma unroll
             for (int jj = 0; jj < FWD_JB; ++jj) x[jj] = th[bo + j + jj];
-#pragma unroll 4
+#pragma unroll 16
             for (int k = 0; k < in; ++k) {
                 const double y = Y[(roff[i] + k) * RS + tid];
                 const int w = wo + k * out + j;
@@ -193,12 +193,16 @@ __device__ __forceinline__ void pg_seed(const double *rw, int A, int i, double l
 // Policy gradient partial sums, any depth / widths: block b accumulates, over its 64-sample
 // passes, the unnormalised gradient [GW, GB per layer, GLogStd] (src/TRPO_Update.c:295-378)
 // plus sum(Adv) at index P, into slabs[b][P + 1].  Activations in Y rows (LDS or scratch).
+template <bool LDSY>
 __global__ void __launch_bounds__(UT)
 pg_kernel(Net net, const double *__restrict__ th, const double *__restrict__ obs, const double *__restrict__ roll,
           int n, double *ws, int rows, int use_lds, double *__restrict__ slabs) {
     extern __shared__ double lds64[];
     const int tid = threadIdx.x;
-    double *Y = use_lds ? lds64 : ws + (long)blockIdx.x * rows * RS;
+    // LDSY (compile time): with a run-time select hipcc cannot tell LDS from global and makes every
+    // Y access a flat load / store (one lgkmcnt for LDS and the scalar theta loads alike: round 5)
+    double *Y = LDSY ? lds64 : ws + (long)blockIdx.x * rows * RS;
+    (void)use_lds;
     int roff[MAXL + 1];
     row_offsets(net, roff);
     const int tot = roff[net.nl], P = net.P, A = net.A, last = net.nl - 1;
@@ -231,7 +235,23 @@ pg_kernel(Net net, const double *__restrict__ th, const double *__restrict__ obs
             }
             if (i >= 2) {
                 const int prev = net.L[i - 1], wo = net.woff[i - 1];
-                for (int j = 0; j < prev; ++j) {
+                // FWD_JB outputs per sweep (independent chains, one read of each g_k for all of them;
+                // each chain keeps its k-ascending order, so the sums are unchanged: round 5)
+                int j = 0;
+                for (; j + FWD_JB <= prev; j += FWD_JB) {
+                    double t[FWD_JB];
+#pragma unroll
+                    for (int jj = 0; jj < FWD_JB; ++jj) t[jj] = 0.0;
+#pragma unroll 16
+                    for (int k = 0; k < cur; ++k) {
+                        const double gk = Y[(G0 + roff[i] + k) * RS + tid];
+#pragma unroll
+                        for (int jj = 0; jj < FWD_JB; ++jj) t[jj] += gk * th[wo + (j + jj) * cur + k];
+                    }
+#pragma unroll
+                    for (int jj = 0; jj < FWD_JB; ++jj) Y[(G0 + roff[i - 1] + j + jj) * RS + tid] = t[jj];
+                }
+                for (; j < prev; ++j) {
                     double t = 0.0;
 #pragma unroll 4
                     for (int k = 0; k < cur; ++k) t += Y[(G0 + roff[i] + k) * RS + tid] * th[wo + j * cur + k];
@@ -345,13 +365,15 @@ __global__ void cand_theta_kernel(const double *__restrict__ th0, const double *
 
 // Line-search surrogate: block (bx, k) sums Adv * exp(LLD) over its passes for candidate k of
 // tk (src/TRPO_Update.c:951-981); parts[bx][k].
+template <bool LDSY>
 __global__ void __launch_bounds__(UT)
 surr_kernel(Net net, const double *__restrict__ tk, const double *__restrict__ obs,
             const double *__restrict__ roll, const double *__restrict__ stdv, int n,
             double *ws, int rows, int use_lds, double *__restrict__ parts) {
     extern __shared__ double lds64[];
     const int tid = threadIdx.x, k = blockIdx.y, nk = gridDim.y;
-    double *Y = use_lds ? lds64 : ws + ((long)k * gridDim.x + blockIdx.x) * rows * RS;
+    double *Y = LDSY ? lds64 : ws + ((long)k * gridDim.x + blockIdx.x) * rows * RS;   // see pg_kernel
+    (void)use_lds;
     int roff[MAXL + 1];
     row_offsets(net, roff);
     const int P = net.P, A = net.A, last = net.nl - 1;
@@ -770,8 +792,8 @@ static bool reg_path(const Net &net) {
 
 static int set_lds_attrs(UpdState *u) {
     if (u->lds_set) return 0;
-    HCHK(hipFuncSetAttribute((const void *)pg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_CAP));
-    HCHK(hipFuncSetAttribute((const void *)surr_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_CAP));
+    HCHK(hipFuncSetAttribute((const void *)pg_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_CAP));
+    HCHK(hipFuncSetAttribute((const void *)surr_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_CAP));
     u->lds_set = 1;
     return 0;
 }
@@ -878,8 +900,8 @@ static int enqueue_policy_gradient(trpo_dev *d, const double **adv_dev) {
         int use_lds = 0;
         const int lds = act_storage(u, rows, G, v.stream, &use_lds);
         if (lds < 0) return -2;
-        hipLaunchKernelGGL(pg_kernel, dim3(G), dim3(UT), lds, v.stream, net, v.theta64, v.obs64, u->roll, n, u->ws,
-                           rows, use_lds, u->slabs);
+        hipLaunchKernelGGL(use_lds ? pg_kernel<true> : pg_kernel<false>, dim3(G), dim3(UT), lds, v.stream, net,
+                           v.theta64, v.obs64, u->roll, n, u->ws, rows, use_lds, u->slabs);
     }
     hipLaunchKernelGGL(sum_slabs64_kernel, dim3(cdiv(P + 1, 16)), dim3(256), 0, v.stream, u->slabs, G, P + 1, u->sum);
     HCHK(hipGetLastError());
@@ -1025,8 +1047,8 @@ static int enqueue_surrogate(trpo_dev *d, const double *fs, int k0, int nk) {
         int use_lds = 0;
         const int lds = act_storage(u, rows, (long)Gs * nk, v.stream, &use_lds);
         if (lds < 0) return -2;
-        hipLaunchKernelGGL(surr_kernel, dim3(Gs, nk), dim3(UT), lds, v.stream, net, (const double *)u->tk,
-                           v.obs64, u->roll, v.std64, n, u->ws, rows, use_lds, u->slabs);
+        hipLaunchKernelGGL(use_lds ? surr_kernel<true> : surr_kernel<false>, dim3(Gs, nk), dim3(UT), lds, v.stream,
+                           net, (const double *)u->tk, v.obs64, u->roll, v.std64, n, u->ws, rows, use_lds, u->slabs);
     }
     hipLaunchKernelGGL(sum_slabs64_kernel, dim3(cdiv(nk, 16)), dim3(256), 0, v.stream, u->slabs, Gs, nk, u->sums);
     HCHK(hipGetLastError());
@@ -1062,13 +1084,27 @@ extern "C" int trpo_dev_surrogate(trpo_dev *d, const double *fullstep, int k0, i
 // 0.02 (Predict - Target), backprop, gradient sums; fp64 like the policy-gradient
 // generic kernel (N is small, ~3000, and L-BFGS wants consistent f and g).
 // ===========================================================================
+// THL: theta staged in LDS behind Y (round 5): read from global its wave-uniform loads are scalar loads,
+// which return out of order, so every use waited for lgkmcnt(0) -- and with it for every LDS read in
+// flight: the per-sample chains ran one memory round trip per multiply-add
+template <bool LDSY, bool THL>
 __global__ void __launch_bounds__(UT)
-baseline_kernel(Net net, const double *__restrict__ th, const double *__restrict__ obs,
+baseline_kernel(Net net, const double *__restrict__ thg, const double *__restrict__ obs,
                 const double *__restrict__ target, int n, double *ws, int rows, int use_lds,
                 double *__restrict__ slabs, double *__restrict__ pred) {
     extern __shared__ double lds64[];
     const int tid = threadIdx.x;
-    double *Y = use_lds ? lds64 : ws + (long)blockIdx.x * rows * RS;
+    // LDSY (compile time): with a run-time select hipcc cannot tell LDS from global and makes every
+    // Y access a flat load / store (one lgkmcnt for LDS and the scalar theta loads alike: round 5)
+    double *Y = LDSY ? lds64 : ws + (long)blockIdx.x * rows * RS;
+    (void)use_lds;
+    const double *th = thg;
+    if constexpr (LDSY && THL) {
+        double *tl = lds64 + rows * RS;
+        for (int q = tid; q < net.P - net.A; q += UT) tl[q] = thg[q];
+        __syncthreads();
+        th = tl;
+    }
     int roff[MAXL + 1];
     row_offsets(net, roff);
     const int tot = roff[net.nl], P = net.P, last = net.nl - 1;
@@ -1097,7 +1133,23 @@ baseline_kernel(Net net, const double *__restrict__ th, const double *__restrict
             }
             if (i >= 2) {
                 const int prev = net.L[i - 1], wo = net.woff[i - 1];
-                for (int j = 0; j < prev; ++j) {
+                // FWD_JB outputs per sweep (independent chains, one read of each g_k for all of them;
+                // each chain keeps its k-ascending order, so the sums are unchanged: round 5)
+                int j = 0;
+                for (; j + FWD_JB <= prev; j += FWD_JB) {
+                    double t[FWD_JB];
+#pragma unroll
+                    for (int jj = 0; jj < FWD_JB; ++jj) t[jj] = 0.0;
+#pragma unroll 16
+                    for (int k = 0; k < cur; ++k) {
+                        const double gk = Y[(G0 + roff[i] + k) * RS + tid];
+#pragma unroll
+                        for (int jj = 0; jj < FWD_JB; ++jj) t[jj] += gk * th[wo + (j + jj) * cur + k];
+                    }
+#pragma unroll
+                    for (int jj = 0; jj < FWD_JB; ++jj) Y[(G0 + roff[i - 1] + j + jj) * RS + tid] = t[jj];
+                }
+                for (; j < prev; ++j) {
                     double t = 0.0;
 #pragma unroll 4
                     for (int k = 0; k < cur; ++k) t += Y[(G0 + roff[i] + k) * RS + tid] * th[wo + j * cur + k];
@@ -1122,7 +1174,7 @@ struct trpo_bdev {
     double *slabs = nullptr;
     size_t slab_cap = 0;
     double *sum = nullptr;
-    int G = 1, rows = 0, use_lds = 0, lds = 0;
+    int G = 1, rows = 0, use_lds = 0, lds = 0, theta_lds = 0;
     double *hst = nullptr, *hst_dev = nullptr;   // pinned mapped host buffer: theta in, sums (+ predictions) out
     size_t hst_cap = 0;
 };
@@ -1195,12 +1247,15 @@ extern "C" trpo_bdev *trpo_bdev_create(int device, size_t nl, const size_t *ls, 
     }
     hipMemsetAsync(b->theta, 0, sizeof(double) * n.P, b->stream);
     b->rows = rows_for(n, false) * 2 + 2;
-    const size_t bytes = sizeof(double) * (size_t)b->rows * RS;
+    const size_t bytes = sizeof(double) * (size_t)b->rows * RS, tbytes = sizeof(double) * (size_t)(n.P - n.A);
     b->use_lds = bytes <= (size_t)LDS_CAP;
-    b->lds = b->use_lds ? (int)bytes : 0;
+    b->theta_lds = b->use_lds && bytes + tbytes <= (size_t)LDS_CAP;
+    b->lds = b->use_lds ? (int)(bytes + (b->theta_lds ? tbytes : 0)) : 0;
     if (b->use_lds &&
-        hipFuncSetAttribute((const void *)baseline_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_CAP) !=
-            hipSuccess) {
+        (hipFuncSetAttribute((const void *)baseline_kernel<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             LDS_CAP) != hipSuccess ||
+         hipFuncSetAttribute((const void *)baseline_kernel<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             LDS_CAP) != hipSuccess)) {
         if (err) snprintf(err, errlen, "baseline LDS attribute failed");
         trpo_bdev_destroy(b);
         return nullptr;
@@ -1258,7 +1313,11 @@ extern "C" int trpo_bdev_eval(trpo_bdev *b, const double *theta, double *gsum, d
     memcpy(hin, theta, sizeof(double) * (P - net.A));
     hipLaunchKernelGGL(copy64_kernel, dim3(cdiv(P - net.A, 256)), dim3(256), 0, b->stream,
                        (const double *)(b->hst_dev + P + 1 + b->n), b->theta, P - net.A);
-    hipLaunchKernelGGL(baseline_kernel, dim3(b->G), dim3(UT), b->lds, b->stream, net, (const double *)b->theta,
+    void (*bk)(Net, const double *, const double *, const double *, int, double *, int, int, double *, double *) =
+        b->theta_lds ? baseline_kernel<true, true> : (b->use_lds ? baseline_kernel<true, false> : baseline_kernel<false, false>);
+    hipLaunchKernelGGL(bk,
+                       dim3(b->G), dim3(UT), b->lds,
+                       b->stream, net, (const double *)b->theta,
                        (const double *)b->obs, (const double *)b->target, (int)b->n, b->ws, b->rows, b->use_lds,
                        b->slabs, b->pred);
     hipLaunchKernelGGL(sum_slabs64_kernel, dim3(cdiv(P + 1, 16)), dim3(256), 0, b->stream, b->slabs, b->G, P + 1,
