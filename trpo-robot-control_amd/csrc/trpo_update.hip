@@ -1320,10 +1320,9 @@ extern "C" int trpo_bdev_eval(trpo_bdev *b, const double *theta, double *gsum, d
                        b->stream, net, (const double *)b->theta,
                        (const double *)b->obs, (const double *)b->target, (int)b->n, b->ws, b->rows, b->use_lds,
                        b->slabs, b->pred);
+    // the sums go straight into the mapped host buffer (round 5: one copy launch fewer per callback)
     hipLaunchKernelGGL(sum_slabs64_kernel, dim3(cdiv(P + 1, 16)), dim3(256), 0, b->stream, b->slabs, b->G, P + 1,
-                       b->sum);
-    hipLaunchKernelGGL(copy64_kernel, dim3(cdiv(P + 1, 256)), dim3(256), 0, b->stream, (const double *)b->sum,
-                       b->hst_dev, P + 1);
+                       b->hst_dev);
     if (pred)
         hipLaunchKernelGGL(copy64_kernel, dim3(cdiv((long)b->n, 256)), dim3(256), 0, b->stream, (const double *)b->pred,
                            b->hst_dev + P + 1, (int)b->n);
