@@ -1163,6 +1163,106 @@ baseline_kernel(Net net, const double *__restrict__ thg, const double *__restric
     }
 }
 
+// The same objective for the [L0, L1, L2, 1] baselines with L0, L1, L2 <= 16 (the trainer's [16, 16, 16, 1]),
+// spread over lanes instead of down one lane's chain (round 5): baseline_kernel keeps a sample per lane,
+// so one wave's ~1 100 dependent fp64 multiply-adds set the kernel time (60-65 us at any N; 46 us after
+// its LDS fixes).  Here a 16-lane group works on one sample at a time, lane j owning neuron j of every
+// layer: each dot product is a 16-step chain over values broadcast within the group (ds_bpermute),
+// kept in the reference's order (bias first, inputs ascending; the backward sums from 0, ascending), so
+// every per-sample value -- prediction, residual, activation gradients -- has the bits of
+// baseline_kernel's.  Lane j accumulates its gradient entries (column j of W0 and W1, b0_j, b1_j, W2_j,
+// and b2 and sum (y - t)^2) over the group's samples in sample order; the block's 16 groups are combined
+// in group order through LDS into the block's slab (natural order, the layout baseline_kernel writes).
+// Only the order of the sums over samples differs from baseline_kernel.
+constexpr int BLK_NE = 37;                 // per-lane accumulators: 16 W0, b0, 16 W1, b1, W2, b2, sum d^2
+__global__ void __launch_bounds__(256)
+baseline_lane_kernel(Net net, const double *__restrict__ thg, const double *__restrict__ obs,
+                     const double *__restrict__ target, int n, double *__restrict__ slabs,
+                     double *__restrict__ pred) {
+    __shared__ double tl[16 * 16 * 2 + 16 * 3 + 2];     // theta (<= 16x16 + 16 + 16x16 + 16 + 16 + 1)
+    __shared__ double acc[16][BLK_NE][16];              // [group][entry][lane]
+    const int tid = threadIdx.x, lane = tid & 63, j = lane & 15, base = lane & ~15;
+    const int gi = tid >> 4;                            // group in the block, 0..15
+    const int L0 = net.L[0], L1 = net.L[1], L2 = net.L[2];
+    const int a1 = net.act[1], a2 = net.act[2], a3 = net.act[3];
+    const int W0 = net.woff[0], B0 = net.boff[0], W1 = net.woff[1], B1 = net.boff[1];
+    const int W2 = net.woff[2], B2 = net.boff[2], PA = net.P - net.A;
+    for (int q = tid; q < PA; q += 256) tl[q] = thg[q];
+    __syncthreads();
+    double dw0[16], dw1[16], db0 = 0.0, db1 = 0.0, dw2 = 0.0, db2 = 0.0, fs = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dw0[k] = dw1[k] = 0.0;
+    const int ngroups = gridDim.x * 16;
+    for (int s = blockIdx.x * 16 + gi; s < n; s += ngroups) {     // group-uniform trip count
+        // forward (forward64's order: bias first, inputs ascending)
+        const double xj = j < L0 ? obs[(long)s * L0 + j] : 0.0;
+        double xk[16], y1k[16], y2k[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) xk[k] = __shfl(xj, base + k, 64);
+        double z = j < L1 ? tl[B0 + j] : 0.0;
+        for (int k = 0; k < L0; ++k) z += xk[k] * (j < L1 ? tl[W0 + k * L1 + j] : 0.0);
+        const double y1 = j < L1 ? act_y64(a1, z) : 0.0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) y1k[k] = __shfl(y1, base + k, 64);
+        z = j < L2 ? tl[B1 + j] : 0.0;
+        for (int k = 0; k < L1; ++k) z += y1k[k] * (j < L2 ? tl[W1 + k * L2 + j] : 0.0);
+        const double y2 = j < L2 ? act_y64(a2, z) : 0.0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) y2k[k] = __shfl(y2, base + k, 64);
+        double z3 = tl[B2];
+        for (int k = 0; k < L2; ++k) z3 += y2k[k] * tl[W2 + k];
+        const double y3 = act_y64(a3, z3);
+        const double d = y3 - target[s];
+        if (j == 0) pred[s] = y3;
+        // backward (baseline_kernel's order)
+        const double g3 = act_d64(a3, y3, 0.02 * d);
+        const double g2 = j < L2 ? act_d64(a2, y2, 0.0 + g3 * tl[W2 + j]) : 0.0;
+        double g2k[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) g2k[k] = __shfl(g2, base + k, 64);
+        double t = 0.0;
+        for (int k = 0; k < L2; ++k) t += g2k[k] * (j < L1 ? tl[W1 + j * L2 + k] : 0.0);
+        const double g1 = j < L1 ? act_d64(a1, y1, t) : 0.0;
+        // this sample's gradient terms, lane j: column j of W0 and W1, b0_j, b1_j, W2_j; b2, d^2
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            dw0[k] += xk[k] * g1;
+            dw1[k] += y1k[k] * g2;
+        }
+        db0 += g1;
+        db1 += g2;
+        dw2 += y2 * g3;
+        db2 += g3;
+        fs += d * d;
+    }
+    // the block's 16 groups in group order -> slab (natural order; then sum d^2, then a zero)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        acc[gi][k][j] = dw0[k];
+        acc[gi][17 + k][j] = dw1[k];
+    }
+    acc[gi][16][j] = db0;
+    acc[gi][33][j] = db1;
+    acc[gi][34][j] = dw2;
+    acc[gi][35][j] = db2;
+    acc[gi][36][j] = fs;
+    __syncthreads();
+    double *slab = slabs + (long)blockIdx.x * (net.P + 1);
+    for (int q = tid; q <= net.P; q += 256) {
+        int e = 36, l = 0;                             // q == PA: sum d^2 (lane 0); q == P: zero
+        if (q < B0) { e = q / L1; l = q % L1; }
+        else if (q < W1) { e = 16; l = q - B0; }
+        else if (q < B1) { e = 17 + (q - W1) / L2; l = (q - W1) % L2; }
+        else if (q < W2) { e = 33; l = q - B1; }
+        else if (q < B2) { e = 34; l = q - W2; }
+        else if (q < PA) { e = 35; l = 0; }
+        double v = 0.0;
+        if (q <= PA)
+            for (int g = 0; g < 16; ++g) v += acc[g][e][l];
+        slab[q] = v;
+    }
+}
+
 struct trpo_bdev {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -1175,6 +1275,7 @@ struct trpo_bdev {
     size_t slab_cap = 0;
     double *sum = nullptr;
     int G = 1, rows = 0, use_lds = 0, lds = 0, theta_lds = 0;
+    int lane_ok = 0, Gl = 1;                       // baseline_lane_kernel applies / its grid (round 5)
     double *hst = nullptr, *hst_dev = nullptr;   // pinned mapped host buffer: theta in, sums (+ predictions) out
     size_t hst_cap = 0;
 };
@@ -1281,7 +1382,14 @@ extern "C" int trpo_bdev_set_data(trpo_bdev *b, const double *obs, const double 
     }
     b->n = n;
     b->G = n ? (cdiv((long)n, UT) < 1024 ? cdiv((long)n, UT) : 1024) : 1;
-    if (ensure(&b->slabs, &b->slab_cap, (size_t)b->G * (b->net.P + 1), b->stream)) return -2;
+    // the lane-parallel kernel: [L0, L1, L2, 1] with widths <= 16; ~2 samples per 16-lane group
+    const Net &nt = b->net;
+    const char *el = getenv("TRPO_BASELINE_LANE");
+    b->lane_ok = !(el && atoi(el) == 0) && nt.nl == 4 && nt.L[3] == 1 && nt.L[0] <= 16 && nt.L[1] <= 16 &&
+                 nt.L[2] <= 16;
+    b->Gl = n ? (cdiv((long)n, 32) < 256 ? (int)cdiv((long)n, 32) : 256) : 1;
+    const int gs = b->lane_ok && b->Gl > b->G ? b->Gl : b->G;
+    if (ensure(&b->slabs, &b->slab_cap, (size_t)gs * (b->net.P + 1), b->stream)) return -2;
     if (!b->use_lds && ensure(&b->ws, &b->ws_cap, (size_t)b->rows * RS * b->G, b->stream)) return -2;
     if (n) {
         HCHK(hipMemcpyAsync(b->obs, obs, sizeof(double) * n * L0, hipMemcpyHostToDevice, b->stream));
@@ -1313,15 +1421,21 @@ extern "C" int trpo_bdev_eval(trpo_bdev *b, const double *theta, double *gsum, d
     memcpy(hin, theta, sizeof(double) * (P - net.A));
     hipLaunchKernelGGL(copy64_kernel, dim3(cdiv(P - net.A, 256)), dim3(256), 0, b->stream,
                        (const double *)(b->hst_dev + P + 1 + b->n), b->theta, P - net.A);
-    void (*bk)(Net, const double *, const double *, const double *, int, double *, int, int, double *, double *) =
-        b->theta_lds ? baseline_kernel<true, true> : (b->use_lds ? baseline_kernel<true, false> : baseline_kernel<false, false>);
-    hipLaunchKernelGGL(bk,
-                       dim3(b->G), dim3(UT), b->lds,
-                       b->stream, net, (const double *)b->theta,
-                       (const double *)b->obs, (const double *)b->target, (int)b->n, b->ws, b->rows, b->use_lds,
-                       b->slabs, b->pred);
+    int gsl = b->G;
+    if (b->lane_ok) {
+        hipLaunchKernelGGL(baseline_lane_kernel, dim3(b->Gl), dim3(256), 0, b->stream, net, (const double *)b->theta,
+                           (const double *)b->obs, (const double *)b->target, (int)b->n, b->slabs, b->pred);
+        gsl = b->Gl;
+    } else {
+        void (*bk)(Net, const double *, const double *, const double *, int, double *, int, int, double *, double *) =
+            b->theta_lds ? baseline_kernel<true, true>
+                         : (b->use_lds ? baseline_kernel<true, false> : baseline_kernel<false, false>);
+        hipLaunchKernelGGL(bk, dim3(b->G), dim3(UT), b->lds, b->stream, net, (const double *)b->theta,
+                           (const double *)b->obs, (const double *)b->target, (int)b->n, b->ws, b->rows, b->use_lds,
+                           b->slabs, b->pred);
+    }
     // the sums go straight into the mapped host buffer (round 5: one copy launch fewer per callback)
-    hipLaunchKernelGGL(sum_slabs64_kernel, dim3(cdiv(P + 1, 16)), dim3(256), 0, b->stream, b->slabs, b->G, P + 1,
+    hipLaunchKernelGGL(sum_slabs64_kernel, dim3(cdiv(P + 1, 16)), dim3(256), 0, b->stream, b->slabs, gsl, P + 1,
                        b->hst_dev);
     if (pred)
         hipLaunchKernelGGL(copy64_kernel, dim3(cdiv((long)b->n, 256)), dim3(256), 0, b->stream, (const double *)b->pred,
