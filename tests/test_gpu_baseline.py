@@ -30,6 +30,24 @@ def test_baseline_context_matches_reference(name):
     assert cases.rel_l2(pred, exp[c["padded"]:]) <= 1e-12
 
 
+@pytest.mark.parametrize("name", BASELINE)
+def test_lane_kernel_matches_one_lane_kernel(name, monkeypatch):
+    """The lane-parallel kernel (round 5, [L0, L1, L2, 1] nets with widths <= 16) keeps every per-sample
+    value's bits (predictions identical) and changes only the order of the sums over samples; the one-lane
+    kernel (TRPO_BASELINE_LANE=0, read at set_data) stays the path for every other shape."""
+    c = cases.case(name)
+    x, obs, tgt = cases.baseline_inputs(c)
+    out = {}
+    for lane in ("1", "0"):
+        monkeypatch.setenv("TRPO_BASELINE_LANE", lane)
+        with trpo_amd.Baseline(c["layers"], c["acfunc"]) as b:
+            b.set_data(obs, tgt, c["num_ep"], c["ep_len"])
+            out[lane] = b.evaluate(x, want_predict=True)
+    np.testing.assert_array_equal(out["1"][2], out["0"][2])
+    assert abs(out["1"][0] - out["0"][0]) <= 1e-14 * abs(out["0"][0])
+    assert cases.rel_l2(out["1"][1], out["0"][1]) <= 1e-13
+
+
 def test_evaluate_drop_in_callback():
     """lbfgs()-style calls through the exported evaluate(TRPOBaselineParam*, x, g, n, step)."""
     c = cases.case("syn_baseline_n3000")
