@@ -792,6 +792,15 @@ constexpr int SCR_LD3 = TRPO_SCR_LD3;  // fvp_mlp3_kernel's transpose scratch (T
 #ifndef TRPO_NO_PF
 #define TRPO_NO_PF 0                    // experiment builds only: no register prefetch of the next tile
 #endif
+#ifndef TRPO_PF_RING
+#define TRPO_PF_RING 1                  // cached-forward kernels: the prefetch into a ring of input slots
+#endif                                  // (loop unrolled by the ring size: no per-trip register copies)
+#ifndef TRPO_PF_DEPTH
+#define TRPO_PF_DEPTH 1                 // trips between a slot's load and its use (ring of DEPTH + 1 slots)
+#endif
+#ifndef TRPO_DIAG_NOCOMPUTE
+#define TRPO_DIAG_NOCOMPUTE 0           // diagnostic builds only: the ring loop streams its inputs, no tile step
+#endif
 #ifndef TRPO_DIAG_NOLOAD
 #define TRPO_DIAG_NOLOAD 0              // diagnostic builds only: every tile reuses the first tile's inputs
 #endif                                  // (1: all of them, 2: the observations only, 3: the cached y only)
@@ -1068,8 +1077,15 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
 #else
     int tile = __builtin_amdgcn_readfirstlane(blockIdx.x * C::WAVES + wave);
 #endif
-    f4 xn[T0];
-    [[maybe_unused]] f4 yn[YC ? NYC : 1];
+    // input slots of the tile loop: slot 0 is the first trip's; the cached-forward kernels stream the
+    // later trips through a ring of PFU slots (TRPO_PF_RING), the others through one slot and a copy
+    constexpr bool RING = YC && TRPO_PF_RING && !TRPO_NO_PF && !TRPO_DIAG_NOLOAD && TRPO_BUF_PF;
+    constexpr int PFD = RING ? TRPO_PF_DEPTH : 1, PFU = RING ? PFD + 1 : 1;
+    static_assert(PFD >= 1 && PFD <= 2, "prefetch depth");
+    f4 xb[PFU][1][T0];
+    [[maybe_unused]] f4 yb[PFU][YC ? NYC : 1];
+    f4(&xn)[T0] = xb[0][0];
+    [[maybe_unused]] f4(&yn)[YC ? NYC : 1] = yb[0];
     const f4 *yc4 = reinterpret_cast<const f4 *>(A.yc);
     const int a3c = ACT >= 0 ? ((ACT >> 4) & 3) : net.act[3];
     // the loads that do not depend on the previous kernel: theta [+ v] pack and the first tile.
@@ -1092,6 +1108,17 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
             if (act_needs_y(a3c))
 #pragma unroll
                 for (int k = T1 + T2; k < NYC; ++k) yn[k] = yc4[((long)tl * NYC + k) * 64 + lane];
+        }
+        if constexpr (PFU > 2) {
+            // a two-trip-deep ring: the second trip's inputs in the same load round
+            const int t2 = max(0, min(tile + nwaves, ntiles - 1));
+#pragma unroll
+            for (int kt = 0; kt < T0; ++kt) xb[1][0][kt] = obs4[(long)(t2 * 16 + c) * (4 * T0) + kt * 4 + g];
+#pragma unroll
+            for (int k = 0; k < T1 + T2; ++k) yb[1][k] = yc4[((long)t2 * NYC + k) * 64 + lane];
+            if (act_needs_y(a3c))
+#pragma unroll
+                for (int k = T1 + T2; k < NYC; ++k) yb[1][k] = yc4[((long)t2 * NYC + k) * 64 + lane];
         }
     };
     if constexpr (!CGK) load_static();
@@ -1805,6 +1832,46 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
 #define TRPO_SETPRIO 0          // 1: the second-dispatched half of the block's waves at s_setprio 1 (guide item 4)
 #endif
     if (TRPO_SETPRIO && wave >= C::WAVES / 2) __builtin_amdgcn_s_setprio(1);
+    if constexpr (RING) {
+        // the loop unrolled by the ring size, so every slot index is a compile-time constant: trip j of a
+        // round issues the loads of trip j + PFD into slot (j + PFD) % PFU at its top (buffer loads off
+        // per-trip descriptors, clamped to the last tile) and computes on slot j -- the tile step reads
+        // the slot registers the loads landed in, with no copy (round 5: 6 v_mov_b64 per tile less)
+        while (tile < ntiles) {
+#pragma unroll
+            for (int j = 0; j < PFU; ++j) {
+                if (tile >= ntiles) break;
+                const int tn = min(tile + PFD * nwaves, ntiles - 1);
+                const int sl = (j + PFD) % PFU;
+                const auto rx = __builtin_amdgcn_make_buffer_rsrc((void *)(obs4 + (long)tn * (16 * 4 * T0)), 0,
+                                                                  16 * 64 * T0, 0x00020000);
+#pragma unroll
+                for (int kt = 0; kt < T0; ++kt)
+                    xb[sl][0][kt] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rx, pf_xoff + kt * 64, 0, 0));
+                const auto ry = __builtin_amdgcn_make_buffer_rsrc((void *)(yc4 + (long)tn * (NYC * 64)), 0, NYC * 1024,
+                                                                  0x00020000);
+#pragma unroll
+                for (int k = 0; k < T1 + T2; ++k)
+                    yb[sl][k] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ry, pf_yoff + k * 1024, 0, 0));
+                if (y3_needed)
+#pragma unroll
+                    for (int k = T1 + T2; k < NYC; ++k)
+                        yb[sl][k] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ry, pf_yoff + k * 1024, 0, 0));
+#if TRPO_PF_PIN
+                __builtin_amdgcn_sched_barrier(0);
+#endif
+                const bool live[1] = {tile * 16 + c < n};
+#if TRPO_DIAG_NOCOMPUTE
+                // diagnostic builds only: the input stream alone (the slots consumed by one add each)
+                sB1[0] += xb[j][0][0] + yb[j][0] + yb[j][T1 + T2 - 1];
+                (void)live;
+#else
+                tile_step(tile, xb[j], yb[j], live);
+#endif
+                tile += nwaves;
+            }
+        }
+    } else
     for (; tile < ntiles; tile += NT * nwaves) {
         // input tiles: lane holds features 16kt+4g..+3 of its sample (D-layout rows)
         f4 x0[NT][T0];
