@@ -3996,6 +3996,7 @@ struct trpo_dev {
     int coop_rdots;             // ... one rank: slab reduce + dots in one launch (TRPO_COOP_RDOTS, round 5)
     int coop_gmaj;              // cooperative kernel: group-major tile order (TRPO_COOP_GMAJ: 1 on, 0 off, unset auto)
     int gmaj_on;                // ... in effect for the current sample count (choose_grid)
+    int gmaj_fvp, grid_fvp;     // ... and the tile order / grid of the standalone FVP calls (choose_grid)
     int vpack_v;                // the fp32 direction pack holds slot V (written by its upload; any other
                                 // writer of the pack -- a CG, a gathered FVP -- clears it)
     int cinit;                  // cooperative CG start inside the first FVP launch (TRPO_COOP_CINIT, default 1)
@@ -4650,14 +4651,26 @@ static int choose_grid(trpo_dev *d) {
         // CG 192.0 -> 185.8 us (profiles/r05_ab_coop.log); TRPO_COOP_GMAJ=1 / 0 forces it on / off
         d->gmaj_on = d->coop && (d->coop_gmaj > 0 ||
                                  (d->coop_gmaj < 0 && (ntiles >= d->k_tiles * cus || 2 * ntiles <= cus)));
-        int g = cdiv(ntiles, d->gmaj_on ? 1 : d->k_tiles);
-        if (g > cus) g = cus;
-        if (e && atoi(e) > 0) g = atoi(e);
-        return g < 1 ? 1 : g;
+        // a standalone FVP call (slab reduce + epilogue, no CG dots) takes group-major tiles up to one tile
+        // per CU as well, while the CG launches keep the rule above (at N = 4 096 the CG is faster
+        // block-major: 192.8 vs 198.2 us).  2x64 FVP kernel at N = 3 000 (188 tiles) 7.89 -> 7.05 and
+        // 8.65 -> 8.18 us; at N = 4 096 (256 tiles, every CU one block) 7.93 -> 7.43, 8.02 -> 8.15 and
+        // 8.16 -> 8.18 us in three runs; at 6 144 it loses (profiles/r05_gmaj_fvp_ab.log).  fp32 only.
+        d->gmaj_fvp = d->gmaj_on || (d->coop && !d->f64 && d->coop_gmaj < 0 && ntiles <= cus);
+        auto grid_of = [&](int gm) {
+            int g = cdiv(ntiles, gm ? 1 : d->k_tiles);
+            if (g > cus) g = cus;
+            if (e && atoi(e) > 0) g = atoi(e);
+            return g < 1 ? 1 : g;
+        };
+        d->grid_fvp = grid_of(d->gmaj_fvp);
+        return grid_of(d->gmaj_on);
     }
     const int npass = cdiv((long)d->n, GEN_T);
     int g = npass < cus ? npass : cus;
     if (e && atoi(e) > 0) g = atoi(e);
+    d->gmaj_fvp = 0;
+    d->grid_fvp = g < 1 ? 1 : g;
     return g < 1 ? 1 : g;
 }
 
@@ -4714,11 +4727,12 @@ extern "C" int trpo_dev_set_obs(trpo_dev *d, const double *obs, size_t n) {
             d->scratch_blocks = d->grid;
         }
     }
-    if (d->grid > d->slab_blocks) {
+    const int sblocks = d->grid > d->grid_fvp ? d->grid : d->grid_fvp;     // CG and FVP-call grids
+    if (sblocks > d->slab_blocks) {
         if (d->slabs) hipFree(d->slabs);
-        HCHK(trpo_malloc((void **)&d->slabs, d->esz * (size_t)d->slab * d->grid));
-        HCHK(hipMemsetAsync(d->slabs, 0, d->esz * (size_t)d->slab * d->grid, d->stream));
-        d->slab_blocks = d->grid;
+        HCHK(trpo_malloc((void **)&d->slabs, d->esz * (size_t)d->slab * sblocks));
+        HCHK(hipMemsetAsync(d->slabs, 0, d->esz * (size_t)d->slab * sblocks, d->stream));
+        d->slab_blocks = sblocks;
     }
     HCHK(hipGetLastError());
     DSYNC(d);
@@ -5310,15 +5324,17 @@ static IterArgs plain_args(trpo_dev *d, const int *skip) {
 
 // block partials (fp32, or fp64 in the fp64 mode) -> d->zacc, fixed order; with zout the FVP
 // epilogue (z = sum / N + damping v, log-std block 2 v + damping v) is applied on the way
+// (grid: the producing launch's block count, default the CG grid)
 static void launch_reduce(trpo_dev *d, const int *skip, const double *vin = nullptr, double *zout = nullptr,
-                          double *zh = nullptr) {
+                          double *zh = nullptr, int grid = 0) {
+    const int G = grid > 0 ? grid : d->grid;
     if (d->f64)
         hipLaunchKernelGGL(reduce_slabs_kernel<double>, dim3(d->slab / RS_POS), dim3(RS_THREADS), 0, d->stream,
-                           (const double *)d->slabs, d->grid, d->slab, d->imap, d->zacc, skip, vin, zout, d->ctl,
+                           (const double *)d->slabs, G, d->slab, d->imap, d->zacc, skip, vin, zout, d->ctl,
                            d->nw, d->P, zh);
     else
         hipLaunchKernelGGL(reduce_slabs_kernel<float>, dim3(d->slab / RS_POS), dim3(RS_THREADS), 0, d->stream,
-                           (const float *)d->slabs, d->grid, d->slab, d->imap, d->zacc, skip, vin, zout, d->ctl,
+                           (const float *)d->slabs, G, d->slab, d->imap, d->zacc, skip, vin, zout, d->ctl,
                            d->nw, d->P, zh);
 }
 
@@ -5326,10 +5342,12 @@ static void launch_reduce(trpo_dev *d, const int *skip, const double *vin = null
 // changed writes the forward-activation cache (MODE 0), later ones read it (MODE 2)
 static int allreduce(trpo_dev *d, double *buf, size_t count);
 
-// Returns the atomic replica set it accumulated into (atomic mode) or NULL (block slabs).
+// Returns the atomic replica set it accumulated into (atomic mode) or NULL (block slabs: d->grid_fvp of
+// them, the FVP-call grid and tile order).
 // sink: a kernel-only launch whose result is never consumed (timing): accumulates into the sink set.
 static double *launch_fvp_plain(trpo_dev *d, IterArgs &a, bool sink = false) {
     double *acc = NULL;
+    a.gmaj = d->gmaj_fvp;
     if (d->atomic) {
         // fp64 atomics into R replicas, like the CG kernels (no slab round trip through HBM); the
         // set is zero on entry because its consumer, acc_epilogue_kernel, leaves it zeroed
@@ -5339,10 +5357,10 @@ static double *launch_fvp_plain(trpo_dev *d, IterArgs &a, bool sink = false) {
     }
     if (d->yc_on) {
         a.yc = reinterpret_cast<float4 *>(d->yc);
-        (d->yc_valid ? d->k_fvp_yc : d->k_fvp)(dim3(d->grid), d->k_lds, d->stream, a, d->net);
+        (d->yc_valid ? d->k_fvp_yc : d->k_fvp)(dim3(d->grid_fvp), d->k_lds, d->stream, a, d->net);
         d->yc_valid = 1;
     } else {
-        d->k_fvp(dim3(d->grid), d->k_lds, d->stream, a, d->net);
+        d->k_fvp(dim3(d->grid_fvp), d->k_lds, d->stream, a, d->net);
     }
     return acc;
 }
@@ -5367,9 +5385,15 @@ static int enqueue_fvp_core(trpo_dev *d, const double *src, const int *skip) {
     if (d->fast) {
         // src has already been packed into d->vpack (by the caller or the CG kernels)
         IterArgs a = plain_args(d, skip);
-        if (skip == &d->ctl->zero && !d->atomic) launch_fvp_plain(d, a);
-        else d->k_fvp(dim3(d->grid), d->k_lds, d->stream, a, n);
+        if (skip == &d->ctl->zero && !d->atomic) {
+            launch_fvp_plain(d, a);
+            launch_reduce(d, skip, nullptr, nullptr, nullptr, d->grid_fvp);
+        } else {
+            d->k_fvp(dim3(d->grid), d->k_lds, d->stream, a, n);
+            launch_reduce(d, skip);
+        }
         HCHK(hipGetLastError());
+        return allreduce(d, d->zacc, d->nw);
     } else {
         hipLaunchKernelGGL(to_elem_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, d->gv, src, (long)d->P,
                            d->f64);
@@ -5402,7 +5426,7 @@ static int fvp_src(trpo_dev *d, const double *src, double **zh) {
                                src, d->vec[TRPO_VEC_Z], d->P, d->Ps, d->nw, d->ctl, zhost);
             *zh = zhost;
         } else {
-            launch_reduce(d, &d->ctl->zero, src, d->vec[TRPO_VEC_Z], zhost);
+            launch_reduce(d, &d->ctl->zero, src, d->vec[TRPO_VEC_Z], zhost, d->grid_fvp);
             *zh = zhost;
         }
         HCHK(hipGetLastError());
