@@ -3437,20 +3437,22 @@ cg_last_kernel(const double *__restrict__ acc, int R_in, const double *__restric
     double2 za[RMAX];
 #pragma unroll
     for (int k = 0; k < RMAX; ++k) za[k] = pair_at(acc, min(k, R_in - 1), Ps);
-    if (done) {
-        for (int e = tid; e < zero_len; e += CGL_T) acc_zero[e] = 0.0;   // inputs unused
-        return;
-    }
-    const double pe[2] = {p2.x, p2.y}, re[2] = {r2.x, r2.y}, xe[2] = {x2.x, x2.y};
-    // the replica values pinned in registers here: z is only used for q < nw, and with the fp64 division
-    // behind it hipcc turned that select into a branch and sank half the replica loads into it (issued
-    // after the first round had drained: a second round trip, round 5)
+    // every loaded value pinned in registers BEFORE the done test: z is only used for q < nw, and with
+    // the fp64 division behind it hipcc turned that select into a branch and sank half the replica loads
+    // into it (a second round trip, round 5); and with the pins after the done test it sank all of them
+    // below that test, behind the ctl->done load (a third round trip: kernel arguments, ctl, vectors)
     double zr[2][RMAX];
 #pragma unroll
     for (int k = 0; k < RMAX; ++k) {
         zr[0][k] = za[k].x;
         zr[1][k] = za[k].y;
         asm volatile("" : "+v"(zr[0][k]), "+v"(zr[1][k]));
+    }
+    double pe[2] = {p2.x, p2.y}, re[2] = {r2.x, r2.y}, xe[2] = {x2.x, x2.y};
+    asm volatile("" : "+v"(pe[0]), "+v"(pe[1]), "+v"(re[0]), "+v"(re[1]), "+v"(xe[0]), "+v"(xe[1]));
+    if (done) {
+        for (int e = tid; e < zero_len; e += CGL_T) acc_zero[e] = 0.0;   // inputs unused
+        return;
     }
     double pv[2], rv[2], xv[2], zv[2];
 #pragma unroll
