@@ -494,12 +494,17 @@ def bench_update(device, L=ARM, n=N_TOTAL, reps=20, cpu_ref=True):
     ctx.set_rollout(mean, action, adv)
     for _ in range(3):      # warm-up: first-call allocations, CG graph capture
         r = ctx.update()
+    # the stall guard: an update whose solve it re-ran in fp64 says so (trpo_ctx_cg_status,
+    # read by update()); counted over the timed updates so the row shows whether its time includes any
+    reruns = 0
     t0 = time.perf_counter()
     for _ in range(reps):
         r = ctx.update()
+        reruns += bool(r["fp64_rerun"])
     wall = (time.perf_counter() - t0) / reps
     ctx.close()
     out = {"update_ms": 1e3 * wall, "accepted": r["accepted"], "cg_iters": int(r["cg_iters"]), "samples": n,
+           "fp64_reruns": reruns, "updates_timed": reps, "ritz_residual": r["ritz_residual"],
            "what": "policy gradient (fp32 tile kernel, fp64 sums) + CG(10, 1e-10) + FVP(x) + fp64 line search"}
     if cpu_ref and os.path.exists(oracle.REF_DRIVER_FAST):
         with tempfile.TemporaryDirectory() as tmp:
@@ -583,7 +588,7 @@ def c5_iteration(u, bl):
     if "device_evaluate_fit_ms" not in fit:
         return {"error": "no caller-liblbfgs fit timing: %s" % fit.get("error")}
     cpu_u = u.get("cpu_reference_compute_s_1core")
-    return {"device_ms": u["update_ms"] + fit["device_evaluate_fit_ms"],
+    return {"device_ms": u["update_ms"] + fit["device_evaluate_fit_ms"], "fp64_reruns": u.get("fp64_reruns"),
             "cpu_reference_ms_1core": (1e3 * cpu_u + fit["reference_cpu_evaluate_fit_ms_1core"]
                                        if cpu_u is not None else None),
             "what": "TRPO_Update (N=50000, device) + the value-baseline fit by the caller's liblbfgs 1.10 "
@@ -752,11 +757,14 @@ def _update_body(dist):
         r = None
         for _ in range(3):
             r = agreed(dist, tag + ".warmup-update", ctx.update)
+        reruns = 0
         t0 = time.perf_counter()
         for _ in range(20):
             r = agreed(dist, tag + ".update", ctx.update)
+            reruns += bool(r["fp64_rerun"])
         wall = dist.max((time.perf_counter() - t0) / 20)
         return {"update_ms": 1e3 * wall, "accepted": r["accepted"], "cg_iters": int(r["cg_iters"]),
+                "fp64_reruns": reruns, "updates_timed": 20,
                 "samples": N_TOTAL, "n_gpus": dist.world, "comm": ctx.comm_backend,
                 "what": "sharded rollout; all-reduces of the policy gradient, every FVP and the surrogate sums; "
                         "host-visible wall per update (max over ranks; each update followed by a cross-rank "
@@ -816,15 +824,19 @@ def latest_traffic_json():
 
 
 PMC_KERNEL = "fvp_mlp3_kernel<1, 1, 1, 1, 5, 3"       # the CG-iteration kernel (MODE 3, every QB variant)
+N_SIMDS = 1024                                        # 256 CUs x 4 SIMDs (MI355X)
+N_XCDS = 8
 
 
 def pmc_child(device):
-    """--pmc-child: the headline workload (armDOF_0, the seeded 50k batch, b) for a few CG solves,
-    run by measure_traffic under rocprofv3's counter collection; nothing printed on stdout."""
+    """--pmc-child: the headline workload (armDOF_0, the seeded batch of TRPO_PMC_N samples -- 50k unless
+    set --, b) for a few CG solves, run by pmc_pass under rocprofv3's counter collection; nothing printed
+    on stdout."""
     from trpo_amd import synth
-    ctx, _, _ = make_ctx(ARM, N_TOTAL, _OneRank(), device)
+    n = int(os.environ.get("TRPO_PMC_N", N_TOTAL))
+    ctx, _, _ = make_ctx(ARM, n, _OneRank(), device)
     ctx.upload_b(synth.make_b(num_params(ARM)))
-    for _ in range(5):
+    for _ in range(5 if n <= 500_000 else 2):
         ctx.enqueue_cg(CG_ITERS, 0.0)
     ctx.synchronize()
     ctx.close()
@@ -847,44 +859,84 @@ def pmc_median(path, counter, kernel=PMC_KERNEL):
     return (statistics.median(per.values()), len(per)) if per else None
 
 
-def measure_traffic(device):
-    """roofline.traffic measured in this run (N = 1): two child processes of this script (--pmc-child, the
-    headline workload) under rocprofv3, one counter per pass as MI355X_MICROARCH.md's HBM section
-    prescribes (FETCH_SIZE, then WRITE_SIZE, each in its own run, kernel dispatches serialised by the
-    profiler), each pass under its own hard time limit; per-launch HBM bytes of the CG-iteration kernel =
-    2 x median FETCH_SIZE (the gfx950 wide-read undercount) + median WRITE_SIZE, KiB -> bytes.  The
-    parent is idle meanwhile (after its timed region).  Returns (bytes, source) or (None, reason)."""
+def pmc_pass(device, counters, n=N_TOTAL, limit=90):
+    """One rocprofv3 counter pass (its own child process of this script, --pmc-child, on the headline
+    workload at n samples, under its own hard time limit): {counter: (median per dispatch of the
+    CG-iteration kernel, dispatches)}, or (None, reason).  The counters of one pass must fit the
+    hardware's slots (MI355X_MICROARCH.md: SQ 8, TCC 4 with FETCH_SIZE = 3 and WRITE_SIZE = 2, GRBM 2)."""
     import shutil
     prof = shutil.which("rocprofv3") or ("/opt/rocm/bin/rocprofv3" if os.path.exists("/opt/rocm/bin/rocprofv3") else None)
     if not prof:
         return None, "rocprofv3 not found"
-    med = {}
     with tempfile.TemporaryDirectory(prefix="trpo_pmc_") as tmp:
-        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
-            out = os.path.join(tmp, counter)
-            cmd = ["timeout", "-s", "KILL", "90", prof, "--pmc", counter, "--output-format", "csv", "-d", out,
-                   "-o", "run", "--", sys.executable, os.path.abspath(__file__), "--pmc-child"]
-            env = dict(os.environ, TRPO_BENCH_DEVICE=str(device))
-            try:
-                r = subprocess.run(cmd, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
-                                   timeout=120)
-            except (OSError, subprocess.SubprocessError) as e:      # no `timeout` binary, a stuck child, ...
-                return None, "rocprofv3 --pmc %s: %s: %s" % (counter, type(e).__name__, e)
-            if r.returncode != 0:
-                return None, "rocprofv3 --pmc %s exited %d: %s" % (counter, r.returncode, r.stderr[-300:].strip())
-            files = [os.path.join(dp, fn) for dp, _, fns in os.walk(out) for fn in fns
-                     if fn.endswith("counter_collection.csv")]
-            if not files:
-                return None, "no counter_collection.csv from the %s pass" % counter
-            m = pmc_median(files[0], counter)
+        cmd = ["timeout", "-s", "KILL", str(limit), prof, "--pmc", *counters, "--output-format", "csv", "-d", tmp,
+               "-o", "run", "--", sys.executable, os.path.abspath(__file__), "--pmc-child"]
+        env = dict(os.environ, TRPO_BENCH_DEVICE=str(device), TRPO_PMC_N=str(n))
+        try:
+            r = subprocess.run(cmd, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
+                               timeout=limit + 30)
+        except (OSError, subprocess.SubprocessError) as e:      # no `timeout` binary, a stuck child, ...
+            return None, "rocprofv3 --pmc %s: %s: %s" % (" ".join(counters), type(e).__name__, e)
+        if r.returncode != 0:
+            return None, "rocprofv3 --pmc %s exited %d: %s" % (" ".join(counters), r.returncode, r.stderr[-300:].strip())
+        files = [os.path.join(dp, fn) for dp, _, fns in os.walk(tmp) for fn in fns
+                 if fn.endswith("counter_collection.csv")]
+        if not files:
+            return None, "no counter_collection.csv from the %s pass" % " ".join(counters)
+        med = {}
+        for c in counters:
+            m = pmc_median(files[0], c)
             if m is None:
-                return None, "no %s dispatches of %s" % (counter, PMC_KERNEL)
-            med[counter] = m
+                return None, "no %s dispatches of %s" % (c, PMC_KERNEL)
+            med[c] = m
+        return med, None
+
+
+def measure_traffic(device):
+    """roofline.traffic measured in this run (N = 1): two counter passes (pmc_pass) as MI355X_MICROARCH.md's
+    HBM section prescribes (FETCH_SIZE, then WRITE_SIZE, each in its own run, kernel dispatches serialised
+    by the profiler); per-launch HBM bytes of the CG-iteration kernel = 2 x median FETCH_SIZE (the gfx950
+    wide-read undercount) + median WRITE_SIZE, KiB -> bytes.  The parent is idle meanwhile (after its
+    timed region).  Returns (bytes, source) or (None, reason)."""
+    med = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        m, why = pmc_pass(device, (counter,))
+        if m is None:
+            return None, why
+        med.update(m)
     fetch = 2.0 * med["FETCH_SIZE"][0] * 1024
     write = med["WRITE_SIZE"][0] * 1024
     return fetch + write, {"measured": "in this run", "fetch_bytes": fetch, "write_bytes": write,
                            "dispatches": [med["FETCH_SIZE"][1], med["WRITE_SIZE"][1]],
                            "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount) + WRITE_SIZE"}
+
+
+MFMA_COUNTERS = ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_MFMA", "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES", "SQ_WAIT_INST_ANY",
+                 "GRBM_GUI_ACTIVE")
+
+
+def mfma_from_counters(med):
+    """MFMA utilisation of the CG-iteration kernel from one counter pass (medians per dispatch):
+    SQ_VALU_MFMA_BUSY_CYCLES (cycles, summed over every SIMD) / (1 024 SIMDs x GRBM_GUI_ACTIVE / 8), the
+    dispatch's GPU-active cycles per XCD (MI355X_MICROARCH.md: GRBM_GUI_ACTIVE is the sum over the 8 XCDs,
+    and reads high on dispatches shorter than ~0.3 ms, so at 50k this is a lower bound)."""
+    busy, grbm = med["SQ_VALU_MFMA_BUSY_CYCLES"][0], med["GRBM_GUI_ACTIVE"][0]
+    out = {"mfma_busy_frac": busy / (N_SIMDS * grbm / N_XCDS) if grbm > 0 else None,
+           "mfma_busy_denominator": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs) "
+                                    "per dispatch of the CG-iteration kernel (medians); a lower bound on "
+                                    "dispatches < 0.3 ms",
+           "counters": {c: m[0] for c, m in med.items()}, "dispatches": med["GRBM_GUI_ACTIVE"][1]}
+    if med.get("SQ_WAVE_CYCLES", (0,))[0] > 0:
+        out["wait_inst_any_frac"] = med["SQ_WAIT_INST_ANY"][0] / med["SQ_WAVE_CYCLES"][0]
+    return out
+
+
+def measure_mfma(device, n=N_TOTAL):
+    """roofline.mfma_busy_frac (VERDICT r05 #2): one counter pass (6 SQ + 1 GRBM slots) at n samples."""
+    med, why = pmc_pass(device, MFMA_COUNTERS, n=n, limit=150 if n > 500_000 else 90)
+    if med is None:
+        return {"error": why}
+    return dict(mfma_from_counters(med), measured="in this run", samples=n)
 
 
 def main():
@@ -1025,6 +1077,16 @@ def main():
         traffic, tsrc = None, None
         if not args.no_pmc and os.environ.get("TRPO_TRAFFIC_JSON") is None:
             traffic, tsrc = measure_traffic(device)
+            mf = measure_mfma(device)
+            with emitter.lock:
+                result["roofline"]["mfma_busy_frac"] = mf.get("mfma_busy_frac")
+                result["roofline"]["mfma"] = mf
+            row4m = (extra or {}).get("C4_sweep", {}).get("cg10_armDOF_0_N4000000")
+            if isinstance(row4m, dict) and "error" not in row4m:
+                mf4 = measure_mfma(device, 4_000_000)
+                with emitter.lock:
+                    row4m["mfma_busy_frac"] = mf4.get("mfma_busy_frac")
+                    row4m["mfma"] = mf4
         if traffic is None:
             # fallback: HBM bytes per launch of this kernel at this workload from the newest committed
             # rocprofv3 PMC passes (tools/profile_round.sh: FETCH_SIZE x2 + WRITE_SIZE, separate passes)

@@ -71,7 +71,7 @@ class FakeContext:
         pass
 
     def update(self, *a, **k):
-        return dict(accepted=True, cg_iters=10)
+        return dict(accepted=True, cg_iters=10, fp64_rerun=False)
 
     @property
     def kernel_name(self):

@@ -255,3 +255,30 @@ def test_measure_traffic_without_profiler(monkeypatch):
     monkeypatch.setattr(shutil, "which", lambda name: None)
     monkeypatch.setattr(bench.os.path, "exists", lambda p: False)
     assert bench.measure_traffic(0) == (None, "rocprofv3 not found")
+
+
+def test_mfma_busy_from_counters():
+    """roofline.mfma_busy_frac: SQ_VALU_MFMA_BUSY_CYCLES (summed over every SIMD) over
+    1 024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs.  Round 5's committed counters of the 50k kernel
+    (profiles/r05_sq_counters_cgiter.txt: 3.0 M busy cycles, ~9 us at ~2.3 GHz) read ~14 %; a dispatch
+    whose every SIMD issued MFMAs for its whole active time reads 1."""
+    import bench
+    med = {"SQ_VALU_MFMA_BUSY_CYCLES": (3.0e6, 9), "SQ_INSTS_MFMA": (112500.0, 9), "SQ_BUSY_CYCLES": (624725.0, 9),
+           "SQ_WAVE_CYCLES": (9.04e6, 9), "SQ_WAIT_INST_ANY": (2.65e6, 9), "GRBM_GUI_ACTIVE": (8 * 20700.0, 9)}
+    m = bench.mfma_from_counters(med)
+    assert abs(m["mfma_busy_frac"] - 3.0e6 / (1024 * 20700.0)) < 1e-12
+    assert 0.13 < m["mfma_busy_frac"] < 0.15
+    assert abs(m["wait_inst_any_frac"] - 2.65e6 / 9.04e6) < 1e-12
+    assert m["dispatches"] == 9 and "GRBM_GUI_ACTIVE" in m["mfma_busy_denominator"]
+    full = dict(med, SQ_VALU_MFMA_BUSY_CYCLES=(1024 * 20700.0, 9))
+    assert abs(bench.mfma_from_counters(full)["mfma_busy_frac"] - 1.0) < 1e-12
+
+
+def test_measure_mfma_without_profiler(monkeypatch):
+    """No rocprofv3: measure_mfma returns the reason, no exception (the line then carries null)."""
+    import shutil
+    import bench
+    monkeypatch.setattr(shutil, "which", lambda name: None)
+    monkeypatch.setattr(bench.os.path, "exists", lambda p: False)
+    assert bench.measure_mfma(0) == {"error": "rocprofv3 not found"}
+    assert bench.measure_mfma(0, 4_000_000) == {"error": "rocprofv3 not found"}

@@ -93,13 +93,15 @@ def test_peer_cg_lockstep_and_golden(bounds):
     assert cases.rel_l2(x0, cases.expected(c)) <= CG_TOL
 
 
-@pytest.mark.parametrize("proto", ["0", "1", "2", "3", "4"])
+@pytest.mark.parametrize("proto", ["1", "3", "4"])
 def test_peer_exchange_forms_agree(proto, monkeypatch):
-    """The four forms of the exchange kernel (TRPO_PEER_PROTO, read when the window is created):
-    0 the round-3 per-element loops, 1 the batched load rounds (default), 2 the flagless tagged
-    granules, 3 the granules on a compile-time world (round 5: the own rank's sum never travels).  Same rank-order sums => the CG solve (the replica-set exchange of the CG graph) and a
-    standalone FVP (the in-place exchange) are bit-identical across the forms (checked against form 1
-    run here), on three ranks with ragged shards (slices that are not a multiple of the load round)."""
+    """The three forms of the exchange kernel (TRPO_PEER_PROTO, read when the window is created): 1 the
+    flag hand-off with batched load rounds (the default through round 4), 3 the tagged granules on a
+    compile-time world (the own rank's sum never travels), 4 the same with separate pushing and polling
+    workgroups (the default since round 5).  Same rank-order sums => the CG solve (the replica-set
+    exchange of the CG graph) and a standalone FVP (the in-place exchange) are bit-identical across the
+    forms (checked against form 1 run here), on three ranks with ragged shards (slices that are not a
+    multiple of the load round)."""
     c = cases.case("syn_arm_cg_n50000")
     x = cases.inputs(c)
     bounds = [(0, 10000), (10000, 30001), (30001, 50000)]
@@ -120,7 +122,7 @@ def test_peer_exchange_forms_agree(proto, monkeypatch):
     for r in range(len(bounds)):
         np.testing.assert_array_equal(got[r][0], ref[0][0])     # CG: lockstep and equal to form 1
         np.testing.assert_array_equal(got[r][1], ref[0][1])     # standalone FVP (in-place exchange)
-        assert ("tagged granules" in got[r][2]) == (proto in ("2", "3", "4")), got[r][2]
+        assert ("tagged granules" in got[r][2]) == (proto in ("3", "4")), got[r][2]
     assert cases.rel_l2(got[0][0], cases.expected(c)) <= CG_TOL
 
     # a long message: the 2x64 policy's FVP (P = 5 443 > one load round of 4 x 256 elements; slices
@@ -266,20 +268,30 @@ def test_peer_slab_paths_torch_runtime_first():
     assert r.stdout.count("ok ") == 6, r.stdout
 
 
-def test_peer_missing_rank_times_out():
+@pytest.mark.parametrize("proto", ["1", "4"])
+def test_peer_missing_rank_times_out(proto, monkeypatch, capfd):
     """Only rank 0 of a world of 2 attaches: its exchange (the shard-size all-reduce of the attach)
-    waits 3 s for rank 1, then gives up with an error -- the GPU is released, nothing hangs."""
+    waits TRPO_PEER_WAIT_MS for rank 1, then gives up with an error -- the GPU is released, nothing hangs
+    -- and says why on stderr: which rank, workgroup and exchange waited, for which
+    peer's slot, and the tag it last read there (the flag form: the flag value)."""
+    monkeypatch.setenv("TRPO_PEER_PROTO", proto)
+    monkeypatch.setenv("TRPO_PEER_WAIT_MS", "500")
     c = cases.case("fix_fvp_n3150")
     x = cases.inputs(c)
     ctxs = _shards(x, [(0, 1000), (1000, 3150)])
     try:
         for ctx in ctxs:
             ctx.peer_handle()
+        capfd.readouterr()
         with pytest.raises(trpo_amd.TRPOError):
             ctxs[0].attach_peers_local(0, ctxs)
+        err = capfd.readouterr().err
     finally:
         for ctx in ctxs:
             ctx.close()
+    assert "peer exchange timed out: rank 0 of 2" in err, err
+    assert "exchange 1: after 0.5 s no data from rank 1" in err, err
+    assert ("tag 0, expected 1; form %s" % proto) in err, err
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])

@@ -185,3 +185,34 @@ def test_repeated_updates_deterministic(layers, monkeypatch):
     for a, e in zip(graph, eager):
         for x, y in zip(a, e):
             np.testing.assert_array_equal(x, y)
+
+
+@pytest.mark.parametrize("solves", ["update", "enqueue_cg"])
+def test_fvp_of_v_after_replayed_solves(solves, monkeypatch):
+    """the cooperative kernel's direction pack holds V after an upload, and every CG
+    solve overwrites it with its directions -- also a solve replayed from the captured graph, whose
+    host-side enqueue ran only at capture.  Sequence: upload V, two graph-mode solves (the update path's
+    CG is always the replayed graph; enqueue_cg with TRPO_CG_GRAPH=1), then an FVP of slot V: it must be
+    F v, not F of the last CG direction."""
+    from trpo_amd import synth
+    layers, n = [15, 64, 64, 3], 3000                   # 2x64: the cooperative kernel (pre-packed direction)
+    th, obs = synth.make_theta(layers), synth.make_obs(n, layers[0])
+    std = np.ones(layers[-1])
+    v = synth.make_v(synth.num_params(layers))
+    if solves == "enqueue_cg":
+        monkeypatch.setenv("TRPO_CG_GRAPH", "1")
+    with trpo_amd.Context(layers, "lttl", th, obs, std, 0.1) as ctx:
+        z_ref = ctx.fvp(v)
+        mean, action, adv = synth.make_rollout(layers, "lttl", th, obs, std)
+        ctx.set_rollout(mean, action, adv)
+        ctx.upload_b(synth.make_b(synth.num_params(layers)))
+        ctx.upload_v(v)
+        for _ in range(2):
+            if solves == "update":
+                ctx.update()
+            else:
+                ctx.enqueue_cg(10, 0.0)
+        ctx.enqueue_fvp()
+        ctx.synchronize()
+        z = ctx.download_z()
+    assert cases.rel_l2(z, z_ref) <= 1e-6

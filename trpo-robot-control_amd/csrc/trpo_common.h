@@ -133,8 +133,8 @@ int trpo_peer_allreduce(trpo_peer *p, hipStream_t st, const double *in, int R, i
                         const int *done);
 int trpo_peer_error(const trpo_peer *p);
 size_t trpo_peer_slot(const trpo_peer *p);
-int trpo_peer_fenced(const trpo_peer *p);
-int trpo_peer_proto(const trpo_peer *p);      // 1 flag + batched loads, 2 tagged granules, 0 round-3 loops
+int trpo_peer_proto(const trpo_peer *p);      // 1 flag form, 3 / 4 tagged granules (4: split roles)
+void trpo_peer_report(trpo_peer *p);          // prints a failed exchange's error records once (stderr)
 void trpo_peer_set_error(trpo_peer *p);
 
 #endif

@@ -5075,7 +5075,7 @@ extern "C" int trpo_dev_comm_verify(trpo_dev *d, long timeout_ms, long *bad) {
     // a buffer that exists already (no allocation while another rank's exchange may be waiting):
     // the atomic sink set (never consumed) or the slab-path reduced vector (rewritten by every FVP)
     double *buf = d->atomic ? d->pacc + (long)d->R * d->Ps : d->zacc;
-    if (ensure_hst(d, count, true)) return -2;
+    if (const int hrc = ensure_hst(d, count, true)) return hrc;
     for (size_t i = 0; i < count; ++i) d->hst[i] = ldexp((double)(1 + i % 251), d->rank);
     if (comm_fault(d, "verify")) d->hst[0] += 1.0;
     hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv((long)count, 256)), dim3(256), 0, d->stream,
@@ -5161,10 +5161,13 @@ extern "C" int trpo_dev_set_peers(trpo_dev *d, int rank, int world, const void *
     return rn ? rn : trpo_dev_comm_error(d);
 }
 
-// -4 after a peer exchange whose wait timed out (a rank missing) or an abort; 0 otherwise
+// -4 after a peer exchange whose wait timed out (a rank missing) or an abort; 0 otherwise.  A timed-out
+// exchange's records (rank, workgroup, exchange, missing peer, tag seen) go to stderr the first time.
 extern "C" int trpo_dev_comm_error(const trpo_dev *d) {
     if (d && d->comm_aborted) return -4;
-    return d && d->peer_on && trpo_peer_error(d->peer) ? -4 : 0;
+    if (!(d && d->peer_on && trpo_peer_error(d->peer))) return 0;
+    trpo_peer_report(d->peer);
+    return -4;
 }
 
 extern "C" const char *trpo_hip_runtime_path(void) {
@@ -5177,9 +5180,8 @@ extern "C" const char *trpo_dev_comm_backend(const trpo_dev *d) {
     if (!d) return "";
     if (d->comm_aborted) return "aborted";
     if (d->peer_on)
-        return trpo_peer_proto(d->peer) >= 2 ? "peer-xgmi (uncached window, tagged granules)"
-               : trpo_peer_fenced(d->peer)   ? "peer-xgmi (uncached window, fenced hand-off)"
-                                             : "peer-xgmi (uncached window)";
+        return trpo_peer_proto(d->peer) != 1 && d->world <= 8 ? "peer-xgmi (uncached window, tagged granules)"
+                                                                : "peer-xgmi (uncached window, fenced hand-off)";
     if (d->comm) return "rccl";
     if (d->group) return "host-group";
     return "none";
@@ -5206,6 +5208,7 @@ __global__ void vcopy_pack_kernel(const double *__restrict__ src, double *__rest
 }
 // host_writes: the caller is about to write the buffer from the host (an upload); device-side
 // writers (downloads) are ordered after a pending upload's copy by the stream and need no wait
+// (its return code is passed on unchanged: -4 when the wait it needed found the collective failed)
 static int ensure_hst(trpo_dev *d, size_t count, bool host_writes = false) {
     if (d->hst_pending && (host_writes || count > d->hst_cap || !d->hst)) {
         DSYNC(d);
@@ -5224,7 +5227,7 @@ static int ensure_hst(trpo_dev *d, size_t count, bool host_writes = false) {
 extern "C" int trpo_dev_upload(trpo_dev *d, int slot, const double *host) {
     if (!d || slot < 0 || slot > 4 || !host) return -1;
     HCHK(hipSetDevice(d->device));
-    if (ensure_hst(d, (size_t)d->P + 2 * (size_t)(d->hist_cap + 8), true)) return -2;
+    if (const int hrc = ensure_hst(d, (size_t)d->P + 2 * (size_t)(d->hist_cap + 8), true)) return hrc;
     memcpy(d->hst, host, sizeof(double) * d->P);
     if (slot == TRPO_VEC_V && d->coop_pk) {
         hipLaunchKernelGGL(vcopy_pack_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream,
@@ -5244,7 +5247,7 @@ extern "C" int trpo_dev_upload(trpo_dev *d, int slot, const double *host) {
 extern "C" int trpo_dev_download(trpo_dev *d, int slot, double *host) {
     if (!d || slot < 0 || slot > 4 || !host) return -1;
     HCHK(hipSetDevice(d->device));
-    if (ensure_hst(d, (size_t)d->P + 2 * (size_t)(d->hist_cap + 8))) return -2;
+    if (const int hrc = ensure_hst(d, (size_t)d->P + 2 * (size_t)(d->hist_cap + 8))) return hrc;
     hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream, (const double *)d->vec[slot],
                        d->hst_dev, d->P);
     HCHK(hipGetLastError());
@@ -5261,7 +5264,7 @@ extern "C" int trpo_dev_download_x_cg(trpo_dev *d, double *host, double *stats, 
     if (!d || !host || !stats || !rdotr || !iters) return -1;
     HCHK(hipSetDevice(d->device));
     const int cw = (int)cdiv(sizeof(Ctl), sizeof(double)), hw = 2 * d->hist_cap;
-    if (ensure_hst(d, (size_t)d->P + cw + hw)) return -2;
+    if (const int hrc = ensure_hst(d, (size_t)d->P + cw + hw)) return hrc;
     hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv(d->P, 256)), dim3(256), 0, d->stream,
                        (const double *)d->vec[TRPO_VEC_X], d->hst_dev, d->P);
     hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv(cw, 256)), dim3(256), 0, d->stream, (const double *)d->ctl,
@@ -5459,7 +5462,7 @@ extern "C" int trpo_dev_fvp(trpo_dev *d) { return d ? trpo_dev_fvp_src(d, d->vec
 extern "C" int trpo_dev_fvp_host(trpo_dev *d, double *host) {
     if (!d || !host) return -1;
     HCHK(hipSetDevice(d->device));
-    if (ensure_hst(d, (size_t)d->P + 2 * (size_t)(d->hist_cap + 8))) return -2;
+    if (const int hrc = ensure_hst(d, (size_t)d->P + 2 * (size_t)(d->hist_cap + 8))) return hrc;
     double *zh = d->hst_dev;                     // ordered after a pending upload's copy by the stream
     int rc = fvp_src(d, d->vec[TRPO_VEC_V], &zh);
     if (rc) return rc;
@@ -5797,6 +5800,10 @@ static int dev_cg(trpo_dev *d, size_t maxiter, double resth, bool in_sequence) {
     int rc = ensure_hist(d, maxiter);
     if (rc) return rc;
     d->cg_last_iters = maxiter;
+    // every solve's kernels write the direction pack (cg_axpy / the fused prologue pack p'), also when
+    // the solve is a replay of the captured graph, whose host-side enqueue_cg_body ran only at capture:
+    // a later FVP of slot V must re-pack V, not read the last CG direction
+    d->vpack_v = 0;
     // Launch form of the solve (round 4): eager stream launches unless an RCCL communicator is attached
     // (or TRPO_CG_GRAPH=1).  A replayed hipGraph runs its 11 kernels back to back, but consecutive graph
     // launches left ~3 us of idle GPU between solves; 11 eager launches cost the host ~40 us, far less
@@ -5845,7 +5852,7 @@ extern "C" int trpo_dev_cg_history(trpo_dev *d, double *rdotr, double *xnorm, si
     // the control block and the whole history in one move (mapped host memory, copy kernels)
     static_assert(sizeof(Ctl) % sizeof(double) == 0, "Ctl moves as 8-byte words");
     const int cw = (int)(sizeof(Ctl) / sizeof(double)), hw = 2 * d->hist_cap;
-    if (ensure_hst(d, (size_t)d->P + 2 * (size_t)(d->hist_cap + 8))) return -2;
+    if (const int hrc = ensure_hst(d, (size_t)d->P + 2 * (size_t)(d->hist_cap + 8))) return hrc;
     hipLaunchKernelGGL(vcopy64_kernel, dim3(1), dim3(64), 0, d->stream, (const double *)(const void *)d->ctl,
                        d->hst_dev, cw);
     hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv(hw, 256)), dim3(256), 0, d->stream, (const double *)d->hist,
