@@ -730,84 +730,15 @@ __global__ void to_elem_kernel(void *dst, const double *src, long len, int f64) 
     else reinterpret_cast<float *>(dst)[e] = (float)src[e];
 }
 
-// ---------------------------------------------------------------------------
-// Diagnostic build only (-DTRPO_STAMPS): s_memrealtime (100 MHz) stamps per block.
-// ---------------------------------------------------------------------------
-#ifdef TRPO_STAMPS
-__device__ unsigned long long g_stamps[1024 * 32];
-#define STAMP(k)                                                                             \
-    do {                                                                                     \
-        if (threadIdx.x == 0 && blockIdx.x < 1024) {                                         \
-            g_stamps[blockIdx.x * 32 + (k)] = __builtin_amdgcn_s_memrealtime();              \
-            g_stamps[blockIdx.x * 32 + 16 + (k)] = __builtin_amdgcn_s_memtime();             \
-        }                                                                                    \
-    } while (0)
-#else
-#define STAMP(k) do { } while (0)
-#endif
-// fvp_coop_kernel's phase profile (diagnostic build only): wave 0 of every block accumulates the
-// s_memtime cycles of each phase of its tile steps in registers (CSTAMP(k, value the phase produced)),
-// and writes them at the end to g_stamps[block][k] (tools/stamps_coop.py)
-#ifdef TRPO_STAMPS
-#define CSTAMP(k, dep)                                          \
-    do {                                                        \
-        asm volatile("" ::"v"(dep));                            \
-        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
-        ph_[k] += t_ - tprev_;                                  \
-        tprev_ = t_;                                            \
-    } while (0)
-#else
-#define CSTAMP(k, dep) do { } while (0)
-#endif
 
 // ---------------------------------------------------------------------------
 // The fused FVP kernel, 3 weight layers (NumLayers == 4), MFMA path.
 // ---------------------------------------------------------------------------
-#ifndef TRPO_TILE_ILV
-#define TRPO_TILE_ILV 0      // 1: tile t -> block t % grid (waves of a block spread over the sample range)
-#endif
-#ifndef TRPO_NAT_ATOMICS
-#define TRPO_NAT_ATOMICS 1  // cross-block fp64 atomics in natural parameter order
-#endif
-#ifndef TRPO_PF_PIN
-#define TRPO_PF_PIN 1       // pin the next-tile observation prefetch to the top of the tile loop
-#endif
 constexpr int SCR_LD = 20;            // scratch row stride (floats): conflict-free b32 writes
-#ifndef TRPO_SCR_LD3
-#define TRPO_SCR_LD3 20
-#endif
-constexpr int SCR_LD3 = TRPO_SCR_LD3;  // fvp_mlp3_kernel's transpose scratch (TRPO_SCR_SWZ=0 layout)
-#ifndef TRPO_SCR_SWZ
-#define TRPO_SCR_SWZ 1                  // swizzled conflict-free transpose layout (scr_off)
-#endif
-#ifndef TRPO_SKIPW
-#define TRPO_SKIPW 1                    // element-less waves skip the CG-state loads (pair layout)
-#endif
-#ifndef TRPO_BUF_PF
-#define TRPO_BUF_PF 1                   // the tile loop's prefetch as buffer loads (scalar tile addressing)
-#endif
-#ifndef TRPO_RGS4_T
-#define TRPO_RGS4_T 1                   // rowgroup_sum4 as a transposed reduction (same bits, half the swaps)
-#endif
-#ifndef TRPO_NO_PF
-#define TRPO_NO_PF 0                    // experiment builds only: no register prefetch of the next tile
-#endif
-#ifndef TRPO_PF_RING
-#define TRPO_PF_RING 1                  // cached-forward kernels: the prefetch into a ring of input slots
-#endif                                  // (loop unrolled by the ring size: no per-trip register copies)
-#ifndef TRPO_PF_DEPTH
-#define TRPO_PF_DEPTH 1                 // trips between a slot's load and its use (ring of DEPTH + 1 slots)
-#endif
-#ifndef TRPO_DIAG_NOCOMPUTE
-#define TRPO_DIAG_NOCOMPUTE 0           // diagnostic builds only: the ring loop streams its inputs, no tile step
-#endif
-#ifndef TRPO_DIAG_NOLOAD
-#define TRPO_DIAG_NOLOAD 0              // diagnostic builds only: every tile reuses the first tile's inputs
-#endif                                  // (1: all of them, 2: the observations only, 3: the cached y only)
-#ifndef TRPO_ISLOT_TABLE
-#define TRPO_ISLOT_TABLE 1              // epilogue slot positions from a table (not islot_at)
-#endif
 
+#ifndef TRPO_YC_NT
+#define TRPO_YC_NT 2
+#endif
 template <int T0, int T1, int T2, int T3>
 struct FastCfg {
     // theta pack (floats)
@@ -833,7 +764,6 @@ struct FastCfg {
     static constexpr int R0 = 16 * (T0 + T1), R1 = 16 * (T1 + T2), R2 = 16 * (T2 + T3);
     static constexpr int ROWS = R0 > R1 ? (R0 > R2 ? R0 : R2) : (R1 > R2 ? R1 : R2);
     static constexpr int SCR = ROWS * 20;             // scr_off: 20 floats per row either way
-    static_assert(TRPO_SCR_SWZ == 0 || SCR_LD3 == 20, "swizzled scratch assumes the 20-float footprint");
     // accumulator registers per lane; the block's partial sums are written in this
     // "accumulator order" (f4 k, lane, r) -- SLAB floats per block, mapped back to
     // natural parameter order by the reduce kernel (imap)
@@ -841,19 +771,15 @@ struct FastCfg {
     static constexpr int SLAB = NACC * 64;
     // small nets: weights live in registers and 16 waves per block keep <= 1 tile per wave
     static constexpr bool REGW = T0 * T1 + T1 * T2 + T2 * T3 <= 3;
-#ifndef TRPO_ARM_WAVES
-#define TRPO_ARM_WAVES 8
-#endif
     // 12 waves (3 per SIMD) for the small nets: ~1 tile per wave at N = 50k, balanced SIMDs
-#ifndef TRPO_BIG_WAVES
-#define TRPO_BIG_WAVES 8
-#endif
-    static constexpr int WAVES = REGW ? TRPO_ARM_WAVES : TRPO_BIG_WAVES;
-    static constexpr int NT = 1;                   // tiles in flight per wave (2 measured no faster)
+    static constexpr int WAVES = 8;
+    // tiles in flight per wave: the cached-forward small-net kernels (MODE 2 / 3) interleave TRPO_YC_NT
+    // tiles' independent MFMA chains (round 6); every other kernel streams one tile per trip
+    static constexpr int NT_YC = REGW ? TRPO_YC_NT : 1;
     static constexpr int THREADS = 64 * WAVES;
     static constexpr int PMAX = 256 * (T0 * T1 + T1 * T2 + T2 * T3) + 16 * (T1 + T2 + 2 * T3);
     // tile scratch; also stages the fp64 direction of the fused CG update
-    static constexpr int SCRATCH = (WAVES * NT * SCR > 2 * PMAX) ? WAVES * NT * SCR : 2 * PMAX;
+    static constexpr int SCRATCH = (WAVES * NT_YC * SCR > 2 * PMAX) ? WAVES * NT_YC * SCR : 2 * PMAX;
     static constexpr int MAIN_BYTES = 4 * (TLEN + VLEN + SCRATCH);
     static constexpr int CAP = MAIN_BYTES > 131072 ? MAIN_BYTES : 131072;
     // waves combined per epilogue round (largest divisor of WAVES whose dumps fit)
@@ -866,7 +792,7 @@ struct FastCfg {
     static constexpr int EMAX = (PMAX + THREADS - 1) / THREADS;
     static constexpr int VEMAX = (VLEN + THREADS - 1) / THREADS;
     static constexpr int EMAX_REPLICAS = 4;        // atomic-replica reduction only for EMAX <= this
-    static_assert(NT == 1 || NT == 2, "NT");
+    static_assert(NT_YC == 1 || NT_YC == 2, "NT");
     static_assert(WAVES % RW == 0, "RW");
     static int lds_bytes() {
         const int b = 4 * RW * SLAB;
@@ -900,7 +826,6 @@ __device__ __forceinline__ float rowgroup_sum(float v) {
 // {0, 2, 1, 3}[g] as (row 0 + row 2) + (row 1 + row 3) -- rowgroup_sum's association, the same bits);
 // three more swaps broadcast the four totals back to every row.  12 instructions instead of ~24.
 __device__ __forceinline__ f4 rowgroup_sum4(f4 v) {
-#if TRPO_RGS4_T
     const auto p01 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[0]), __float_as_uint(v[1]), false, false);
     const auto p23 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[2]), __float_as_uint(v[3]), false, false);
     const float s01 = __uint_as_float(p01[0]) + __uint_as_float(p01[1]);   // rows: v0, v0, v1, v1 (half sums)
@@ -916,12 +841,6 @@ __device__ __forceinline__ f4 rowgroup_sum4(f4 v) {
     r[2] = __uint_as_float(b02[1]);
     r[3] = __uint_as_float(b13[1]);
     return r;
-#else
-    f4 r;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) r[i] = rowgroup_sum(v[i]);
-    return r;
-#endif
 }
 
 // Transpose scratch of fvp_mlp3_kernel: scr_put writes lane (c, g)'s accumulator rows 4g + r of
@@ -934,24 +853,13 @@ __device__ __forceinline__ f4 rowgroup_sum4(f4 v) {
 // round-1 row stride of 20 floats left 3 two-way conflicts per read group (42 % of the kernel's LDS
 // cycles were conflict cycles).  Same footprint: 20 floats per row.
 // the tile loop's streamed inputs (observations, forward cache)
-#ifndef TRPO_NT_STREAM
-#define TRPO_NT_STREAM 0
-#endif
 __device__ __forceinline__ f4 stream_ld(const f4 *p) {
-#if TRPO_NT_STREAM
-    return __builtin_nontemporal_load(p);
-#else
     return *p;
-#endif
 }
 
 __device__ __forceinline__ int scr_off(int row, int chunk) {
-#if TRPO_SCR_SWZ
     const int q = (row >> 2) & 3;
     return row * 16 + (row >> 2) * 16 + ((chunk ^ ((4 - q) & 3)) << 2);
-#else
-    return row * SCR_LD3 + 4 * chunk;
-#endif
 }
 // TRPO_SCR_XT (round 4): the tile is stored as it is held -- ONE ds_write_b128 of the lane's D-layout
 // registers at V index lane + lane / 16 (a 4-float pad after every 16 lanes; 272 of the 320 floats a
@@ -959,19 +867,10 @@ __device__ __forceinline__ int scr_off(int row, int chunk) {
 // floats 4 (4g + 17 (c / 4)) + c % 4 + 4s of the slot (two ds_read2_b32; banks 16g + 4 (c / 4) +
 // c % 4 + 4s mod 64, distinct over the 64 lanes).  hipcc issues the reads as four ds_read_b32 here (not
 // ds_read2_b32: the constant part of the slot address exceeds its 8-bit offsets), so the count stays 5.
-#ifndef TRPO_SCR_XT
-#define TRPO_SCR_XT 1
-#endif
 __device__ __forceinline__ void scr_put(float *scr, int row0, f4 t, int c, int g) {
-#if TRPO_SCR_XT
     reinterpret_cast<f4 *>(scr)[(row0 >> 4) * 68 + c + 17 * g] = t;
-#else
-#pragma unroll
-    for (int r = 0; r < 4; ++r) scr[scr_off(row0 + 4 * g + r, c >> 2) + (c & 3)] = t[r];
-#endif
 }
 __device__ __forceinline__ f4 scr_get(const float *scr, int row0, int c, int g) {
-#if TRPO_SCR_XT
     const float *p = scr + (row0 >> 4) * 272 + 4 * (4 * g + 17 * (c >> 2)) + (c & 3);
     f4 r;
     r[0] = p[0];
@@ -979,9 +878,6 @@ __device__ __forceinline__ f4 scr_get(const float *scr, int row0, int c, int g) 
     r[2] = p[8];
     r[3] = p[12];
     return r;
-#else
-    return *reinterpret_cast<const f4 *>(scr + scr_off(row0 + c, g));
-#endif
 }
 
 // ACT >= 0: activations of layers 1..3 fixed at compile time (a1 | a2 << 2 | a3 << 4);
@@ -1022,40 +918,27 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
     constexpr bool YC = MODE == 2 || MODE == 3;     // forward activations from the cache
     constexpr int NYC = T1 + T2 + T3;               // cached f4 per lane per tile
     using C = FastCfg<T0, T1, T2, T3>;
-    static_assert(!YC || C::NT == 1, "forward cache with one tile in flight");
+    constexpr int NT = YC ? C::NT_YC : 1;           // tiles per trip
     // the cache only for the register-resident small nets: on the wide shapes its extra registers
     // push the kernel into scratch spills (and those runs were not bitwise reproducible)
-#ifndef TRPO_YC_ALL
-#define TRPO_YC_ALL 0   // diagnostic build: the forward cache for every tile shape
-#endif
-    static_assert(!YC || C::REGW || TRPO_YC_ALL, "forward cache only for the small-net kernels");
+    static_assert(!YC || C::REGW, "forward cache only for the small-net kernels");
     extern __shared__ __attribute__((aligned(16))) float lds[];
     __shared__ double sh64[(5 + QB) * 4 * C::WAVES];      // 5 + QB DPP block sums, 4 rows per wave
     // streaming basis dots of a MODE 0 update: the tile scratch, unused until the tile loop's barrier
     double *shq = reinterpret_cast<double *>(lds + C::TLEN + C::VLEN);
     float *qf = reinterpret_cast<float *>(A.q);                     // fp32 reorthogonalisation basis
     const float *qfz = reinterpret_cast<const float *>(A.qz);
-#ifndef TRPO_KPRE
-#define TRPO_KPRE 1
-#endif
-#if TRPO_KPRE
     const int kPs = k_meta & 0xFFFFF, kR = (k_meta >> 20) & 63, knq = (k_meta >> 26) & 63;
     const float *kq = reinterpret_cast<const float *>(k_q);
-#else
-    const int kPs = A.Ps, kR = A.R_in, knq = A.nq;
-    const float *kq = qf;
-    k_acc = A.acc_in, k_p = A.p_in, k_r = A.r_in, k_x = A.x, k_pslot = A.pslot;
-#endif
     static_assert(C::SCRATCH >= 2 * QCAP * 4 * C::WAVES, "basis-dot scratch");
     float *tw = lds;                                   // theta pack
     float *vw = lds + C::TLEN;                         // v pack (fragment order, fp32)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int c = lane & 15, g = lane >> 4;
-    float *scr = lds + C::TLEN + C::VLEN + wave * C::NT * C::SCR;
+    float *scr = lds + C::TLEN + C::VLEN + wave * C::NT_YC * C::SCR;
     const int nwaves = gridDim.x * C::WAVES;
     const int ntiles = A.ntiles, n = A.n;
     const f4 *obs4 = reinterpret_cast<const f4 *>(A.obs4);
-    STAMP(0);
 
     // ---- prologue: ONE round of global loads (flags, theta pack, [v pack | CG state], first tile) ----
     // MODE 3 is always a CG update (compile time: no run-time mode branches around its loads)
@@ -1072,20 +955,14 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
     f4 st[PER];
     // the wave's tile index is wave-uniform: kept in an SGPR (readfirstlane), the tile loop's
     // bookkeeping, bound test and input addresses are scalar work, not VALU
-#if TRPO_TILE_ILV
-    int tile = __builtin_amdgcn_readfirstlane(wave * gridDim.x + blockIdx.x);
-#else
     int tile = __builtin_amdgcn_readfirstlane(blockIdx.x * C::WAVES + wave);
-#endif
-    // input slots of the tile loop: slot 0 is the first trip's; the cached-forward kernels stream the
-    // later trips through a ring of PFU slots (TRPO_PF_RING), the others through one slot and a copy
-    constexpr bool RING = YC && TRPO_PF_RING && !TRPO_NO_PF && !TRPO_DIAG_NOLOAD && TRPO_BUF_PF;
-    constexpr int PFD = RING ? TRPO_PF_DEPTH : 1, PFU = RING ? PFD + 1 : 1;
-    static_assert(PFD >= 1 && PFD <= 2, "prefetch depth");
-    f4 xb[PFU][1][T0];
-    [[maybe_unused]] f4 yb[PFU][YC ? NYC : 1];
+    // input slots of the tile loop (NT tiles each): slot 0 is the first trip's; the cached-forward kernels
+    // stream the later trips through a ring of two slots, the others through one slot and a copy
+    constexpr bool RING = YC;
+    constexpr int PFU = RING ? 2 : 1;
+    f4 xb[PFU][NT][T0];
+    [[maybe_unused]] f4 yb[PFU][NT][YC ? NYC : 1];
     f4(&xn)[T0] = xb[0][0];
-    [[maybe_unused]] f4(&yn)[YC ? NYC : 1] = yb[0];
     const f4 *yc4 = reinterpret_cast<const f4 *>(A.yc);
     const int a3c = ACT >= 0 ? ((ACT >> 4) & 3) : net.act[3];
     // the loads that do not depend on the previous kernel: theta [+ v] pack and the first tile.
@@ -1099,26 +976,18 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
             const int e = min(tid + k * C::THREADS, NALL - 1);
             st[k] = e < NT4 ? tp4[e] : vp4[e - NT4];
         }
-        const int tl = max(0, min(tile, ntiles - 1));
 #pragma unroll
-        for (int kt = 0; kt < T0; ++kt) xn[kt] = obs4[(long)(tl * 16 + c) * (4 * T0) + kt * 4 + g];
-        if constexpr (YC) {
+        for (int t = 0; t < NT; ++t) {
+            const int tl = max(0, min(tile + t * nwaves, ntiles - 1));
 #pragma unroll
-            for (int k = 0; k < T1 + T2; ++k) yn[k] = yc4[((long)tl * NYC + k) * 64 + lane];
-            if (act_needs_y(a3c))
+            for (int kt = 0; kt < T0; ++kt) xb[0][t][kt] = obs4[(long)(tl * 16 + c) * (4 * T0) + kt * 4 + g];
+            if constexpr (YC) {
 #pragma unroll
-                for (int k = T1 + T2; k < NYC; ++k) yn[k] = yc4[((long)tl * NYC + k) * 64 + lane];
-        }
-        if constexpr (PFU > 2) {
-            // a two-trip-deep ring: the second trip's inputs in the same load round
-            const int t2 = max(0, min(tile + nwaves, ntiles - 1));
+                for (int k = 0; k < T1 + T2; ++k) yb[0][t][k] = yc4[((long)tl * NYC + k) * 64 + lane];
+                if (act_needs_y(a3c))
 #pragma unroll
-            for (int kt = 0; kt < T0; ++kt) xb[1][0][kt] = obs4[(long)(t2 * 16 + c) * (4 * T0) + kt * 4 + g];
-#pragma unroll
-            for (int k = 0; k < T1 + T2; ++k) yb[1][k] = yc4[((long)t2 * NYC + k) * 64 + lane];
-            if (act_needs_y(a3c))
-#pragma unroll
-                for (int k = T1 + T2; k < NYC; ++k) yb[1][k] = yc4[((long)t2 * NYC + k) * 64 + lane];
+                    for (int k = T1 + T2; k < NYC; ++k) yb[0][t][k] = yc4[((long)tl * NYC + k) * 64 + lane];
+            }
         }
     };
     if constexpr (!CGK) load_static();
@@ -1145,8 +1014,8 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
             // (the preloaded scalar arguments: no wait for the kernarg segment before these loads)
             const double *xk = blockIdx.x == 0 ? k_x : k_p;
             // waves whose first pair lies beyond Ps hold no CG element (armDOF_0: waves 5-7): they skip
-            // the state loads in a wave-uniform scalar branch and keep zeros (TRPO_SKIPW)
-            const bool holds = !TRPO_SKIPW || 128 * __builtin_amdgcn_readfirstlane(wave) < kPs;
+            // the state loads in a wave-uniform scalar branch and keep zeros
+            const bool holds = 128 * __builtin_amdgcn_readfirstlane(wave) < kPs;
             double2 p2 = {0.0, 0.0}, r2 = {0.0, 0.0}, x2 = {0.0, 0.0};
             double2 za[RMAX];
 #pragma unroll
@@ -1188,10 +1057,8 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
 #pragma unroll
                 for (int k = 0; k < RMAX; ++k) za[k] = A.acc_in[(long)min(k, A.R_in - 1) * A.Ps + qz];
                 z = za[0];                                // R_in >= 1: no select on the first term
-#ifndef TRPO_ABL_R1
 #pragma unroll
                 for (int k = 1; k < RMAX; ++k) z += k < A.R_in ? za[k] : 0.0;
-#endif
             } else {
                 z = A.acc_in[qz];                         // slab mode: one reduced vector
             }
@@ -1232,7 +1099,7 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
                 // QB > 0 implies nq >= 1 (qb_index): the clamped row is a stored basis vector, selected
                 // away for the slots >= nq (no zero-line pointer needed); skipped by element-less waves
                 float2 v = make_float2(0.0f, 0.0f);
-                if (!TRPO_SKIPW || 128 * __builtin_amdgcn_readfirstlane(wave) < kPs) v = pair_at(kq, min(i, knq - 1), kPs);
+                if (128 * __builtin_amdgcn_readfirstlane(wave) < kPs) v = pair_at(kq, min(i, knq - 1), kPs);
                 const bool ok = i < knq;
                 qv[i][0] = (ok && 2 * tid < A.P) ? (double)v.x : 0.0;
                 qv[i][1] = (ok && 2 * tid + 1 < A.P) ? (double)v.y : 0.0;
@@ -1269,7 +1136,6 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
             if (ve < C::VLEN) vw[ve] = vg[e];
         }
     }
-    STAMP(7);
     if (ini) {
         #pragma clang fp contract(off)   // explicit rounding: MODE 0 and MODE 3 give the same bits
 #pragma unroll
@@ -1338,11 +1204,7 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
         if constexpr (QB == 0) {
             if (A.reorth && A.nq > 0) qdots_stage1<C::EMAX, float, PAIR>(qf, qfz, A.P, A.Ps, A.nq, zv, C::THREADS, shq);
         }
-        STAMP(8);
-#ifndef TRPO_ABL_NORED
         block_sums_dpp<5 + QB, C::WAVES>(red, sh64);
-#endif
-        STAMP(9);
         const double alpha = sin.rdotr / red[0];
         // coefficient along the current residual r (unit vector r / |r|): |r| - alpha (r . z) / |r|
         double cs = 0.0, cr = 0.0;
@@ -1371,7 +1233,6 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
         }
         const double nr = sin.rdotr - 2.0 * alpha * red[1] + alpha * alpha * red[2] - cs;
         const double xn2 = sin.xx + 2.0 * alpha * red[3] + alpha * alpha * red[4];
-        STAMP(10);
         const double beta = nr / sin.rdotr;
 #pragma unroll
         for (int e = 0; e < C::EMAX; ++e) {
@@ -1399,7 +1260,6 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
             if (it <= CG_AMAX) A.ctl->alpha[it - 1] = alpha;
         }
         if (done) return;                              // block-uniform (identical in every block)
-        STAMP(11);
         // p' straight into the fragment LDS: natural element q -> its pack slot (an LDS scatter),
         // the padding slots zeroed by their owners -- disjoint writes, so no staging barrier
 #pragma unroll
@@ -1410,30 +1270,26 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
             const int ve = tid + e * C::THREADS;
             if (ve < C::VLEN && vm[e] < 0) vw[ve] = 0.0f;
         }
-        STAMP(12);
     }
     if constexpr (CGK) stage_static();
     __syncthreads();
-    STAMP(1);
-#if TRPO_NAT_ATOMICS
     // the epilogue's natural -> accumulator positions (a table built at context creation: islot_at's
     // integer divisions cost ~0.3 us per launch on the epilogue's critical path); loaded now, used
     // after the tile loop, so the load's latency hides behind the tiles
     [[maybe_unused]] int jslot[C::EMAX];
-    if constexpr (C::RW == C::WAVES && TRPO_ISLOT_TABLE) {
+    if constexpr (C::RW == C::WAVES) {
         if (A.islot) {
 #pragma unroll
             for (int e = 0; e < C::EMAX; ++e) jslot[e] = A.islot[min(tid + e * C::THREADS, A.nw - 1)];
         }
     }
-#endif
     [[maybe_unused]] bool first_tile = true;
 
     const int a1 = ACT >= 0 ? (ACT & 3) : net.act[1];
     const int a2 = ACT >= 0 ? ((ACT >> 2) & 3) : net.act[2];
     const int a3 = ACT >= 0 ? ((ACT >> 4) & 3) : net.act[3];
     const bool y3_needed = act_needs_y(a3);
-    f4 *ycs = (MODE == 0 && (C::REGW || TRPO_YC_ALL)) ? reinterpret_cast<f4 *>(A.yc) : nullptr;   // cache writer
+    f4 *ycs = (MODE == 0 && C::REGW) ? reinterpret_cast<f4 *>(A.yc) : nullptr;   // cache writer
     const f4 *TW = reinterpret_cast<const f4 *>(tw);
     const f4 *VW = reinterpret_cast<const f4 *>(vw);
 
@@ -1453,7 +1309,7 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
     }
 #define WLD(REG, EXPR) (C::REGW ? (REG) : (EXPR))
     constexpr int NOUT = NO & 7;                            // outputs of the narrow layer (0: off)
-    static_assert(NO == 0 || (T3 == 1 && NOUT >= 1 && NOUT <= 4 && C::NT == 1), "narrow output layer");
+    static_assert(NO == 0 || (T3 == 1 && NOUT >= 1 && NOUT <= 4), "narrow output layer");
     constexpr int NOA = NOUT ? NOUT : 1;
     constexpr bool NOV = NOUT && !(NO & NO_MFMA_RGW2);      // RGW2 / B3 on the VALU
     [[maybe_unused]] f4 nFA2[T2], nVFA2[T2], w2n[T2][4];    // NO: 4x4 A operands, W2[16kt + 4g + r][0..3]
@@ -1499,11 +1355,12 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
 #pragma unroll
     for (int a = 0; a < T3; ++a) sB3[a] = zero4;
 
-    // NT independent tiles per loop trip (ILP: the scheduler interleaves their MFMA chains)
-    constexpr int NT = C::NT;
+    // NT independent tiles per loop trip, their chains interleaved instruction by instruction (the t loops
+    // innermost).  Every accumulator still receives the tiles in the order one tile per trip gives (tile
+    // t of a trip before tile t + 1, each tile's products in the same order), so the sums are bit-identical.
     [[maybe_unused]] const int pf_xoff = (c * (4 * T0) + g) * 16, pf_yoff = lane * 16;   // prefetch lane offsets (bytes)
     // one tile (NT tiles) of work: inputs x0, the cached activations ycur, live columns
-    auto tile_step = [&](const int tile, const f4 (&x0)[NT][T0], const f4 (&ycur)[YC ? NYC : 1],
+    auto tile_step = [&](const int tile, const f4 (&x0)[NT][T0], const f4 (&ycur)[NT][YC ? NYC : 1],
                          const bool (&live)[NT]) __attribute__((always_inline)) {
         // ---- layer 0: x1 = W0^T x0 + b0 ; Rx1 = VW0^T x0 + vb0 (Ry0 = 0) ----
         f4 y1[NT][T1], r1[NT][T1];
@@ -1529,20 +1386,17 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
                     }
             }
             if constexpr (YC) {
-                y1[0][ot] = ycur[ot];
-                r1[0][ot] = act_r4(a1, y1[0][ot], ra[0]);
+#pragma unroll
+                for (int t = 0; t < NT; ++t) {
+                    y1[t][ot] = ycur[t][ot];
+                    r1[t][ot] = act_r4(a1, y1[t][ot], ra[t]);
+                }
             } else {
 #pragma unroll
                 for (int t = 0; t < NT; ++t) y1[t][ot] = act_fwd(a1, a[t], ra[t], r1[t][ot]);
                 if (ycs) ycs[((long)tile * NYC + ot) * 64 + lane] = y1[0][ot];
             }
         }
-#ifdef TRPO_STAMPS
-        if (first_tile) {
-            asm volatile("" ::"v"(y1[0][0]));
-            STAMP(13);
-        }
-#endif
         // ---- layer 1 ----
         f4 y2[NT][T2], r2[NT][T2];
 #pragma unroll
@@ -1571,56 +1425,64 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
                     }
             }
             if constexpr (YC) {
-                y2[0][ot] = ycur[T1 + ot];
-                r2[0][ot] = act_r4(a2, y2[0][ot], ra[0] + rb[0]);
+#pragma unroll
+                for (int t = 0; t < NT; ++t) {
+                    y2[t][ot] = ycur[t][T1 + ot];
+                    r2[t][ot] = act_r4(a2, y2[t][ot], ra[t] + rb[t]);
+                }
             } else {
 #pragma unroll
                 for (int t = 0; t < NT; ++t) y2[t][ot] = act_fwd(a2, a[t], ra[t] + rb[t], r2[t][ot]);
                 if (ycs) ycs[((long)tile * NYC + T1 + ot) * 64 + lane] = y2[0][ot];
             }
         }
-#ifdef TRPO_STAMPS
-        if (first_tile) {
-            asm volatile("" ::"v"(y2[0][0]));
-            STAMP(14);
-        }
-#endif
         // ---- layer 2 (output) and G3 = act3'(Ry3 / sigma^2) ----
         f4 g3[NT][T3];
         if constexpr (NO) {
             // narrow: outputs 0..3 of sample c in registers 0..3 of every lane (see the kernel comment)
-            f4 a = nb2, ra = nvb2, rb = zero4;
+            f4 a[NT], ra[NT], rb[NT];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                a[t] = nb2;
+                ra[t] = nvb2;
+                rb[t] = zero4;
+            }
 #pragma unroll
             for (int kt = 0; kt < T2; ++kt)
 #pragma unroll
-                for (int s = 0; s < 4; ++s) {
-                    if (!YC && y3_needed) a = MFMA4(nFA2[kt][s], y2[0][kt][s], a);
-                    if constexpr (FV) {
-                        ra = MFMA4(nFA2[kt][s], r2[0][kt][s], ra);
-                        rb = MFMA4(nVFA2[kt][s], y2[0][kt][s], rb);
-                    }
-                }
-            const f4 rx = FV ? rowgroup_sum4(ra + rb) : zero4;
-            f4 r3, gg, y3;
-            if constexpr (YC) {
-                y3 = y3_needed ? ycur[T1 + T2] : zero4;
-                r3 = act_r4(a3, y3, rx);
-            } else {
-                y3 = act_fwd(a3, y3_needed ? rowgroup_sum4(a) : zero4, rx, r3);
-                if (ycs && y3_needed) ycs[((long)tile * NYC + T1 + T2) * 64 + lane] = y3;
-            }
-            if constexpr (FV) {
-                gg = act_bwd(a3, y3, r3 * niv);
-            } else {
-                const int tt = min(tile, ntiles - 1);
-                const f4 dm = reinterpret_cast<const f4 *>(A.pg_d4)[(long)(tt * 16 + c) * 4];
-                const float adv = A.pg_adv[tt * 16 + c];
-                gg = act_bwd(a3, y3, (adv * dm) * reinterpret_cast<const f4 *>(A.pg_iv4)[0]);
-            }
-            g3[0][0] = live[0] ? gg : zero4;
-            if constexpr (NOV) {
+                for (int s = 0; s < 4; ++s)
 #pragma unroll
-                for (int o = 0; o < NOA; ++o) sb3n[o] += g3[0][0][o];
+                    for (int t = 0; t < NT; ++t) {
+                        if (!YC && y3_needed) a[t] = MFMA4(nFA2[kt][s], y2[t][kt][s], a[t]);
+                        if constexpr (FV) {
+                            ra[t] = MFMA4(nFA2[kt][s], r2[t][kt][s], ra[t]);
+                            rb[t] = MFMA4(nVFA2[kt][s], y2[t][kt][s], rb[t]);
+                        }
+                    }
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const f4 rx = FV ? rowgroup_sum4(ra[t] + rb[t]) : zero4;
+                f4 r3, gg, y3;
+                if constexpr (YC) {
+                    y3 = y3_needed ? ycur[t][T1 + T2] : zero4;
+                    r3 = act_r4(a3, y3, rx);
+                } else {
+                    y3 = act_fwd(a3, y3_needed ? rowgroup_sum4(a[t]) : zero4, rx, r3);
+                    if (ycs && y3_needed) ycs[((long)tile * NYC + T1 + T2) * 64 + lane] = y3;
+                }
+                if constexpr (FV) {
+                    gg = act_bwd(a3, y3, r3 * niv);
+                } else {
+                    const int tt = min(tile + t * nwaves, ntiles - 1);
+                    const f4 dm = reinterpret_cast<const f4 *>(A.pg_d4)[(long)(tt * 16 + c) * 4];
+                    const float adv = A.pg_adv[tt * 16 + c];
+                    gg = act_bwd(a3, y3, (adv * dm) * reinterpret_cast<const f4 *>(A.pg_iv4)[0]);
+                }
+                g3[t][0] = live[t] ? gg : zero4;
+                if constexpr (NOV) {
+#pragma unroll
+                    for (int o = 0; o < NOA; ++o) sb3n[o] += g3[t][0][o];
+                }
             }
         } else
 #pragma unroll
@@ -1653,7 +1515,7 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
             for (int t = 0; t < NT; ++t) {
                 f4 r3, gg, y3;
                 if constexpr (YC) {
-                    y3 = y3_needed ? ycur[T1 + T2 + ot] : zero4;
+                    y3 = y3_needed ? ycur[t][T1 + T2 + ot] : zero4;
                     r3 = act_r4(a3, y3, ra[t] + rb[t]);
                 } else {
                     y3 = act_fwd(a3, a[t], ra[t] + rb[t], r3);
@@ -1672,26 +1534,26 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
                 sB3[ot] += g3[t][ot];
             }
         }
-#ifdef TRPO_STAMPS
-        if (first_tile) {
-            asm volatile("" ::"v"(g3[0][0]));
-            STAMP(2);
-        }
-#endif
         // ---- contraction RGW2 += Y2 . G3^T (K = 16 samples per tile) ----
         [[maybe_unused]] f4 g3m[NT][T3];                  // G3 in the 16x16x4 layout (rows 4g + r)
         if constexpr (NO && !NOV) {
-            g3m[0][0] = g == 0 ? g3[0][0] : zero4;
-            sB3[0] += g3m[0][0];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                g3m[t][0] = g == 0 ? g3[t][0] : zero4;
+                sB3[0] += g3m[t][0];
+            }
         }
         if constexpr (NOV) {
             // per lane: hidden 16kt + 4g + r x output o of the lane's own sample column
 #pragma unroll
-            for (int kt = 0; kt < T2; ++kt)
+            for (int t = 0; t < NT; ++t)
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
+                for (int kt = 0; kt < T2; ++kt)
 #pragma unroll
-                    for (int o = 0; o < NOA; ++o) acc2[kt][r][o] = fmaf(y2[0][kt][r], g3[0][0][o], acc2[kt][r][o]);
+                    for (int r = 0; r < 4; ++r)
+#pragma unroll
+                        for (int o = 0; o < NOA; ++o)
+                            acc2[kt][r][o] = fmaf(y2[t][kt][r], g3[t][0][o], acc2[kt][r][o]);
         } else {
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
@@ -1727,9 +1589,11 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
             if constexpr (NO) {
                 // the fmaf chain over the outputs a 16x16x4 MFMA forms (its padded rows add zeros)
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
+                for (int t = 0; t < NT; ++t)
 #pragma unroll
-                    for (int o = 0; o < NOA; ++o) a[0][r] = fmaf(w2n[it][r][o], g3[0][0][o], a[0][r]);
+                    for (int r = 0; r < 4; ++r)
+#pragma unroll
+                        for (int o = 0; o < NOA; ++o) a[t][r] = fmaf(w2n[it][r][o], g3[t][0][o], a[t][r]);
             } else
 #pragma unroll
             for (int kt = 0; kt < T3; ++kt) {
@@ -1745,12 +1609,6 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
                 sB2[it] += g2[t][it];
             }
         }
-#ifdef TRPO_STAMPS
-        if (first_tile) {
-            asm volatile("" ::"v"(g2[0][0]));
-            STAMP(15);
-        }
-#endif
         // ---- contraction RGW1 += Y1 . G2^T ----
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
@@ -1820,150 +1678,75 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
                     for (int s = 0; s < 4; ++s) accW0[at][bt] = MFMA(ya[s], gb[bt][s], accW0[at][bt]);
             }
         }
-#ifdef TRPO_STAMPS
-        if (first_tile) {
-            asm volatile("" ::"v"(accW0[0][0]));
-            STAMP(3);
-        }
-        first_tile = false;
-#endif
     };
-#ifndef TRPO_SETPRIO
-#define TRPO_SETPRIO 0          // 1: the second-dispatched half of the block's waves at s_setprio 1 (guide item 4)
-#endif
-    if (TRPO_SETPRIO && wave >= C::WAVES / 2) __builtin_amdgcn_s_setprio(1);
     if constexpr (RING) {
         // the loop unrolled by the ring size, so every slot index is a compile-time constant: trip j of a
-        // round issues the loads of trip j + PFD into slot (j + PFD) % PFU at its top (buffer loads off
-        // per-trip descriptors, clamped to the last tile) and computes on slot j -- the tile step reads
-        // the slot registers the loads landed in, with no copy (round 5: 6 v_mov_b64 per tile less)
+        // round issues the loads of trip j + 1 into slot (j + 1) % 2 at its top (buffer loads off per-trip
+        // descriptors, clamped to the last tile) and computes on slot j -- the tile step reads the slot
+        // registers the loads landed in, with no copy (round 5: 6 v_mov_b64 per tile less).  A trip is NT
+        // tiles: tile + t * nwaves, t < NT (the tile -> wave assignment of one tile per trip).
         while (tile < ntiles) {
 #pragma unroll
             for (int j = 0; j < PFU; ++j) {
                 if (tile >= ntiles) break;
-                const int tn = min(tile + PFD * nwaves, ntiles - 1);
-                const int sl = (j + PFD) % PFU;
-                const auto rx = __builtin_amdgcn_make_buffer_rsrc((void *)(obs4 + (long)tn * (16 * 4 * T0)), 0,
-                                                                  16 * 64 * T0, 0x00020000);
+                const int sl = (j + 1) % PFU;
 #pragma unroll
-                for (int kt = 0; kt < T0; ++kt)
-                    xb[sl][0][kt] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rx, pf_xoff + kt * 64, 0, 0));
-                const auto ry = __builtin_amdgcn_make_buffer_rsrc((void *)(yc4 + (long)tn * (NYC * 64)), 0, NYC * 1024,
-                                                                  0x00020000);
+                for (int t = 0; t < NT; ++t) {
+                    const int tn = min(tile + (NT + t) * nwaves, ntiles - 1);
+                    const auto rx = __builtin_amdgcn_make_buffer_rsrc((void *)(obs4 + (long)tn * (16 * 4 * T0)), 0,
+                                                                      16 * 64 * T0, 0x00020000);
 #pragma unroll
-                for (int k = 0; k < T1 + T2; ++k)
-                    yb[sl][k] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ry, pf_yoff + k * 1024, 0, 0));
-                if (y3_needed)
+                    for (int kt = 0; kt < T0; ++kt)
+                        xb[sl][t][kt] =
+                            __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rx, pf_xoff + kt * 64, 0, 0));
+                    const auto ry = __builtin_amdgcn_make_buffer_rsrc((void *)(yc4 + (long)tn * (NYC * 64)), 0,
+                                                                      NYC * 1024, 0x00020000);
 #pragma unroll
-                    for (int k = T1 + T2; k < NYC; ++k)
-                        yb[sl][k] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ry, pf_yoff + k * 1024, 0, 0));
-#if TRPO_PF_PIN
+                    for (int k = 0; k < T1 + T2; ++k)
+                        yb[sl][t][k] =
+                            __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ry, pf_yoff + k * 1024, 0, 0));
+                    if (y3_needed)
+#pragma unroll
+                        for (int k = T1 + T2; k < NYC; ++k)
+                            yb[sl][t][k] = __builtin_bit_cast(
+                                f4, __builtin_amdgcn_raw_buffer_load_b128(ry, pf_yoff + k * 1024, 0, 0));
+                }
+                // keep the prefetch at the top of the trip: left to itself hipcc sinks the loads toward
+                // their use (4M: 171.0 -> 186.7 us without this, profiles/r05_pf_pin_ab.log)
                 __builtin_amdgcn_sched_barrier(0);
-#endif
-                const bool live[1] = {tile * 16 + c < n};
-#if TRPO_DIAG_NOCOMPUTE
-                // diagnostic builds only: the input stream alone (the slots consumed by one add each)
-                sB1[0] += xb[j][0][0] + yb[j][0] + yb[j][T1 + T2 - 1];
-                (void)live;
-#else
+                bool live[NT];
+#pragma unroll
+                for (int t = 0; t < NT; ++t) live[t] = (tile + t * nwaves) * 16 + c < n;
                 tile_step(tile, xb[j], yb[j], live);
-#endif
-                tile += nwaves;
+                tile += NT * nwaves;
             }
         }
-    } else
-    for (; tile < ntiles; tile += NT * nwaves) {
-        // input tiles: lane holds features 16kt+4g..+3 of its sample (D-layout rows)
-        f4 x0[NT][T0];
-        [[maybe_unused]] f4 ycur[YC ? NYC : 1];
-#if TRPO_NO_PF
-        // experiment (round 5): no register prefetch -- the trip's own inputs loaded at its top (12 VGPRs
-        // fewer, for more waves per SIMD to hide the latency instead)
-        {
-            const int tc = min(tile, ntiles - 1);
-            const auto rx = __builtin_amdgcn_make_buffer_rsrc((void *)(obs4 + (long)tc * (16 * 4 * T0)), 0,
-                                                              16 * 64 * T0, 0x00020000);
+    } else {
+        static_assert(NT == 1, "one tile per trip outside the cached-forward ring");
+        for (; tile < ntiles; tile += nwaves) {
+            // input tile: lane holds features 16kt+4g..+3 of its sample (D-layout rows)
+            f4 x0[1][T0];
+            const f4 ycur[1][1] = {{zero4}};
+            const bool live[1] = {tile * 16 + c < n};
 #pragma unroll
-            for (int kt = 0; kt < T0; ++kt)
-                xn[kt] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rx, pf_xoff + kt * 64, 0, 0));
-            if constexpr (YC) {
-                const auto ry = __builtin_amdgcn_make_buffer_rsrc((void *)(yc4 + (long)tc * (NYC * 64)), 0, NYC * 1024,
-                                                                  0x00020000);
-#pragma unroll
-                for (int k = 0; k < T1 + T2; ++k)
-                    yn[k] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ry, pf_yoff + k * 1024, 0, 0));
-                if (y3_needed)
-#pragma unroll
-                    for (int k = T1 + T2; k < NYC; ++k)
-                        yn[k] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ry, pf_yoff + k * 1024, 0, 0));
-            }
-        }
-#endif
-        if constexpr (YC) {
-#pragma unroll
-            for (int k = 0; k < NYC; ++k) ycur[k] = yn[k];
-        }
-        bool live[NT];
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const int tt = tile + t * nwaves;
-            live[t] = tt * 16 + c < n;
-            if (t == 0) {
-#pragma unroll
-                for (int kt = 0; kt < T0; ++kt) x0[0][kt] = xn[kt];
-            } else {
-                const int tc = min(tt, ntiles - 1);
-#pragma unroll
-                for (int kt = 0; kt < T0; ++kt) x0[t][kt] = obs4[(long)(tc * 16 + c) * (4 * T0) + kt * 4 + g];
-            }
-        }
-        if constexpr (TRPO_DIAG_NOLOAD != 1 && !TRPO_NO_PF) {   // unconditional (clamped) prefetch of the next trip's first tile
-            const int tn = min(tile + NT * nwaves, ntiles - 1);
-#if TRPO_BUF_PF
-            // buffer loads off per-trip descriptors of the tile's records: the wave-uniform part of the
-            // address is SALU work, the lane offsets loop-invariant (no per-trip VALU address arithmetic)
-            if constexpr (TRPO_DIAG_NOLOAD != 2) {
+            for (int kt = 0; kt < T0; ++kt) x0[0][kt] = xn[kt];
+            {   // unconditional (clamped) prefetch of the next trip's tile: buffer loads off a per-trip
+                // descriptor of the tile's records (the wave-uniform part of the address is SALU work, the
+                // lane offsets loop-invariant)
+                const int tn = min(tile + nwaves, ntiles - 1);
                 const auto rx = __builtin_amdgcn_make_buffer_rsrc((void *)(obs4 + (long)tn * (16 * 4 * T0)), 0,
                                                                   16 * 64 * T0, 0x00020000);
 #pragma unroll
                 for (int kt = 0; kt < T0; ++kt)
                     xn[kt] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rx, pf_xoff + kt * 64, 0, 0));
+                // the prefetch stays at the top of the trip (left to itself the scheduler sinks it to the
+                // loop latch, where the x0 = xn copy then waits out a full memory round trip)
+                __builtin_amdgcn_sched_barrier(0);
             }
-            if constexpr (YC && TRPO_DIAG_NOLOAD != 3) {
-                const auto ry = __builtin_amdgcn_make_buffer_rsrc((void *)(yc4 + (long)tn * (NYC * 64)), 0, NYC * 1024,
-                                                                  0x00020000);
-#pragma unroll
-                for (int k = 0; k < T1 + T2; ++k)
-                    yn[k] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ry, pf_yoff + k * 1024, 0, 0));
-                if (y3_needed)
-#pragma unroll
-                    for (int k = T1 + T2; k < NYC; ++k)
-                        yn[k] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ry, pf_yoff + k * 1024, 0, 0));
-            }
-#else
-            if constexpr (TRPO_DIAG_NOLOAD != 2) {
-#pragma unroll
-                for (int kt = 0; kt < T0; ++kt) xn[kt] = stream_ld(obs4 + (long)(tn * 16 + c) * (4 * T0) + kt * 4 + g);
-            }
-            if constexpr (YC && TRPO_DIAG_NOLOAD != 3) {
-#pragma unroll
-                for (int k = 0; k < T1 + T2; ++k) yn[k] = stream_ld(yc4 + ((long)tn * NYC + k) * 64 + lane);
-                if (y3_needed)
-#pragma unroll
-                    for (int k = T1 + T2; k < NYC; ++k) yn[k] = stream_ld(yc4 + ((long)tn * NYC + k) * 64 + lane);
-            }
-#endif
-#if TRPO_PF_PIN
-            // keep the prefetch at the top of the trip: left to itself the scheduler sinks it to
-            // the loop latch, where the x0 = xn copy then waits out a full memory round trip
-            __builtin_amdgcn_sched_barrier(0);
-#endif
+            tile_step(tile, x0, ycur, live);
         }
-
-        tile_step(tile, x0, ycur, live);
     }
 
-    STAMP(4);
     // ---- epilogue: bias partials summed over the 16 sample columns (DPP), then the
     //      block's 8 wave copies combined in LDS in a fixed order, all threads writing ----
 #pragma unroll
@@ -2023,7 +1806,6 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
         for (int a = 0; a < T3; ++a) acc[k++] = sB3[a];
     }
     f4 *red = reinterpret_cast<f4 *>(lds);
-#if TRPO_NAT_ATOMICS
     if constexpr (C::RW == C::WAVES) {
         if (A.acc_out) {
             // all wave dumps fit at once: each thread sums its natural parameters straight from
@@ -2032,13 +1814,12 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
 #pragma unroll
             for (int k = 0; k < C::NACC / 4; ++k) red[wave * (C::SLAB / 4) + k * 64 + lane] = acc[k];
             __syncthreads();
-            STAMP(5);
             double *dst = A.acc_out + (long)(blockIdx.x % A.R_out) * A.Ps;
 #pragma unroll
             for (int e = 0; e < C::EMAX; ++e) {
                 const int q = tid + e * C::THREADS;
                 if (q < A.nw) {
-                    const int j = (TRPO_ISLOT_TABLE && A.islot) ? jslot[e] : islot_at(net, Tc, q);
+                    const int j = A.islot ? jslot[e] : islot_at(net, Tc, q);
                     float t = 0.0f;
 #pragma unroll
                     for (int w = 0; w < C::WAVES; ++w) t += lds[w * C::SLAB + j];
@@ -2047,11 +1828,9 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
             }
             if (blockIdx.x == 0)
                 for (int e = tid; e < A.zero_len; e += C::THREADS) A.acc_zero[e] = 0.0;
-            STAMP(6);
             return;
         }
     }
-#endif
     f4 part[C::EPT];
 #pragma unroll
     for (int j = 0; j < C::EPT; ++j) part[j] = zero4;
@@ -2072,7 +1851,6 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
             }
         }
     }
-    STAMP(5);
     if (A.acc_out) {
         // cross-block sum by fp64 atomics into R replicas: the fp32 block partials are added
         // exactly unless their exponents span > 29 bits, so the order cannot matter in practice
@@ -2094,7 +1872,6 @@ fvp_mlp3_kernel(const double *__restrict__ k_acc, const double *__restrict__ k_p
             if (e < C::SLAB / 4) slab4[e] = part[j];
         }
     }
-    STAMP(6);
 #undef WLD
 }
 
@@ -2189,7 +1966,7 @@ __device__ __forceinline__ V actv_bwd(int a, V y, V g) {
 }
 template <typename T>
 __device__ __forceinline__ void scr_put_t(T *scr, int row0, typename PT<T>::V t, int c, int g) {
-    if constexpr (sizeof(T) == 4 && TRPO_SCR_XT) {      // fp32: the scr_put form (one 16-byte store)
+    if constexpr (sizeof(T) == 4) {      // fp32: the scr_put form (one 16-byte store)
         reinterpret_cast<typename PT<T>::V *>(scr)[(row0 >> 4) * 68 + c + 17 * g] = t;
     } else {
 #pragma unroll
@@ -2198,7 +1975,7 @@ __device__ __forceinline__ void scr_put_t(T *scr, int row0, typename PT<T>::V t,
 }
 template <typename T>
 __device__ __forceinline__ typename PT<T>::V scr_get_t(const T *scr, int row0, int c, int g) {
-    if constexpr (sizeof(T) == 4 && TRPO_SCR_XT) {      // fp32: the scr_get form (transposed reads)
+    if constexpr (sizeof(T) == 4) {      // fp32: the scr_get form (transposed reads)
         const T *p = scr + (row0 >> 4) * 272 + 4 * (4 * g + 17 * (c >> 2)) + (c & 3);
         typename PT<T>::V r;
         r[0] = p[0];
@@ -2219,20 +1996,14 @@ __device__ __forceinline__ typename PT<T>::V dvec(const T *base, int g) {
     return v;
 }
 
-#ifndef TRPO_COOP_XT
-#define TRPO_COOP_XT 1
-#endif
 template <typename T, int T0, int TH>
 struct CoopCfg {
     static constexpr bool F64 = sizeof(T) == 8;
-#ifndef TRPO_F64_TH1_WAVES
-#define TRPO_F64_TH1_WAVES 4      // one wave per SIMD: room for the forward cache without spills
-#endif
-    static constexpr int WAVES = F64 ? (TH > 1 ? 4 : TRPO_F64_TH1_WAVES) : 8;   // fp64 exchanges: twice the bytes
+    static constexpr int WAVES = F64 ? 4 : 8;   // fp64 TH = 1: one wave per SIMD, room for the forward cache;   // fp64 exchanges: twice the bytes
     static constexpr int GW = TH, NG = WAVES / GW, THREADS = 64 * WAVES;
     // XT (fp32): the y1 and g2 exchange rows padded by one V after every 16 lanes (68 V per 64-lane row),
     // so that RGW1 reads its operands TRANSPOSED straight from them, conflict-free (see the kernel)
-    static constexpr bool XT = !F64 && GW > 1 && TRPO_COOP_XT;
+    static constexpr bool XT = !F64 && GW > 1;
     static constexpr int XR = XT ? 68 : 64;
     static constexpr int NW = T0 + TH + 4;                 // accumulator vectors per lane per wave
     static constexpr int SLAB = TH * NW * 256;             // T per block partial
@@ -2258,12 +2029,9 @@ struct CoopCfg {
 // full or, with the narrow output layer (NO, <= 4 outputs), only its 16 lanes of output columns c < 4; the
 // three bias rows only from the 4 lanes with c == 0 (after the 16-column sums every other lane holds
 // padding) -- 40 % fewer bytes for the FVP epilogue to store and the slab reduce to read (2x64).
-#ifndef TRPO_COOP_COMPACT
-#define TRPO_COOP_COMPACT 1
-#endif
 template <typename T, int T0, int TH, int NO>
 struct CoopSlab {
-    static constexpr bool COMPACT = sizeof(T) == 4 && TRPO_COOP_COMPACT;
+    static constexpr bool COMPACT = sizeof(T) == 4;
     static constexpr int A2 = NO ? 16 : 64;                           // V of the RGW2 tile
     static constexpr int WV = COMPACT ? (T0 + TH) * 64 + A2 + 12 : (T0 + TH + 4) * 64;   // V per wave
     static constexpr int SLAB = ((TH * WV * 4 + 31) / 32) * 32;      // T per block (reduce: multiple of RS_POS)
@@ -2293,7 +2061,7 @@ __device__ __forceinline__ int imap_coop_at(const Net &n, int T0, int TH, int j,
 // the same for the fp32 compact slab layout (CoopSlab): position j -> (wave, vector, lane, r) of the full
 // accumulator order, then imap_coop_at
 __device__ __forceinline__ int imap_coop_slab(const Net &n, int T0, int TH, int no, int j, bool p64) {
-    if (p64 || !TRPO_COOP_COMPACT) return imap_coop_at(n, T0, TH, j, p64);
+    if (p64) return imap_coop_at(n, T0, TH, j, p64);
     const int A2 = no ? 16 : 64, WV = (T0 + TH) * 64 + A2 + 12, NW = T0 + TH + 4;
     const int w = j / (4 * WV), rem = j % (4 * WV);
     if (w >= TH) return -1;                               // the block slab's padding
@@ -2352,9 +2120,6 @@ fvp_coop_kernel(IterArgs A, Net net) {
     // wave runs only its own group's schedule (the rotated one below) with its own barriers
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int c = lane & 15, g = lane >> 4, grp = wave / Q::GW, w = wave % Q::GW;
-#ifdef TRPO_STAMPS
-    const unsigned long long tentry_ = __builtin_amdgcn_s_memtime();
-#endif
     T *scr = ldsT + 4 * Q::MAIN_V + wave * Q::SCR;
     const int ntiles = A.ntiles, n = A.n;
     const V *obs4 = reinterpret_cast<const V *>(A.obs4);
@@ -2592,15 +2357,6 @@ fvp_coop_kernel(IterArgs A, Net net) {
 
     // every wave of the block runs the same number of tile steps (barriers inside)
     const int nsteps = (ntiles + gstride - 1) / gstride;
-#ifndef TRPO_COOP_PRIO
-#define TRPO_COOP_PRIO TRPO_SETPRIO   // the second lane group (waves WAVES/2 ..) at s_setprio 1
-#endif
-    if (TRPO_COOP_PRIO && wave >= Q::WAVES / 2) __builtin_amdgcn_s_setprio(1);
-#ifdef TRPO_STAMPS
-    unsigned long long ph_[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    unsigned long long tprev_ = __builtin_amdgcn_s_memtime();
-    const unsigned long long tloop_ = tprev_;
-#endif
     // One tile step is four segments separated by the group's three LDS exchanges (block barriers):
     //   S0 layer 0 (R chain) -> [y1/r1 rows] -> S1 layer 1, the layer-2 partial over this row tile ->
     //   [layer-2 partials] -> S2 G3, RGW2, G2 -> [g2 rows] -> S3 G1, RGW1, RGW0.
@@ -2611,10 +2367,7 @@ fvp_coop_kernel(IterArgs A, Net net) {
     // NOV (round 5, fp32 narrow output): RGW2 as per-lane VALU partials over the lane's own sample column
     // (hidden 16w + 4g + r x output o), summed over the 16 columns once in the epilogue -- 16 FMAs per tile
     // instead of two LDS transposes and 4 MFMAs whose 16 columns carried <= 4 outputs
-#ifndef TRPO_COOP_NOV
-#define TRPO_COOP_NOV 1
-#endif
-    constexpr bool NOV = NO != 0 && sizeof(T) == 4 && TRPO_COOP_NOV;
+    constexpr bool NOV = NO != 0 && sizeof(T) == 4;
     [[maybe_unused]] float acc2v[4][NO > 0 ? NO : 1];
     if constexpr (NOV) {
 #pragma unroll
@@ -2641,9 +2394,7 @@ fvp_coop_kernel(IterArgs A, Net net) {
                 yn1 = ycl[((long)tn * 2 * TH + w) * 64 + lane];
                 yn2 = ycl[((long)tn * 2 * TH + TH + w) * 64 + lane];
             }
-#if TRPO_PF_PIN
             __builtin_amdgcn_sched_barrier(0);             // keep the prefetch here (see fvp_mlp3_kernel)
-#endif
         }
         // ---- layer 0, row tile w ----
         V a = b0w, ra = vb0w;
@@ -2665,7 +2416,6 @@ fvp_coop_kernel(IterArgs A, Net net) {
             xb[w * 2 * Q::XR + xl] = y1w;
             if constexpr (FV) xb[w * 2 * Q::XR + Q::XR + xl] = r1w;
         }
-        CSTAMP(0, r1w[0]);
     };
     auto seg1 = [&](int step) __attribute__((always_inline)) {
         const int tile = step * gstride + gbase;
@@ -2731,7 +2481,6 @@ fvp_coop_kernel(IterArgs A, Net net) {
             pb[w * 128 + lane] = a3p;
             pb[w * 128 + 64 + lane] = r3p + r3q;
         }
-        CSTAMP(2, r3p[0]);
     };
     auto seg2 = [&](int step) __attribute__((always_inline)) {
         const int tile = step * gstride + gbase;
@@ -2793,7 +2542,6 @@ fvp_coop_kernel(IterArgs A, Net net) {
         g2w = actv_bwd<T>(a2, y2w, t);
         sB2 += g2w;
         if constexpr (Q::GW > 1) gb[w * Q::XR + xl] = g2w;
-        CSTAMP(4, g2w[0]);
     };
     auto seg3 = [&](int step) __attribute__((always_inline)) {
         const int par = step & 1;
@@ -2815,7 +2563,6 @@ fvp_coop_kernel(IterArgs A, Net net) {
             for (int s = 0; s < 4; ++s) t = PT<T>::mfma(fb1[kt][s], g2[kt][s], t);
         const V g1w = actv_bwd<T>(a1, y1w, t);
         sB1 += g1w;
-        CSTAMP(6, g1w[0]);
         // ---- RGW1 tiles (at, w) += Y1_at . G2_w^T ----
         if constexpr (Q::XT) {
             // both operands read transposed from the exchange rows, which hold them in the D layout
@@ -2863,7 +2610,6 @@ fvp_coop_kernel(IterArgs A, Net net) {
                 for (int s = 0; s < 4; ++s) accW0[kt] = PT<T>::mfma(ya[s], gg[s], accW0[kt]);
             }
         }
-        CSTAMP(7, accW0[T0 - 1][0]);
     };
     // the group exchanges' barrier (none with one wave per group)
     auto xsync = [&]() __attribute__((always_inline)) {
@@ -2875,25 +2621,12 @@ fvp_coop_kernel(IterArgs A, Net net) {
         const bool act = step * gstride + gbase < ntiles;
         if (act) seg0(step);
         xsync();
-        CSTAMP(1, r1w[0]);
         if (act) seg1(step);
         xsync();
-        CSTAMP(3, y2w[0]);
         if (act) seg2(step);
         xsync();
-        CSTAMP(5, g2w[0]);
         if (act) seg3(step);
     }
-#ifdef TRPO_STAMPS
-    const unsigned long long tend_ = __builtin_amdgcn_s_memtime();
-    if ((threadIdx.x == 0 || threadIdx.x == 64 * (Q::WAVES / 2)) && blockIdx.x < 1024) {
-        const int o = threadIdx.x ? 16 : 0;                             // wave 0 | the first wave of group 1
-        for (int k = 0; k < 8; ++k) g_stamps[blockIdx.x * 32 + o + k] = ph_[k];
-        g_stamps[blockIdx.x * 32 + o + 8] = tend_ - tloop_;           // the whole tile loop
-        g_stamps[blockIdx.x * 32 + o + 9] = (unsigned long long)nsteps;
-        g_stamps[blockIdx.x * 32 + o + 10] = tloop_ - tentry_;        // prologue: entry -> tile loop
-    }
-#endif
 
     // ---- epilogue: bias sums over the sample columns, NG-way group combine, block partial ----
 #pragma unroll
@@ -2970,12 +2703,6 @@ fvp_coop_kernel(IterArgs A, Net net) {
 #pragma unroll
                 for (int k = 0; k < Q::NW; ++k) slab4[(w * Q::NW + k) * 64 + lane] = acc[k];
             }
-#ifdef TRPO_STAMPS
-            if (threadIdx.x == 0 && blockIdx.x < 1024) {        // epilogue: tile loop end -> slab stored
-                asm volatile("" ::"v"(acc[0][0]));
-                g_stamps[blockIdx.x * 32 + 11] = __builtin_amdgcn_s_memtime() - tend_;
-            }
-#endif
         }
     }
 }
@@ -3075,10 +2802,7 @@ fvp_generic_kernel(const T *__restrict__ obs, int n, const T *__restrict__ th, c
 // layout (contiguous).  A block of 256 threads owns RS_POS consecutive slab positions; each
 // thread loads 16 B (4 fp32 / 2 fp64 positions) from every SG-th block partial (all its loads in
 // flight together), then the SG sub-sums are added in a fixed order through LDS.
-#ifndef TRPO_RS_POS
-#define TRPO_RS_POS 32
-#endif
-constexpr int RS_POS = TRPO_RS_POS, RS_THREADS = 256;
+constexpr int RS_POS = 32, RS_THREADS = 256;
 template <typename ST>
 __global__ void __launch_bounds__(RS_THREADS)
 reduce_slabs_kernel(const ST *__restrict__ slabs, int G, int slab, const int *__restrict__ imap,
@@ -3512,17 +3236,11 @@ cg_last_kernel(const double *__restrict__ acc, int R_in, const double *__restric
     for (int e = tid; e < zero_len; e += CGL_T) acc_zero[e] = 0.0;
 }
 
-#ifndef TRPO_CGS_T
-#define TRPO_CGS_T 256
-#endif
-constexpr int CGS_T = TRPO_CGS_T, CGS_K = 5 + QCAP;
+constexpr int CGS_T = 256, CGS_K = 5 + QCAP;
 // layout of the per-block partial dots (value k of block b of G): block-major [b][CGS_K] (default) or
 // value-major [k][G] (TRPO_DOTS_VMAJ=1: cg_axpy's loads coalesced, but each producer block's 21 values
 // land on 21 lines shared with other blocks)
-#ifndef TRPO_DOTS_VMAJ
-#define TRPO_DOTS_VMAJ 0
-#endif
-#define DOTS_AT(k, b, G) (TRPO_DOTS_VMAJ ? (long)(k) * (G) + (b) : (long)(b) * CGS_K + (k))
+#define DOTS_AT(k, b, G) ((long)(b) * CGS_K + (k))
 template <typename QT>
 __global__ void __launch_bounds__(CGS_T)
 cg_dots_kernel(const double *__restrict__ zacc, const double *__restrict__ p, const double *__restrict__ r,
@@ -3857,7 +3575,7 @@ static hipError_t fast_attr(int lds) {
     hipError_t e = hipFuncSetAttribute((const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 0, 0, NO>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
-    if constexpr (FastCfg<T0, T1, T2, T3>::REGW || TRPO_YC_ALL) {
+    if constexpr (FastCfg<T0, T1, T2, T3>::REGW) {
         e = hipFuncSetAttribute((const void *)fvp_mlp3_kernel<T0, T1, T2, T3, ACT, 2, 0, NO>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return e;
@@ -3877,7 +3595,7 @@ static hipError_t fast_attr(int lds) {
 // MODE 2 (forward cache) exists for the register-resident small-net shapes only
 template <int T0, int T1, int T2, int T3, int ACT, int MODE, int QB = 0, int NO = 0>
 static constexpr fast_launch_fn yc_launch() {
-    if constexpr (FastCfg<T0, T1, T2, T3>::REGW || TRPO_YC_ALL) return fast_launch<T0, T1, T2, T3, ACT, MODE, QB, NO>;
+    if constexpr (FastCfg<T0, T1, T2, T3>::REGW) return fast_launch<T0, T1, T2, T3, ACT, MODE, QB, NO>;
     else return nullptr;
 }
 
@@ -3911,15 +3629,9 @@ struct FastEntry {
         FAST_NO_PAIR(a, b, c, d, -1, 4)
 
 static const FastEntry kFast[] = {
-#ifdef TRPO_ARM_ONLY    // experiment builds (make variant): armDOF_0-class shapes only, fast to compile
-    FAST_ENTRY(1, 1, 1, 1, ACT_TTL), FAST_NO_PAIR(1, 1, 1, 1, ACT_TTL, 3),
-#elif defined(TRPO_DIAG_1441)   // diagnostic build: the 2x64 one-wave-per-tile shape only (with TRPO_COOP=0)
-    FAST_ENTRY(1, 4, 4, 1, ACT_TTL),
-#else
     FAST_SHAPE(1, 1, 1, 1), FAST_SHAPE(1, 2, 2, 1), FAST_SHAPE(1, 4, 4, 1),
     FAST_SHAPE(2, 1, 1, 1), FAST_SHAPE(2, 2, 2, 1), FAST_SHAPE(2, 4, 4, 1),
     FAST_SHAPE_NO(1, 1, 1, 1),
-#endif
 };
 
 // cooperative kernels (T1 == T2 == TH, T3 == 1); element type T: fp32 or the fp64 precision mode;
@@ -3931,7 +3643,7 @@ static void coop_launch(dim3 g, int lds, hipStream_t st, const IterArgs &a, cons
 }
 template <typename T, int T0, int TH>
 struct CoopYC {
-    static constexpr bool ok = sizeof(T) == 4 ? !(T0 == 2 && TH == 4) : (TH > 1 || TRPO_F64_TH1_WAVES <= 4);
+    static constexpr bool ok = sizeof(T) == 4 ? !(T0 == 2 && TH == 4) : true;
 };
 template <typename T, int T0, int TH, int ACT, int NO = 0>
 static hipError_t coop_attr(int lds) {
@@ -3972,14 +3684,10 @@ struct CoopEntry {
 #define COOP_SHAPE(T, t0, th) COOP_ENTRY(T, t0, th, ACT_TTL), COOP_ENTRY(T, t0, th, -1)
 #define COOP_SHAPE_NO(t0, th) COOP_ENTRY_NO(float, t0, th, ACT_TTL, 4), COOP_ENTRY_NO(float, t0, th, -1, 4)
 static const CoopEntry kCoop[] = {
-#if defined(TRPO_ARM_ONLY) || defined(TRPO_DIAG_1441)
-    COOP_ENTRY(double, 1, 1, ACT_TTL)};
-#else
     COOP_SHAPE(float, 1, 2),  COOP_SHAPE(float, 1, 4),  COOP_SHAPE(float, 2, 2),  COOP_SHAPE(float, 2, 4),
     COOP_SHAPE(double, 1, 1), COOP_SHAPE(double, 1, 2), COOP_SHAPE(double, 1, 4), COOP_SHAPE(double, 2, 1),
     COOP_SHAPE(double, 2, 2), COOP_SHAPE(double, 2, 4),
     COOP_SHAPE_NO(1, 2),      COOP_SHAPE_NO(1, 4),      COOP_SHAPE_NO(2, 2),      COOP_SHAPE_NO(2, 4)};
-#endif
 
 struct trpo_dev {
     int device;
@@ -4160,12 +3868,7 @@ static int hgroup_allreduce(trpo_dev *d, double *buf, size_t count) {
     // copies by KERNEL through the mapped buffer, not hipMemcpyAsync: a host-to-device hipMemcpyAsync
     // into buf followed by kernels reading buf gave intermittently stale reads (ranks diverging in
     // whole 512-element cg_axpy slices, 6 of 10 sharded 2x64 solves; tools/diag/shard_race.py)
-#ifndef TRPO_HGROUP_MEMCPY
-#define TRPO_HGROUP_MEMCPY 0      // diagnostic builds: the copies as hipMemcpyAsync instead
-#endif
-    if (ok && TRPO_HGROUP_MEMCPY)
-        ok = hipMemcpyAsync(d->gbuf, buf, sizeof(double) * count, hipMemcpyDeviceToHost, d->stream) == hipSuccess;
-    else if (ok) hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv((long)count, 256)), dim3(256), 0, d->stream,
+    if (ok) hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv((long)count, 256)), dim3(256), 0, d->stream,
                                (const double *)buf, d->gbuf_dev, (int)count);
     ok = ok && hipGetLastError() == hipSuccess;
     ok = ok && hipStreamSynchronize(d->stream) == hipSuccess;
@@ -4186,11 +3889,8 @@ static int hgroup_allreduce(trpo_dev *d, double *buf, size_t count) {
     if (!sum) return -4;
     memcpy(d->gbuf, sum, sizeof(double) * count);
     free(sum);
-    if (TRPO_HGROUP_MEMCPY)
-        HCHK(hipMemcpyAsync(buf, d->gbuf, sizeof(double) * count, hipMemcpyHostToDevice, d->stream));
-    else
-        hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv((long)count, 256)), dim3(256), 0, d->stream,
-                           (const double *)d->gbuf_dev, buf, (int)count);
+    hipLaunchKernelGGL(vcopy64_kernel, dim3(cdiv((long)count, 256)), dim3(256), 0, d->stream,
+                       (const double *)d->gbuf_dev, buf, (int)count);
     HCHK(hipGetLastError());
     DSYNC(d);
     return 0;
@@ -5988,15 +5688,9 @@ extern "C" const char *trpo_dev_kernel_name(const trpo_dev *d) { return d ? d->n
 
 // Diagnostic builds only: copy the per-block phase stamps (100 MHz ticks) to the host.
 extern "C" int trpo_dev_read_stamps(unsigned long long *out, int n) {
-#ifdef TRPO_STAMPS
-    if (n > 1024 * 32) n = 1024 * 32;
-    HCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * n, 0, hipMemcpyDeviceToHost));
-    return n;
-#else
     (void)out;
     (void)n;
     return -1;
-#endif
 }
 
 extern "C" int trpo_dev_geometry(const trpo_dev *d, int *blocks, int *threads, int *lds_bytes) {
