@@ -915,7 +915,10 @@ MFMA_COUNTERS = ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_MFMA", "SQ_BUSY_CYCLES", 
                  "GRBM_GUI_ACTIVE")
 
 
-def mfma_from_counters(med):
+PEAK_CLOCK_GHZ = 2.4                                  # MI355X peak engine clock (MI355X_MICROARCH.md)
+
+
+def mfma_from_counters(med, kernel_ms=None):
     """MFMA utilisation of the CG-iteration kernel from one counter pass (medians per dispatch):
     SQ_VALU_MFMA_BUSY_CYCLES (cycles, summed over every SIMD) / (1 024 SIMDs x GRBM_GUI_ACTIVE / 8), the
     dispatch's GPU-active cycles per XCD (MI355X_MICROARCH.md: GRBM_GUI_ACTIVE is the sum over the 8 XCDs,
@@ -926,17 +929,23 @@ def mfma_from_counters(med):
                                     "per dispatch of the CG-iteration kernel (medians); a lower bound on "
                                     "dispatches < 0.3 ms",
            "counters": {c: m[0] for c, m in med.items()}, "dispatches": med["GRBM_GUI_ACTIVE"][1]}
+    if kernel_ms:
+        # the same busy cycles over the kernel's HIP-event time at the peak clock: another lower bound (the
+        # clock under load is at most 2.4 GHz), one that short dispatches do not dilute
+        out["mfma_busy_frac_at_peak_clock"] = busy / (N_SIMDS * kernel_ms * 1e-3 * PEAK_CLOCK_GHZ * 1e9)
+        out["kernel_ms_events"] = kernel_ms
     if med.get("SQ_WAVE_CYCLES", (0,))[0] > 0:
         out["wait_inst_any_frac"] = med["SQ_WAIT_INST_ANY"][0] / med["SQ_WAVE_CYCLES"][0]
     return out
 
 
-def measure_mfma(device, n=N_TOTAL):
-    """roofline.mfma_busy_frac (VERDICT r05 #2): one counter pass (6 SQ + 1 GRBM slots) at n samples."""
+def measure_mfma(device, n=N_TOTAL, kernel_ms=None):
+    """roofline.mfma_busy_frac: one counter pass (5 SQ + 1 GRBM slots) at n samples;
+    kernel_ms: the kernel's HIP-event time from this run, for the peak-clock form."""
     med, why = pmc_pass(device, MFMA_COUNTERS, n=n, limit=150 if n > 500_000 else 90)
     if med is None:
         return {"error": why}
-    return dict(mfma_from_counters(med), measured="in this run", samples=n)
+    return dict(mfma_from_counters(med, kernel_ms), measured="in this run", samples=n)
 
 
 def main():
@@ -1077,13 +1086,13 @@ def main():
         traffic, tsrc = None, None
         if not args.no_pmc and os.environ.get("TRPO_TRAFFIC_JSON") is None:
             traffic, tsrc = measure_traffic(device)
-            mf = measure_mfma(device)
+            mf = measure_mfma(device, kernel_ms=k3)
             with emitter.lock:
                 result["roofline"]["mfma_busy_frac"] = mf.get("mfma_busy_frac")
                 result["roofline"]["mfma"] = mf
             row4m = (extra or {}).get("C4_sweep", {}).get("cg10_armDOF_0_N4000000")
             if isinstance(row4m, dict) and "error" not in row4m:
-                mf4 = measure_mfma(device, 4_000_000)
+                mf4 = measure_mfma(device, 4_000_000, kernel_ms=row4m.get("cg_iter_kernel_ms"))
                 with emitter.lock:
                     row4m["mfma_busy_frac"] = mf4.get("mfma_busy_frac")
                     row4m["mfma"] = mf4

@@ -736,9 +736,6 @@ __global__ void to_elem_kernel(void *dst, const double *src, long len, int f64) 
 // ---------------------------------------------------------------------------
 constexpr int SCR_LD = 20;            // scratch row stride (floats): conflict-free b32 writes
 
-#ifndef TRPO_YC_NT
-#define TRPO_YC_NT 2
-#endif
 template <int T0, int T1, int T2, int T3>
 struct FastCfg {
     // theta pack (floats)
@@ -773,9 +770,12 @@ struct FastCfg {
     static constexpr bool REGW = T0 * T1 + T1 * T2 + T2 * T3 <= 3;
     // 12 waves (3 per SIMD) for the small nets: ~1 tile per wave at N = 50k, balanced SIMDs
     static constexpr int WAVES = 8;
-    // tiles in flight per wave: the cached-forward small-net kernels (MODE 2 / 3) interleave TRPO_YC_NT
-    // tiles' independent MFMA chains (round 6); every other kernel streams one tile per trip
-    static constexpr int NT_YC = REGW ? TRPO_YC_NT : 1;
+    // tiles per trip of the cached-forward kernels (MODE 2 / 3).  Round 6 measured two
+    // tiles per trip, their MFMA chains interleaved instruction by instruction and every sum in the same order
+    // (bit-identical): slower at every size -- CG-iteration kernel 169.1 -> 171.9 us at 4M, 24.4 -> 26.0 us at
+    // 500k, 8.8 -> 9.7 us at 50k (profiles/r06_nt2_ab.log) -- so one tile per trip stays; the tile step
+    // keeps the NT-generic form
+    static constexpr int NT_YC = 1;
     static constexpr int THREADS = 64 * WAVES;
     static constexpr int PMAX = 256 * (T0 * T1 + T1 * T2 + T2 * T3) + 16 * (T1 + T2 + 2 * T3);
     // tile scratch; also stages the fp64 direction of the fused CG update
@@ -3295,6 +3295,181 @@ cg_dots_kernel(const double *__restrict__ zacc, const double *__restrict__ p, co
     }
 }
 
+// The CG step over natural-order slices (src/TRPO_CG.c:77-103 with the reorthogonalisation of DESIGN §3):
+// slice `sl` (CGS_T pairs) of x, r, p, the basis vector q_it and the fp32 direction pack, from the G producer
+// blocks' partial dots.  Two phases, so that a caller can issue the loads of the step's inputs (p, r, x,
+// the pack slots, the basis -- none of them written by the producers) before it waits for the producers:
+// axpy_load_inputs, then axpy_finish (z and the partial dots, the step, the stores).
+template <typename QT> struct AxIn {
+    double2 p2, r2, x2;
+    int2 ps2;
+    double qv[QCAP][2];
+};
+template <typename QT>
+__device__ __forceinline__ void axpy_load_inputs(AxIn<QT> &in, int sl, const double *__restrict__ p_in,
+                                                 const double *__restrict__ r_in, const double *__restrict__ x,
+                                                 const void *qbuf_v, const void *qz_v, int nq, int Ps,
+                                                 const float *vpk, const int *__restrict__ pslot) {
+    const QT *Q = reinterpret_cast<const QT *>(qbuf_v);
+    const QT *qz = reinterpret_cast<const QT *>(qz_v);
+    const int tid = threadIdx.x, t = sl * CGS_T + tid;
+    const int tc = min(t, (Ps >> 1) - 1);
+    in.p2 = reinterpret_cast<const double2 *>(p_in)[tc];
+    in.r2 = reinterpret_cast<const double2 *>(r_in)[tc];
+    in.x2 = reinterpret_cast<const double2 *>(x)[tc];
+    // vpk: p' also into the fp32 fragment-order direction pack of the next FVP (slots pslot[q], -1 for
+    // LogStd), so its cooperative kernel loads the pack coalesced instead of gathering p' itself
+    in.ps2 = vpk ? reinterpret_cast<const int2 *>(pslot)[tc] : make_int2(-1, -1);
+    typedef typename V2T<QT>::type QV2;
+#pragma unroll
+    for (int i = 0; i < QCAP; ++i) {
+        const bool ok = i < nq;
+        const QV2 *src = ok ? reinterpret_cast<const QV2 *>(Q + (long)i * Ps) + tc
+                            : reinterpret_cast<const QV2 *>(qz) + (tid & 7);
+        const QV2 v = *src;
+        in.qv[i][0] = ok ? (double)v.x : 0.0;
+        in.qv[i][1] = ok ? (double)v.y : 0.0;
+    }
+}
+template <typename QT>
+__device__ __forceinline__ void axpy_finish(const AxIn<QT> &in, int sl, const double *__restrict__ dots, int G,
+                                            const double *__restrict__ zbuf, double *__restrict__ p_out,
+                                            double *__restrict__ r_out, double *__restrict__ x, void *qbuf_v,
+                                            int reorth, int P, int Ps, Ctl *__restrict__ ctl,
+                                            const CgSt *__restrict__ st_in, CgSt *__restrict__ st_out,
+                                            double *__restrict__ hist, float *__restrict__ vpk, double *tot) {
+#pragma clang fp contract(off)
+    QT *Q = reinterpret_cast<QT *>(qbuf_v);
+    const int tid = threadIdx.x, t = sl * CGS_T + tid;
+    const int tc = min(t, (Ps >> 1) - 1);
+    const double2 z2 = reinterpret_cast<const double2 *>(zbuf)[tc];
+    // the partial dots of the G producer blocks (DOTS_AT): wave w sums values k = w,
+    // w + 4, ...; lane l takes partials l, l + 64, l + 128, l + 192 (all loads issued together, unconditional), then the
+    // fixed-order wave tree (a serial chain of G dependent loads by one thread was measured ~100 us
+    // at G = 176 partials)
+    constexpr int NW = CGS_T / 64, NI = (CGS_K + NW - 1) / NW, NJ = 4;
+    const int lane = tid & 63, w = tid >> 6;
+    double pv_[NI];
+    {
+        double v[NI][NJ];
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int k = w + NW * i, b = lane + 64 * j;
+                const double d = dots[DOTS_AT(min(k, CGS_K - 1), min(b, G - 1), G)];
+                // a multiply, not a select: with `cond ? d : 0` hipcc sank the loads under the condition
+                // (exec-masked, one vmcnt(0) drain each: 16 serialised round trips, round 5)
+                v[i][j] = d * ((k < CGS_K && b < G) ? 1.0 : 0.0);
+            }
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            double a = (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
+            for (int b = lane + 64 * NJ; b < G; b += 64) a += dots[DOTS_AT(min(w + NW * i, CGS_K - 1), b, G)];
+            pv_[i] = wave_tree_sum(a);
+        }
+    }
+    const CgSt sin = *st_in;
+    const double cth = ctl->resth;
+    const int cmax = ctl->maxiter;
+    // grid-uniform stop test on the state this step starts from: the value ctl->done held when the
+    // launch began (cg_init_kernel / the previous step set it by this formula).  Not *skip: block 0
+    // of THIS launch rewrites ctl->done at its end, and a block that starts after that (a GPU shared
+    // with other processes) would skip its slice of the final x update.  A stopped step carries the
+    // state forward (st_out = st_in) so that the next launch's test sees it too.
+    if (sin.rdotr < cth || sin.iter >= cmax) {
+        if (sl == 0 && tid == 0) *st_out = sin;
+        return;
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+            if (w + NW * i < CGS_K) tot[w + NW * i] = pv_[i];
+    }
+    __syncthreads();
+    const double pz = tot[0], rz = tot[1], zz = tot[2], xp = tot[3], pp = tot[4];
+    const double alpha = sin.rdotr / pz;
+    // reorthogonalisation coefficients (as the fused step, fvp_mlp3_kernel / DESIGN §3)
+    double cs = 0.0, cr = 0.0;
+    const bool ro = reorth && sin.rdotr > 0.0;
+    if (ro) {
+        const double nrm = sqrt(sin.rdotr), cl = nrm - alpha * (rz / nrm);
+        cs = cl * cl;
+        cr = cl / nrm;
+    }
+    double c[QCAP];
+#pragma unroll
+    for (int i = 0; i < QCAP; ++i) {
+        c[i] = ro ? -alpha * tot[5 + i] : 0.0;             // zero for the slots >= nq
+        cs += c[i] * c[i];
+    }
+    const double nr = sin.rdotr - 2.0 * alpha * rz + alpha * alpha * zz - cs;
+    const double xn2 = sin.xx + 2.0 * alpha * xp + alpha * alpha * pp;
+    const double beta = nr / sin.rdotr;
+    const int it = sin.iter + 1;
+    const double pe[2] = {in.p2.x, in.p2.y}, re[2] = {in.r2.x, in.r2.y}, xe[2] = {in.x2.x, in.x2.y},
+                 ze[2] = {z2.x, z2.y};
+    double xo[2], ro2[2], po[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        double rv = __builtin_fma(-alpha, ze[e], re[e]);
+        rv = __builtin_fma(-cr, re[e], rv);
+#pragma unroll
+        for (int i = 0; i < QCAP; ++i) rv = __builtin_fma(-c[i], in.qv[i][e], rv);
+        ro2[e] = rv;
+        xo[e] = __builtin_fma(alpha, pe[e], xe[e]);
+        po[e] = __builtin_fma(beta, pe[e], rv);
+    }
+    if (2 * t + 1 < P) {                                 // whole pairs: 16-byte stores
+        reinterpret_cast<double2 *>(x)[t] = make_double2(xo[0], xo[1]);
+        reinterpret_cast<double2 *>(r_out)[t] = make_double2(ro2[0], ro2[1]);
+        reinterpret_cast<double2 *>(p_out)[t] = make_double2(po[0], po[1]);
+    } else if (2 * t < P) {
+        x[2 * t] = xo[0];
+        r_out[2 * t] = ro2[0];
+        p_out[2 * t] = po[0];
+    }
+    if (vpk) {
+        if (2 * t < P && in.ps2.x >= 0) vpk[in.ps2.x] = (float)po[0];
+        if (2 * t + 1 < P && in.ps2.y >= 0) vpk[in.ps2.y] = (float)po[1];
+    }
+    if (reorth && it < QCAP) {                            // q_it = r' / |r'|
+        const double inv = nr > 0.0 ? 1.0 / sqrt(nr) : 0.0;
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+            if (2 * t + e < P) Q[(long)it * Ps + 2 * t + e] = (QT)(ro2[e] * inv);
+    }
+    if (sl == 0 && tid == 0) {
+        const int done = (nr < cth || it >= cmax) ? 1 : 0;
+        st_out->rdotr = nr;
+        st_out->xx = xn2;
+        st_out->iter = it;
+        hist[2 * it] = nr;
+        hist[2 * it + 1] = sqrt(xn2);
+        ctl->rdotr = nr;
+        ctl->iter = it;
+        ctl->done = done;
+        note_orth(&ctl->orth, cs, nr);
+        if (it <= CG_AMAX) ctl->alpha[it - 1] = alpha;
+    }
+}
+
+template <typename QT>
+__global__ void __launch_bounds__(CGS_T)
+cg_axpy_kernel(const double *__restrict__ dots, int G, const double *__restrict__ zbuf,
+               const double *__restrict__ p_in, const double *__restrict__ r_in, double *__restrict__ p_out,
+               double *__restrict__ r_out, double *__restrict__ x, void *qbuf_v, const void *qz_v, int nq, int reorth,
+               int P, int Ps, Ctl *__restrict__ ctl, const CgSt *__restrict__ st_in, CgSt *__restrict__ st_out,
+               double *__restrict__ hist, const int *__restrict__ skip, float *__restrict__ vpk = nullptr,
+               const int *__restrict__ pslot = nullptr) {
+    __shared__ double tot[CGS_K];
+    (void)skip;
+    AxIn<QT> in;
+    axpy_load_inputs<QT>(in, blockIdx.x, p_in, r_in, x, qbuf_v, qz_v, nq, Ps, vpk, pslot);
+    axpy_finish<QT>(in, blockIdx.x, dots, G, zbuf, p_out, r_out, x, qbuf_v, reorth, P, Ps, ctl, st_in, st_out, hist, vpk,
+                    tot);
+}
+
 // One rank (no all-reduce between the slab reduce and the step): reduce_slabs_kernel<float> and
 // cg_dots_kernel in ONE launch (round 5; TRPO_COOP_RDOTS=0 keeps the two).  Block b reduces its RS_POS
 // slab positions exactly as reduce_slabs_kernel does (same loads, same fixed order, the same zacc
@@ -3304,13 +3479,18 @@ cg_dots_kernel(const double *__restrict__ zacc, const double *__restrict__ p, co
 // q_i.z -> dots (DOTS_AT; cg_axpy_kernel sums the slab/RS_POS partials in block order).  The gathers
 // of p, r, x and the basis at the block's natural indices are issued between the slab loads and
 // their sums, so they add no round trip.  Only the dots' partition differs from the two-kernel form.
+// (Round 6, VERDICT r05 #5, measured and dropped: the step itself in this launch -- cg_axpy_kernel's work by
+// the first GA blocks once every block had published its z slice and dots, behind eight per-XCD arrival
+// counters, the step inputs' loads issued before the wait.  Bit-identical, but the fused launch took 11.6 us
+// against 5.3 + 5.4 us for the two, and the 2x64 CG solve 381.0 -> 392.8 us at 50k, 194.4 -> 205.3 us at
+// 4 096: the in-kernel fan-in costs more than the launch boundary it removes; profiles/r06_axf_ab.log.)
 template <typename QT>
 __global__ void __launch_bounds__(RS_THREADS)
 reduce_dots_kernel(const float *__restrict__ slabs, int G, int slab, const int *__restrict__ imap,
                    double *__restrict__ zacc, const double *__restrict__ p, const double *__restrict__ r,
-                   const double *__restrict__ x, double *__restrict__ zbuf, double *__restrict__ dots,
+                   const double *x, double *__restrict__ zbuf, double *__restrict__ dots,
                    const void *qbuf_v, const void *qz_v, int nq, int P, int Ps, int nw,
-                   const Ctl *__restrict__ ctl, const int *__restrict__ skip) {
+                   const Ctl *ctl, const int *__restrict__ skip) {
 #pragma clang fp contract(off)
     constexpr int VE = 4, LP = RS_POS / VE, SG = RS_THREADS / LP, NLD = 256 / SG;
     typedef float VT __attribute__((ext_vector_type(VE)));
@@ -3390,148 +3570,6 @@ reduce_dots_kernel(const float *__restrict__ slabs, int G, int slab, const int *
 #pragma unroll
         for (int k = 1; k < CGS_K; ++k) o = t == k ? red[k] : o;
         dots[DOTS_AT(t, blockIdx.x, gridDim.x)] = o;
-    }
-}
-
-template <typename QT>
-__global__ void __launch_bounds__(CGS_T)
-cg_axpy_kernel(const double *__restrict__ dots, int G, const double *__restrict__ zbuf,
-               const double *__restrict__ p_in, const double *__restrict__ r_in, double *__restrict__ p_out,
-               double *__restrict__ r_out, double *__restrict__ x, void *qbuf_v, const void *qz_v, int nq, int reorth,
-               int P, int Ps, Ctl *__restrict__ ctl, const CgSt *__restrict__ st_in, CgSt *__restrict__ st_out,
-               double *__restrict__ hist, const int *__restrict__ skip, float *__restrict__ vpk = nullptr,
-               const int *__restrict__ pslot = nullptr) {
-#pragma clang fp contract(off)
-    __shared__ double tot[CGS_K];
-    QT *Q = reinterpret_cast<QT *>(qbuf_v);
-    const QT *qz = reinterpret_cast<const QT *>(qz_v);
-    const int tid = threadIdx.x, t = blockIdx.x * CGS_T + tid;
-    const int tc = min(t, (Ps >> 1) - 1);
-    // the partial dots of the G producer blocks (DOTS_AT): wave w sums values k = w,
-    // w + 4, ...; lane l takes partials l, l + 64, l + 128, l + 192 (all loads issued together, unconditional), then the
-    // fixed-order wave tree (a serial chain of G dependent loads by one thread was measured ~100 us
-    // at G = 176 partials)
-    // this slice's vectors first (independent of the dots: their round trip overlaps the dots')
-    const double2 p2 = reinterpret_cast<const double2 *>(p_in)[tc], r2 = reinterpret_cast<const double2 *>(r_in)[tc];
-    const double2 x2 = reinterpret_cast<const double2 *>(x)[tc], z2 = reinterpret_cast<const double2 *>(zbuf)[tc];
-    // vpk: p' also into the fp32 fragment-order direction pack of the next FVP (slots pslot[q], -1 for
-    // LogStd), so its cooperative kernel loads the pack coalesced instead of gathering p' itself
-    const int2 ps2 = vpk ? reinterpret_cast<const int2 *>(pslot)[tc] : make_int2(-1, -1);
-    double qv[QCAP][2];
-    typedef typename V2T<QT>::type QV2;
-#pragma unroll
-    for (int i = 0; i < QCAP; ++i) {
-        const bool ok = i < nq;
-        const QV2 *src = ok ? reinterpret_cast<const QV2 *>(Q + (long)i * Ps) + tc
-                            : reinterpret_cast<const QV2 *>(qz) + (tid & 7);
-        const QV2 v = *src;
-        qv[i][0] = ok ? (double)v.x : 0.0;
-        qv[i][1] = ok ? (double)v.y : 0.0;
-    }
-    constexpr int NW = CGS_T / 64, NI = (CGS_K + NW - 1) / NW, NJ = 4;
-    const int lane = tid & 63, w = tid >> 6;
-    double pv_[NI];
-    {
-        double v[NI][NJ];
-#pragma unroll
-        for (int i = 0; i < NI; ++i)
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                const int k = w + NW * i, b = lane + 64 * j;
-                const double d = dots[DOTS_AT(min(k, CGS_K - 1), min(b, G - 1), G)];
-                // a multiply, not a select: with `cond ? d : 0` hipcc sank the loads under the condition
-                // (exec-masked, one vmcnt(0) drain each: 16 serialised round trips, round 5)
-                v[i][j] = d * ((k < CGS_K && b < G) ? 1.0 : 0.0);
-            }
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
-            double a = (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
-            for (int b = lane + 64 * NJ; b < G; b += 64) a += dots[DOTS_AT(min(w + NW * i, CGS_K - 1), b, G)];
-            pv_[i] = wave_tree_sum(a);
-        }
-    }
-    const CgSt sin = *st_in;
-    const double cth = ctl->resth;
-    const int cmax = ctl->maxiter;
-    // grid-uniform stop test on the state this step starts from: the value ctl->done held when the
-    // launch began (cg_init_kernel / the previous step set it by this formula).  Not *skip: block 0
-    // of THIS launch rewrites ctl->done at its end, and a block that starts after that (a GPU shared
-    // with other processes) would skip its slice of the final x update.  A stopped step carries the
-    // state forward (st_out = st_in) so that the next launch's test sees it too.
-    (void)skip;
-    if (sin.rdotr < cth || sin.iter >= cmax) {
-        if (blockIdx.x == 0 && tid == 0) *st_out = sin;
-        return;
-    }
-    if (lane == 0) {
-#pragma unroll
-        for (int i = 0; i < NI; ++i)
-            if (w + NW * i < CGS_K) tot[w + NW * i] = pv_[i];
-    }
-    __syncthreads();
-    const double pz = tot[0], rz = tot[1], zz = tot[2], xp = tot[3], pp = tot[4];
-    const double alpha = sin.rdotr / pz;
-    // reorthogonalisation coefficients (as the fused step, fvp_mlp3_kernel / DESIGN §3)
-    double cs = 0.0, cr = 0.0;
-    const bool ro = reorth && sin.rdotr > 0.0;
-    if (ro) {
-        const double nrm = sqrt(sin.rdotr), cl = nrm - alpha * (rz / nrm);
-        cs = cl * cl;
-        cr = cl / nrm;
-    }
-    double c[QCAP];
-#pragma unroll
-    for (int i = 0; i < QCAP; ++i) {
-        c[i] = ro ? -alpha * tot[5 + i] : 0.0;             // zero for the slots >= nq
-        cs += c[i] * c[i];
-    }
-    const double nr = sin.rdotr - 2.0 * alpha * rz + alpha * alpha * zz - cs;
-    const double xn2 = sin.xx + 2.0 * alpha * xp + alpha * alpha * pp;
-    const double beta = nr / sin.rdotr;
-    const int it = sin.iter + 1;
-    const double pe[2] = {p2.x, p2.y}, re[2] = {r2.x, r2.y}, xe[2] = {x2.x, x2.y}, ze[2] = {z2.x, z2.y};
-    double xo[2], ro2[2], po[2];
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-        double rv = __builtin_fma(-alpha, ze[e], re[e]);
-        rv = __builtin_fma(-cr, re[e], rv);
-#pragma unroll
-        for (int i = 0; i < QCAP; ++i) rv = __builtin_fma(-c[i], qv[i][e], rv);
-        ro2[e] = rv;
-        xo[e] = __builtin_fma(alpha, pe[e], xe[e]);
-        po[e] = __builtin_fma(beta, pe[e], rv);
-    }
-    if (2 * t + 1 < P) {                                 // whole pairs: 16-byte stores
-        reinterpret_cast<double2 *>(x)[t] = make_double2(xo[0], xo[1]);
-        reinterpret_cast<double2 *>(r_out)[t] = make_double2(ro2[0], ro2[1]);
-        reinterpret_cast<double2 *>(p_out)[t] = make_double2(po[0], po[1]);
-    } else if (2 * t < P) {
-        x[2 * t] = xo[0];
-        r_out[2 * t] = ro2[0];
-        p_out[2 * t] = po[0];
-    }
-    if (vpk) {
-        if (2 * t < P && ps2.x >= 0) vpk[ps2.x] = (float)po[0];
-        if (2 * t + 1 < P && ps2.y >= 0) vpk[ps2.y] = (float)po[1];
-    }
-    if (reorth && it < QCAP) {                            // q_it = r' / |r'|
-        const double inv = nr > 0.0 ? 1.0 / sqrt(nr) : 0.0;
-#pragma unroll
-        for (int e = 0; e < 2; ++e)
-            if (2 * t + e < P) Q[(long)it * Ps + 2 * t + e] = (QT)(ro2[e] * inv);
-    }
-    if (blockIdx.x == 0 && tid == 0) {
-        const int done = (nr < cth || it >= cmax) ? 1 : 0;
-        st_out->rdotr = nr;
-        st_out->xx = xn2;
-        st_out->iter = it;
-        hist[2 * it] = nr;
-        hist[2 * it + 1] = sqrt(xn2);
-        ctl->rdotr = nr;
-        ctl->iter = it;
-        ctl->done = done;
-        note_orth(&ctl->orth, cs, nr);
-        if (it <= CG_AMAX) ctl->alpha[it - 1] = alpha;
     }
 }
 
@@ -5686,12 +5724,6 @@ extern "C" double trpo_dev_time(trpo_dev *d, int what, int reps, size_t maxiter,
 
 extern "C" const char *trpo_dev_kernel_name(const trpo_dev *d) { return d ? d->name : ""; }
 
-// Diagnostic builds only: copy the per-block phase stamps (100 MHz ticks) to the host.
-extern "C" int trpo_dev_read_stamps(unsigned long long *out, int n) {
-    (void)out;
-    (void)n;
-    return -1;
-}
 
 extern "C" int trpo_dev_geometry(const trpo_dev *d, int *blocks, int *threads, int *lds_bytes) {
     if (!d) return -1;
