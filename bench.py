@@ -924,15 +924,21 @@ def mfma_from_counters(med, kernel_ms=None):
     dispatch's GPU-active cycles per XCD (MI355X_MICROARCH.md: GRBM_GUI_ACTIVE is the sum over the 8 XCDs,
     and reads high on dispatches shorter than ~0.3 ms, so at 50k this is a lower bound)."""
     busy, grbm = med["SQ_VALU_MFMA_BUSY_CYCLES"][0], med["GRBM_GUI_ACTIVE"][0]
-    out = {"mfma_busy_frac": busy / (N_SIMDS * grbm / N_XCDS) if grbm > 0 else None,
-           "mfma_busy_denominator": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs) "
-                                    "per dispatch of the CG-iteration kernel (medians); a lower bound on "
-                                    "dispatches < 0.3 ms",
+    grbm_frac = busy / (N_SIMDS * grbm / N_XCDS) if grbm > 0 else None
+    out = {"mfma_busy_frac": grbm_frac, "mfma_busy_frac_grbm": grbm_frac,
+           "mfma_busy_denominator": "1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs (the dispatch's GPU-active cycles, "
+                                    "per dispatch of the CG-iteration kernel, medians)",
            "counters": {c: m[0] for c, m in med.items()}, "dispatches": med["GRBM_GUI_ACTIVE"][1]}
     if kernel_ms:
-        # the same busy cycles over the kernel's HIP-event time at the peak clock: another lower bound (the
-        # clock under load is at most 2.4 GHz), one that short dispatches do not dilute
+        # the same busy cycles over the kernel's HIP-event time at the peak clock (the clock under load is at
+        # most 2.4 GHz, so a lower bound).  GRBM_GUI_ACTIVE reads high on dispatches shorter than ~0.3 ms
+        # (MI355X_MICROARCH.md), which dilutes the GRBM form at 50k (0.075 there against 0.14 here, round 6);
+        # at 4M the two agree (0.54 / 0.50).  So this form is the line's mfma_busy_frac when the event time is
+        # known.
         out["mfma_busy_frac_at_peak_clock"] = busy / (N_SIMDS * kernel_ms * 1e-3 * PEAK_CLOCK_GHZ * 1e9)
+        out["mfma_busy_frac"] = out["mfma_busy_frac_at_peak_clock"]
+        out["mfma_busy_denominator"] = ("1024 SIMDs x the kernel's HIP-event time x 2.4 GHz (peak clock: a lower "
+                                        "bound); mfma_busy_frac_grbm: over GRBM_GUI_ACTIVE / 8 XCDs instead")
         out["kernel_ms_events"] = kernel_ms
     if med.get("SQ_WAVE_CYCLES", (0,))[0] > 0:
         out["wait_inst_any_frac"] = med["SQ_WAIT_INST_ANY"][0] / med["SQ_WAVE_CYCLES"][0]

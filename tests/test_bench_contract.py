@@ -273,6 +273,8 @@ def test_mfma_busy_from_counters():
     assert "mfma_busy_frac_at_peak_clock" not in m
     m = bench.mfma_from_counters(med, kernel_ms=0.009)              # 9 us at 2.4 GHz = 21 600 cycles
     assert abs(m["mfma_busy_frac_at_peak_clock"] - 3.0e6 / (1024 * 21600.0)) < 1e-12
+    assert m["mfma_busy_frac"] == m["mfma_busy_frac_at_peak_clock"]          # the event form leads when known
+    assert abs(m["mfma_busy_frac_grbm"] - 3.0e6 / (1024 * 20700.0)) < 1e-12
     full = dict(med, SQ_VALU_MFMA_BUSY_CYCLES=(1024 * 20700.0, 9))
     assert abs(bench.mfma_from_counters(full)["mfma_busy_frac"] - 1.0) < 1e-12
 
