@@ -1129,6 +1129,11 @@ def main():
             pass
     if dist.broken:
         ctx.comm_abort()                        # a rank may be stuck: do not wait on the collective
+        # the exit status stays 0 (the headline was measured and verified before any secondary ran); the
+        # line itself says that a secondary's gloo collective failed, as do the secondaries'
+        # own error records
+        with emitter.lock:
+            result["dist_broken"] = True
     ctx.close()
     emitter.emit(result)
     if dist.broken:

@@ -61,6 +61,7 @@ def _ok(row):
 
 def test_secondaries_all_run_without_faults():
     d, _, _ = _run2()
+    assert "dist_broken" not in d
     ex = d["extra"]
     for k in ("C4_peer_exchange", "C4_peer_flag_exchange", "C5_update_armDOF_0_N50000"):
         assert _ok(ex[k]), (k, ex[k])
@@ -109,6 +110,7 @@ def test_hung_rank_in_a_secondary_is_bounded():
     secondary gloo group (6 s here), the remaining secondaries are skipped, rank 0 prints the line; rank
     1's watchdog ends it at the deadline.  Both exit 0, well inside the limit."""
     d, wall, _ = _run2("update.hang:1")
+    assert d.get("dist_broken") is True                    # the line says a secondary's collective failed
     ex = d["extra"]
     assert _ok(ex["C4_peer_exchange"])
     assert "error" in ex["C5_update_armDOF_0_N50000"]
