@@ -7,7 +7,12 @@ so exactly 10 Fisher-vector products + the fp64 CG vector updates) over a
 synthetic armDOF_0 batch of 50 000 samples resident in HBM (SURVEY.md §8d,
 configs C3/C4).  With --gpus N the 50 000 samples are split into contiguous
 shards, one per rank (one process per GPU), and every FVP all-reduces the
-P-sized partial sum over RCCL (strong scaling, config C4).
+P-sized partial sum over xGMI (strong scaling, config C4): by default with the
+library's one-shot peer-window exchange (--comm peer; SURVEY §5 / §8e: "prefer
+... a custom P2P one-shot all-reduce over IPC buffers" for these 2-43 KB
+messages), RCCL's all-reduce timed beside it (extra.C4_rccl_exchange) and taken
+instead if the peer exchange fails its setup or self-check (--comm rccl swaps
+the two roles).
 
     python bench.py                      # N=1
     python bench.py --gpus 8             # launches 8 rank processes itself
@@ -59,8 +64,12 @@ def parse_args():
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--comm", choices=("rccl", "peer"), default="rccl",
-                    help="N > 1: collective of the headline solve (peer: the peer-window exchange over xGMI)")
+    # round 6: the peer-window exchange is the headline's default collective at N > 1.  Its one-GPU floor is
+    # 3.56 us per exchange (profiles/r05_peer_floor_1gpu.txt) against RCCL's multi-step protocol for the 9-37 KB
+    # replica message; RCCL stays the measured A/B (extra.C4_rccl_exchange) and the fallback of the agreed setup
+    ap.add_argument("--comm", choices=("rccl", "peer"), default="peer",
+                    help="N > 1: collective of the headline solve (peer: the peer-window exchange over xGMI, "
+                         "default; rccl: RCCL's all-reduce)")
     ap.add_argument("--no-pmc", action="store_true",
                     help="N = 1: take roofline.traffic from the newest committed profile instead of measuring it")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)   # internal: see measure_traffic

@@ -22,7 +22,10 @@ def _port():
         return s.getsockname()[1]
 
 
-def _run2(fault=None, env_extra=None, args=("--steps", "3", "--warmup", "1", "--no-cpu-baseline"), limit=150):
+def _run2(fault=None, env_extra=None, args=("--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--comm", "rccl"),
+          limit=150):
+    # (--comm rccl: the scenario these cases were written for -- RCCL headline, the peer forms as secondaries;
+    # the default collective is the peer exchange since round 6, which the fake context serves the same way)
     port = _port()
     procs = []
     t0 = time.monotonic()
@@ -126,3 +129,14 @@ def test_hung_rank0_prints_by_watchdog():
     assert _ok(d["extra"]["C4_peer_exchange"])
     assert "C4_peer_flag_exchange" not in d["extra"]
     assert wall < 90
+
+
+def test_default_collective_is_the_peer_exchange():
+    """Round 6: without --comm the headline's collective is the peer-window exchange, and RCCL is the
+    measured secondary (extra.C4_rccl_exchange) beside the flag form and the sharded update."""
+    d, _, _ = _run2(args=("--steps", "3", "--warmup", "1", "--no-cpu-baseline"))
+    assert d["comm"]["backend"] == "peer" and "peer-window" in d["config"]["parallelism"]
+    ex = d["extra"]
+    for k in ("C4_rccl_exchange", "C4_peer_flag_exchange", "C5_update_armDOF_0_N50000"):
+        assert _ok(ex[k]), (k, ex[k])
+    assert ex["C4_rccl_exchange"]["backend"] == "rccl"
