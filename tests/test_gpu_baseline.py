@@ -88,3 +88,59 @@ def test_lbfgs_fit_matches_oracle_fit():
     assert fd < 0.9 * oracle.baseline_evaluate(L, acf, x0, obs, tgt, nep, eplen)[0]   # it fits
     assert cases.rel_l2(xd, xo) <= 1e-8
     assert abs(fd - fo) <= 1e-10 * abs(fo)
+
+
+@pytest.mark.parametrize("num_ep,ep_len", [(1, 20), (5, 106), (20, 150), (40, 300)])
+def test_lane_kernel_in_launch_sum_and_handoff(num_ep, ep_len, monkeypatch):
+    """Round 6: the lane kernel sums its block slabs in the same launch (groups of 16 blocks, then the
+    groups) and hands the result over through pinned memory.  Grids of 1, 17 (a last group of one
+    block), 94 and 256 blocks (16 full groups) against the one-lane kernel, and repeated calls -- with
+    and without predictions, on changing parameters -- bit-identical to a fresh context's."""
+    L, acf = [16, 16, 16, 1], "lttl"
+    x, obs, tgt = trpo_amd.synth.make_baseline_problem(L, num_ep, ep_len)
+    xs = [x, x * 0.9 + 0.01, x]
+    monkeypatch.setenv("TRPO_BASELINE_LANE", "0")
+    with trpo_amd.Baseline(L, acf) as b:
+        b.set_data(obs, tgt, num_ep, ep_len)
+        ref = [b.evaluate(v, want_predict=True) for v in xs]
+    monkeypatch.setenv("TRPO_BASELINE_LANE", "1")
+    with trpo_amd.Baseline(L, acf) as b:
+        b.set_data(obs, tgt, num_ep, ep_len)
+        got = [b.evaluate(v, want_predict=(k % 2 == 0)) for k in range(6) for v in xs]
+    with trpo_amd.Baseline(L, acf) as b:
+        b.set_data(obs, tgt, num_ep, ep_len)
+        fresh = [b.evaluate(v, want_predict=True) for v in xs]
+    for k, r in enumerate(got):
+        f = fresh[k % 3]
+        assert r[0] == f[0]
+        np.testing.assert_array_equal(r[1], f[1])
+        if len(r) == 3:
+            np.testing.assert_array_equal(r[2], f[2])
+    for f, r in zip(fresh, ref):
+        np.testing.assert_array_equal(f[2], r[2])
+        assert abs(f[0] - r[0]) <= 1e-14 * abs(r[0])
+        assert cases.rel_l2(f[1], r[1]) <= 1e-13
+
+
+def test_evaluate_sees_arrays_rewritten_in_place():
+    """Round 6: the drop-in evaluate starts the device on the data it uploaded and compares the caller's
+    arrays meanwhile; arrays rewritten IN PLACE (same addresses) between callbacks must still give the
+    new data's objective -- the stale result is dropped and the evaluation repeated (observations, then
+    targets, then unchanged again)."""
+    import oracle
+    c = cases.case("syn_baseline_n3000")
+    x, obs, tgt = cases.baseline_inputs(c)
+    p = trpo_amd.make_baseline_param(c["layers"], c["acfunc"], obs, tgt, c["num_ep"], c["ep_len"])
+    o_arr, t_arr = p._keep[0], p._keep[1]
+    g = np.zeros(c["padded"])
+    trpo_amd.evaluate(p, x, g)
+    for change in ("obs", "tgt", None):
+        if change == "obs":
+            o_arr[7, 3] += 0.25
+        elif change == "tgt":
+            t_arr[11] -= 0.5
+        f = trpo_amd.evaluate(p, x, g)
+        fr, gr, pr = oracle.baseline_evaluate(c["layers"], c["acfunc"], x, o_arr, t_arr, c["num_ep"], c["ep_len"])
+        assert abs(f - fr) <= 1e-13 * abs(fr), change
+        assert cases.rel_l2(g, gr) <= 1e-12, change
+        assert cases.rel_l2(p.predict, pr) <= 1e-12, change

@@ -110,6 +110,8 @@ trpo_bdev *trpo_bdev_create(int device, size_t nl, const size_t *ls, const char 
 void trpo_bdev_destroy(trpo_bdev *b);
 int trpo_bdev_set_data(trpo_bdev *b, const double *obs, const double *target, size_t n);
 int trpo_bdev_eval(trpo_bdev *b, const double *theta, double *gsum, double *pred);
+int trpo_bdev_eval_start(trpo_bdev *b, const double *theta, int want_pred);
+int trpo_bdev_eval_finish(trpo_bdev *b, double *gsum, double *pred);
 
 const char *trpo_dev_kernel_name(const trpo_dev *d);
 int trpo_dev_geometry(const trpo_dev *d, int *blocks, int *threads, int *lds_bytes);

@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <math.h>
+#include <chrono>
 #include <stdlib.h>
 #include <string.h>
 
@@ -1174,12 +1175,27 @@ baseline_kernel(Net net, const double *__restrict__ thg, const double *__restric
 // and b2 and sum (y - t)^2) over the group's samples in sample order; the block's 16 groups are combined
 // in group order through LDS into the block's slab (natural order, the layout baseline_kernel writes).
 // Only the order of the sums over samples differs from baseline_kernel.
+//
+// Round 6: two launches per evaluate instead of three and no hipStreamSynchronize -- a small launch
+// costs the host ~2.5 us to enqueue and the stream sync ~4.7 us more than spinning on pinned memory
+// (tools/micro/host_wait, profiles/r06_host_wait.log):
+//   - theta arrives BY VALUE in the kernel arguments (BlTheta, 4.5 KB: [16,16,16,1]'s 561 weights and
+//     biases are the most this kernel takes; tools/micro/kernarg_big: +0.16 us of enqueue), no copy kernel;
+//   - the slab sum (sum_slabs64_host_kernel) stores the sums into the pinned host buffer, each of its
+//     blocks then its own flag word (the call's sequence number), and the host spins on the flags.
+//     Summing the slabs in the same launch instead (the last block of each 16 sums their slabs, the
+//     last group the partials, then one flag) was measured slower: 35 -> 58 us per evaluate with
+//     agent-scope fences, 35 -> 43 us with fence-free `sc1` hand-offs -- each in-launch hand-off is a
+//     drained store plus an atomic round trip, ~2 us apiece on this chip (profiles/r06_baseline_eval_ab.log).
 constexpr int BLK_NE = 37;                 // per-lane accumulators: 16 W0, b0, 16 W1, b1, W2, b2, sum d^2
+constexpr int BL_PA_MAX = 16 * 16 * 2 + 16 * 3 + 1;    // [16,16,16,1]: 561 weights and biases
+struct BlTheta {
+    double v[BL_PA_MAX];
+};
 __global__ void __launch_bounds__(256)
-baseline_lane_kernel(Net net, const double *__restrict__ thg, const double *__restrict__ obs,
-                     const double *__restrict__ target, int n, double *__restrict__ slabs,
-                     double *__restrict__ pred) {
-    __shared__ double tl[16 * 16 * 2 + 16 * 3 + 2];     // theta (<= 16x16 + 16 + 16x16 + 16 + 16 + 1)
+baseline_lane_kernel(Net net, BlTheta th, const double *__restrict__ obs, const double *__restrict__ target, int n,
+                     double *__restrict__ slabs, double *__restrict__ pred) {
+    __shared__ double tl[BL_PA_MAX + 1];                // theta (<= 16x16 + 16 + 16x16 + 16 + 16 + 1)
     __shared__ double acc[16][BLK_NE][16];              // [group][entry][lane]
     const int tid = threadIdx.x, lane = tid & 63, j = lane & 15, base = lane & ~15;
     const int gi = tid >> 4;                            // group in the block, 0..15
@@ -1187,7 +1203,7 @@ baseline_lane_kernel(Net net, const double *__restrict__ thg, const double *__re
     const int a1 = net.act[1], a2 = net.act[2], a3 = net.act[3];
     const int W0 = net.woff[0], B0 = net.boff[0], W1 = net.woff[1], B1 = net.boff[1];
     const int W2 = net.woff[2], B2 = net.boff[2], PA = net.P - net.A;
-    for (int q = tid; q < PA; q += 256) tl[q] = thg[q];
+    for (int q = tid; q < PA; q += 256) tl[q] = th.v[q];
     __syncthreads();
     double dw0[16], dw1[16], db0 = 0.0, db1 = 0.0, dw2 = 0.0, db2 = 0.0, fs = 0.0;
 #pragma unroll
@@ -1213,7 +1229,7 @@ baseline_lane_kernel(Net net, const double *__restrict__ thg, const double *__re
         for (int k = 0; k < L2; ++k) z3 += y2k[k] * tl[W2 + k];
         const double y3 = act_y64(a3, z3);
         const double d = y3 - target[s];
-        if (j == 0) pred[s] = y3;
+        if (pred && j == 0) __hip_atomic_store(pred + s, y3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);   // pinned
         // backward (baseline_kernel's order)
         const double g3 = act_d64(a3, y3, 0.02 * d);
         const double g2 = j < L2 ? act_d64(a2, y2, 0.0 + g3 * tl[W2 + j]) : 0.0;
@@ -1262,6 +1278,30 @@ baseline_lane_kernel(Net net, const double *__restrict__ thg, const double *__re
         slab[q] = v;
     }
 }
+// the slab sum of the evaluate (sum_slabs64_kernel's order) into pinned host memory; each block stores
+// the call's sequence number into its own flag word behind its drained system-scope stores
+__global__ void sum_slabs64_host_kernel(const double *__restrict__ slabs, int G, int len, double *__restrict__ out,
+                                        unsigned *__restrict__ flags, unsigned seq) {
+    __shared__ double part[16][17];
+    const int tq = threadIdx.x & 15, tj = threadIdx.x >> 4;
+    const int q = blockIdx.x * 16 + tq;
+    double s = 0.0;
+    if (q < len) {
+#pragma unroll 8
+        for (int b = tj; b < G; b += 16) s += slabs[(long)b * len + q];
+    }
+    part[tj][tq] = s;
+    __syncthreads();
+    if (tj == 0 && q < len) {
+        double t = 0.0;
+        for (int j = 0; j < 16; ++j) t += part[j][tq];
+        __hip_atomic_store(out + q, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flags + blockIdx.x, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 
 struct trpo_bdev {
     int device = 0;
@@ -1278,6 +1318,8 @@ struct trpo_bdev {
     int lane_ok = 0, Gl = 1;                       // baseline_lane_kernel applies / its grid (round 5)
     double *hst = nullptr, *hst_dev = nullptr;   // pinned mapped host buffer: theta in, sums (+ predictions) out
     size_t hst_cap = 0;
+    unsigned seq = 0;                            // the lane path's host hand-off: the last call's sequence number
+    int started = 0, want_pred = 0;              // an eval_start without its eval_finish yet; with predictions
 };
 
 static int act_code64(char a) {
@@ -1387,7 +1429,9 @@ extern "C" int trpo_bdev_set_data(trpo_bdev *b, const double *obs, const double 
     const char *el = getenv("TRPO_BASELINE_LANE");
     b->lane_ok = !(el && atoi(el) == 0) && nt.nl == 4 && nt.L[3] == 1 && nt.L[0] <= 16 && nt.L[1] <= 16 &&
                  nt.L[2] <= 16;
-    b->Gl = n ? (cdiv((long)n, 32) < 256 ? (int)cdiv((long)n, 32) : 256) : 1;
+    // one sample per 16-lane group up to 256 blocks (round 6; 2 per group before: 31.3 -> 25.7 us per
+    // evaluate at N = 3 000, profiles/r06_baseline_eval_ab.log)
+    b->Gl = n ? (cdiv((long)n, 16) < 256 ? (int)cdiv((long)n, 16) : 256) : 1;
     const int gs = b->lane_ok && b->Gl > b->G ? b->Gl : b->G;
     if (ensure(&b->slabs, &b->slab_cap, (size_t)gs * (b->net.P + 1), b->stream)) return -2;
     if (!b->use_lds && ensure(&b->ws, &b->ws_cap, (size_t)b->rows * RS * b->G, b->stream)) return -2;
@@ -1399,16 +1443,43 @@ extern "C" int trpo_bdev_set_data(trpo_bdev *b, const double *obs, const double 
     return 0;
 }
 
+// Waits until the nf flag words in pinned host memory read seq.  Spinning answers ~4.7 us sooner than
+// hipStreamSynchronize for one small launch (tools/micro/host_wait: 6.9 vs 11.6 us round trip); after
+// the first 100 us the stream is queried between spins, so a launch that failed returns its error
+// instead of spinning (and one that completed without its flags is an error too).
+static int wait_host_flags(hipStream_t st, const unsigned *flags, int nf, unsigned seq) {
+    const auto t0 = std::chrono::steady_clock::now();
+    int k = 0;                                   // flags[0 .. k) already read seq
+    for (unsigned long i = 1;; ++i) {
+        while (k < nf && __atomic_load_n(flags + k, __ATOMIC_ACQUIRE) == seq) ++k;
+        if (k == nf) return 0;
+        if ((i & 63) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(100)) {
+            const hipError_t e = hipStreamQuery(st);
+            if (e == hipSuccess) {
+                while (k < nf && __atomic_load_n(flags + k, __ATOMIC_ACQUIRE) == seq) ++k;
+                return k == nf ? 0 : -2;
+            }
+            if (e != hipErrorNotReady) return -2;
+        }
+        __builtin_ia32_pause();
+    }
+}
+
 // theta: natural [W, B per layer] (P - A values); gsum[P + 1]: gradient sums (P - A entries),
 // then sum (y - t)^2 at P - A; pred (n, may be NULL) receives the predictions
-extern "C" int trpo_bdev_eval(trpo_bdev *b, const double *theta, double *gsum, double *pred) {
-    if (!b || !theta || !gsum || !b->n) return -1;
+// trpo_bdev_eval in two halves, so that a caller can do host work while the device evaluates
+// (evaluate()'s comparison of the caller's arrays, trpo_host.c): _start enqueues, _finish waits and
+// copies out; every _start must be followed by one _finish.  want_pred: the predictions are produced.
+extern "C" int trpo_bdev_eval_start(trpo_bdev *b, const double *theta, int want_pred) {
+    if (!b || !theta || !b->n || b->started) return -1;
     HCHK(hipSetDevice(b->device));
     const Net &net = b->net;
     const int P = net.P;
     // x in and (f, g[, predictions]) out through pinned device-mapped host memory, moved by small
     // kernels: no pageable copies on the L-BFGS callback's critical path
-    const size_t need = (size_t)P + 1 + b->n + (size_t)(P - net.A);   // [f, g | predictions | theta in]
+    // [f, g | predictions | theta in | the slab sum's per-block flags]
+    const int nfl = cdiv(P + 1, 16);
+    const size_t need = (size_t)P + 1 + b->n + (size_t)(P - net.A) + cdiv(nfl, 2);
     if (need > b->hst_cap) {
         if (b->hst) hipHostFree(b->hst);
         b->hst = b->hst_dev = nullptr;
@@ -1416,17 +1487,30 @@ extern "C" int trpo_bdev_eval(trpo_bdev *b, const double *theta, double *gsum, d
         HCHK(hipHostMalloc((void **)&b->hst, sizeof(double) * need, TRPO_HOST_COHERENT));
         HCHK(hipHostGetDevicePointer((void **)&b->hst_dev, b->hst, 0));
         b->hst_cap = need;
+        memset(b->hst, 0, sizeof(double) * need);
+    }
+    if (b->lane_ok && P - net.A <= BL_PA_MAX) {
+        // theta by value, the sums (and the predictions) straight into the pinned buffer, a spin on the
+        // slab sum's flags (baseline_lane_kernel)
+        BlTheta th;
+        memcpy(th.v, theta, sizeof(double) * (P - net.A));
+        if (++b->seq == 0) b->seq = 1;
+        const size_t foff = (size_t)P + 1 + b->n + (size_t)(P - net.A);
+        hipLaunchKernelGGL(baseline_lane_kernel, dim3(b->Gl), dim3(256), 0, b->stream, net, th, (const double *)b->obs,
+                           (const double *)b->target, (int)b->n, b->slabs, want_pred ? b->hst_dev + P + 1 : nullptr);
+        hipLaunchKernelGGL(sum_slabs64_host_kernel, dim3(nfl), dim3(256), 0, b->stream, (const double *)b->slabs, b->Gl,
+                           P + 1, b->hst_dev, (unsigned *)(b->hst_dev + foff), b->seq);
+        HCHK(hipGetLastError());
+        b->started = 1;
+        b->want_pred = want_pred;
+        return 0;
     }
     double *hin = b->hst + P + 1 + b->n;                   // theta staging after the outputs
     memcpy(hin, theta, sizeof(double) * (P - net.A));
     hipLaunchKernelGGL(copy64_kernel, dim3(cdiv(P - net.A, 256)), dim3(256), 0, b->stream,
                        (const double *)(b->hst_dev + P + 1 + b->n), b->theta, P - net.A);
-    int gsl = b->G;
-    if (b->lane_ok) {
-        hipLaunchKernelGGL(baseline_lane_kernel, dim3(b->Gl), dim3(256), 0, b->stream, net, (const double *)b->theta,
-                           (const double *)b->obs, (const double *)b->target, (int)b->n, b->slabs, b->pred);
-        gsl = b->Gl;
-    } else {
+    const int gsl = b->G;
+    {
         void (*bk)(Net, const double *, const double *, const double *, int, double *, int, int, double *, double *) =
             b->theta_lds ? baseline_kernel<true, true>
                          : (b->use_lds ? baseline_kernel<true, false> : baseline_kernel<false, false>);
@@ -1437,12 +1521,35 @@ extern "C" int trpo_bdev_eval(trpo_bdev *b, const double *theta, double *gsum, d
     // the sums go straight into the mapped host buffer (round 5: one copy launch fewer per callback)
     hipLaunchKernelGGL(sum_slabs64_kernel, dim3(cdiv(P + 1, 16)), dim3(256), 0, b->stream, b->slabs, gsl, P + 1,
                        b->hst_dev);
-    if (pred)
+    if (want_pred)
         hipLaunchKernelGGL(copy64_kernel, dim3(cdiv((long)b->n, 256)), dim3(256), 0, b->stream, (const double *)b->pred,
                            b->hst_dev + P + 1, (int)b->n);
     HCHK(hipGetLastError());
-    HCHK(hipStreamSynchronize(b->stream));
+    b->started = 1;
+    b->want_pred = want_pred;
+    return 0;
+}
+
+extern "C" int trpo_bdev_eval_finish(trpo_bdev *b, double *gsum, double *pred) {
+    if (!b || !gsum || !b->started || (pred && !b->want_pred)) return -1;
+    b->started = 0;
+    HCHK(hipSetDevice(b->device));
+    const Net &net = b->net;
+    const int P = net.P;
+    if (b->lane_ok && P - net.A <= BL_PA_MAX) {
+        const size_t foff = (size_t)P + 1 + b->n + (size_t)(P - net.A);
+        if (const int rc = wait_host_flags(b->stream, (const unsigned *)(b->hst + foff), cdiv(P + 1, 16), b->seq))
+            return rc;
+    } else {
+        HCHK(hipStreamSynchronize(b->stream));
+    }
     memcpy(gsum, b->hst, sizeof(double) * (P + 1));
     if (pred) memcpy(pred, b->hst + P + 1, sizeof(double) * b->n);
     return 0;
+}
+
+extern "C" int trpo_bdev_eval(trpo_bdev *b, const double *theta, double *gsum, double *pred) {
+    if (!gsum) return -1;
+    const int rc = trpo_bdev_eval_start(b, theta, pred != nullptr);
+    return rc ? rc : trpo_bdev_eval_finish(b, gsum, pred);
 }
