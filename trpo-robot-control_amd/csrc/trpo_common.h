@@ -114,6 +114,8 @@ int trpo_dev_pg_sums_fast(trpo_dev *d, const double *roll64, unsigned roll_gen, 
 int trpo_dev_pg_prepare(trpo_dev *d, const double *roll64, unsigned roll_gen);
 // the update path's CG (graph-replayed unless TRPO_CG_GRAPH=0: it sits between other kernels)
 int trpo_dev_cg_in_sequence(trpo_dev *d, size_t maxiter, double resth);
+// whether the context has a collective attached (RCCL, host group or peer exchange): its waits are bounded
+int trpo_dev_has_collective(const trpo_dev *d);
 // forward-cache bookkeeping after a CG solve
 void trpo_dev_ycache_written(trpo_dev *d);
 // per-context storage of the update path (owned by trpo_update.hip)

@@ -4750,6 +4750,8 @@ static int wait_stream(trpo_dev *d, long timeout_ms, bool spin) {
 // The host's wait at the end of a synchronous call (update, FVP, surrogate, ...): a plain stream
 // synchronisation on one rank; with a collective attached a peer that never arrives must not hang the
 // caller, so the wait is bounded (TRPO_COMM_TIMEOUT_MS / 120 s) and reports -6 / the collective's error.
+int trpo_dev_has_collective(const trpo_dev *d) { return has_collective(d) ? 1 : 0; }
+
 extern "C" int trpo_dev_wait_done(trpo_dev *d) {
     if (!has_collective(d)) return hipStreamSynchronize(d->stream) == hipSuccess ? 0 : -2;
     const int rc = wait_stream(d, 0, true);

@@ -54,6 +54,7 @@ struct UpdState {
     // round trips through pageable memory); fullstep goes the other way through it
     double *hst = nullptr, *hst_dev = nullptr;
     size_t hst_cap = 0;
+    unsigned seq = 0;                       // export_solve_kernel's flags: the last update's sequence number
     unsigned roll_gen = 0;                 // bumped by every rollout upload
 };
 
@@ -716,25 +717,36 @@ static int ensure_host(UpdState *u, size_t count) {
     HCHK(hipHostMalloc((void **)&u->hst, sizeof(double) * count, TRPO_HOST_COHERENT));
     HCHK(hipHostGetDevicePointer((void **)&u->hst_dev, u->hst, 0));
     u->hst_cap = count;
+    memset(u->hst, 0, sizeof(double) * count);     // export_solve_kernel's flag words start below any seq
     return 0;
 }
 
 // b, x, z (P each), sum(Adv), the CG iteration count and 2 (H) history values -> mapped host memory
+// The update's results into the pinned host buffer: b, x, z, the advantage sum, the iteration count, the
+// (rdotr, |x|) history and the CG statistics (out + 3P + 5 + H); then every block stores the call's
+// sequence number into its own flag word behind its drained system-scope stores, and the host spins on
+// the flags instead of a stream sync (round 6, as the baseline evaluate: ~4.7 us sooner per update, one
+// launch fewer than a separate statistics copy).
 __global__ void export_solve_kernel(const double *__restrict__ b, const double *__restrict__ x,
                                     const double *__restrict__ z, const double *__restrict__ adv,
                                     const int *__restrict__ iter, const double *__restrict__ hist, int P, int H,
-                                    double *out) {
+                                    const double *__restrict__ stats, double *out, unsigned *flags, unsigned seq) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    constexpr int MS = __HIP_MEMORY_SCOPE_SYSTEM;
     if (i < P) {
-        out[i] = b[i];
-        out[P + i] = x[i];
-        out[2 * P + i] = z[i];
+        __hip_atomic_store(out + i, b[i], __ATOMIC_RELAXED, MS);
+        __hip_atomic_store(out + P + i, x[i], __ATOMIC_RELAXED, MS);
+        __hip_atomic_store(out + 2 * P + i, z[i], __ATOMIC_RELAXED, MS);
     }
     if (i == 0) {
-        out[3 * P] = *adv;
-        out[3 * P + 1] = (double)*iter;
+        __hip_atomic_store(out + 3 * P, *adv, __ATOMIC_RELAXED, MS);
+        __hip_atomic_store(out + 3 * P + 1, (double)*iter, __ATOMIC_RELAXED, MS);
     }
-    if (i < H) out[3 * P + 2 + i] = hist[i];
+    if (i < H) __hip_atomic_store(out + 3 * P + 2 + i, hist[i], __ATOMIC_RELAXED, MS);
+    if (i < TRPO_CG_STATS) __hip_atomic_store(out + 3 * P + 5 + H + i, stats[i], __ATOMIC_RELAXED, MS);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flags + blockIdx.x, seq, __ATOMIC_RELAXED, MS);
 }
 
 // Step size of the update (src/TRPO_Update.c:836-846): shs = 0.5 x.Fx, lm = sqrt(shs / max_kl),
@@ -925,7 +937,14 @@ extern "C" int trpo_dev_policy_gradient(trpo_dev *d, double *b_host, double *adv
     return 0;
 }
 
-static int enqueue_surrogate(trpo_dev *d, const double *fs, int k0, int nk);
+static int enqueue_surrogate(trpo_dev *d, const double *fs, int k0, int nk, double *host_out = nullptr);
+static int wait_host_flags(hipStream_t st, const unsigned *flags, int nf, unsigned seq, long query_after_us);
+// export_solve_kernel's grid and the offset of its flag words in the update's pinned buffer
+static int export_blocks(int P, int H) {
+    const int m = P > H ? P : H;
+    return cdiv(m > TRPO_CG_STATS ? m : TRPO_CG_STATS, 256);
+}
+static size_t export_flags_at(int P, int H) { return (size_t)3 * P + 5 + H + TRPO_CG_STATS; }
 
 // policy gradient -> B, CG -> X, FVP(x) -> Z, [step + full-step surrogate], results -> mapped host memory
 static int enqueue_update_device(trpo_dev *d, size_t maxiter, double resth, double max_kl, bool surr) {
@@ -945,15 +964,13 @@ static int enqueue_update_device(trpo_dev *d, size_t maxiter, double resth, doub
     hipLaunchKernelGGL(step_kernel, dim3(1), dim3(STEP_T), 0, v.stream, (const double *)v.vec_x,
                        (const double *)v.vec_z, P, max_kl, u->fs, u->hst_dev + 3 * P + 3 + H);
     if (surr) {
-        rc = enqueue_surrogate(d, u->fs, 0, 1);
+        rc = enqueue_surrogate(d, u->fs, 0, 1, u->hst_dev + 3 * P + 2 + H);
         if (rc) return rc;
-        hipLaunchKernelGGL(copy64_kernel, dim3(1), dim3(64), 0, v.stream, (const double *)u->sums,
-                           u->hst_dev + 3 * P + 2 + H, 1);
     }
-    hipLaunchKernelGGL(export_solve_kernel, dim3(cdiv(P > H ? P : H, 256)), dim3(256), 0, v.stream, v.vec_b, v.vec_x,
-                       v.vec_z, adv_dev, v.cg_iter, v.cg_hist, P, H, u->hst_dev);
-    hipLaunchKernelGGL(copy64_kernel, dim3(1), dim3(128), 0, v.stream, v.cg_stats, u->hst_dev + 3 * P + 5 + H,
-                       TRPO_CG_STATS);
+    if (++u->seq == 0) u->seq = 1;
+    hipLaunchKernelGGL(export_solve_kernel, dim3(export_blocks(P, H)), dim3(256), 0, v.stream, v.vec_b, v.vec_x,
+                       v.vec_z, adv_dev, v.cg_iter, v.cg_hist, P, H, v.cg_stats, u->hst_dev,
+                       (unsigned *)(u->hst_dev + export_flags_at(P, H)), u->seq);
     HCHK(hipGetLastError());
     return 0;
 }
@@ -971,14 +988,19 @@ extern "C" int trpo_dev_update_solve(trpo_dev *d, size_t maxiter, double resth, 
     const size_t bytes = sizeof(double) * P;
     const bool surr = surr0 != nullptr;
     // outside any graph: buffers, and the rollout rows of the policy-gradient kernel (new rollout only)
-    if (ensure_host(u, (size_t)3 * P + 5 + H + TRPO_CG_STATS)) return -2;
+    if (ensure_host(u, export_flags_at(P, H) + cdiv(export_blocks(P, H), 2))) return -2;
     if (!u->fs) HCHK(trpo_malloc((void **)&u->fs, sizeof(double) * P));
     if (trpo_dev_pg_prepare(d, u->roll, u->roll_gen) < 0) return -2;
     // (capturing this whole sequence into one graph was measured: ~3 % faster per update, ~10 ms to
     // capture -- not kept)
     int rc = enqueue_update_device(d, maxiter, resth, max_kl, surr);
     if (rc) return rc;
-    DSYNC(d);
+    if (trpo_dev_has_collective(d)) {
+        DSYNC(d);                               // bounded wait, and the collective's own error
+    } else if (const int wrc = wait_host_flags(v.stream, (const unsigned *)(u->hst + export_flags_at(P, H)),
+                                               export_blocks(P, H), u->seq, 2000)) {
+        return wrc;
+    }
     if (surr0) *surr0 = u->hst[3 * P + 2 + H];
     if (stats) memcpy(stats, u->hst + 3 * P + 5 + H, sizeof(double) * TRPO_CG_STATS);
     if (shs_lm) {
@@ -1001,7 +1023,8 @@ extern "C" int trpo_dev_update_solve(trpo_dev *d, size_t maxiter, double resth, 
 
 // enqueue the surrogate sums of candidates theta + 2^-k fs, k = k0 .. k0+nk-1 (fs on the device),
 // all-reduced over the ranks, into u->sums[0 .. nk)
-static int enqueue_surrogate(trpo_dev *d, const double *fs, int k0, int nk) {
+// host_out (pinned, device-mapped; optional): without a collective the sums are stored there directly
+static int enqueue_surrogate(trpo_dev *d, const double *fs, int k0, int nk, double *host_out) {
     trpo_dev_view v;
     trpo_dev_get_view(d, &v);
     UpdState *u = state(d);
@@ -1029,9 +1052,17 @@ static int enqueue_surrogate(trpo_dev *d, const double *fs, int k0, int nk) {
         }
 #undef SURR_CASE
         if (rc) return rc;
+        if (host_out && !trpo_dev_has_collective(d)) {
+            hipLaunchKernelGGL(sum_slabs64_kernel, dim3(cdiv(nk, 16)), dim3(256), 0, v.stream, u->slabs, Gm, nk,
+                               host_out);
+            HCHK(hipGetLastError());
+            return 0;
+        }
         hipLaunchKernelGGL(sum_slabs64_kernel, dim3(cdiv(nk, 16)), dim3(256), 0, v.stream, u->slabs, Gm, nk, u->sums);
         HCHK(hipGetLastError());
         if (trpo_dev_allreduce64(d, u->sums, (size_t)nk)) return -4;
+        if (host_out)
+            hipLaunchKernelGGL(copy64_kernel, dim3(1), dim3(64), 0, v.stream, (const double *)u->sums, host_out, nk);
         return 0;
     }
     if (reg_path(net)) {
@@ -1054,6 +1085,7 @@ static int enqueue_surrogate(trpo_dev *d, const double *fs, int k0, int nk) {
     hipLaunchKernelGGL(sum_slabs64_kernel, dim3(cdiv(nk, 16)), dim3(256), 0, v.stream, u->slabs, Gs, nk, u->sums);
     HCHK(hipGetLastError());
     if (trpo_dev_allreduce64(d, u->sums, (size_t)nk)) return -4;
+    if (host_out) hipLaunchKernelGGL(copy64_kernel, dim3(1), dim3(64), 0, v.stream, (const double *)u->sums, host_out, nk);
     return 0;
 }
 
@@ -1445,15 +1477,15 @@ extern "C" int trpo_bdev_set_data(trpo_bdev *b, const double *obs, const double 
 
 // Waits until the nf flag words in pinned host memory read seq.  Spinning answers ~4.7 us sooner than
 // hipStreamSynchronize for one small launch (tools/micro/host_wait: 6.9 vs 11.6 us round trip); after
-// the first 100 us the stream is queried between spins, so a launch that failed returns its error
+// the first query_after_us the stream is queried between spins, so a launch that failed returns its error
 // instead of spinning (and one that completed without its flags is an error too).
-static int wait_host_flags(hipStream_t st, const unsigned *flags, int nf, unsigned seq) {
+static int wait_host_flags(hipStream_t st, const unsigned *flags, int nf, unsigned seq, long query_after_us) {
     const auto t0 = std::chrono::steady_clock::now();
     int k = 0;                                   // flags[0 .. k) already read seq
     for (unsigned long i = 1;; ++i) {
         while (k < nf && __atomic_load_n(flags + k, __ATOMIC_ACQUIRE) == seq) ++k;
         if (k == nf) return 0;
-        if ((i & 63) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(100)) {
+        if ((i & 63) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(query_after_us)) {
             const hipError_t e = hipStreamQuery(st);
             if (e == hipSuccess) {
                 while (k < nf && __atomic_load_n(flags + k, __ATOMIC_ACQUIRE) == seq) ++k;
@@ -1538,7 +1570,7 @@ extern "C" int trpo_bdev_eval_finish(trpo_bdev *b, double *gsum, double *pred) {
     const int P = net.P;
     if (b->lane_ok && P - net.A <= BL_PA_MAX) {
         const size_t foff = (size_t)P + 1 + b->n + (size_t)(P - net.A);
-        if (const int rc = wait_host_flags(b->stream, (const unsigned *)(b->hst + foff), cdiv(P + 1, 16), b->seq))
+        if (const int rc = wait_host_flags(b->stream, (const unsigned *)(b->hst + foff), cdiv(P + 1, 16), b->seq, 100))
             return rc;
     } else {
         HCHK(hipStreamSynchronize(b->stream));
