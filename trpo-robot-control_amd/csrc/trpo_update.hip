@@ -25,7 +25,6 @@
 #include <hip/hip_runtime.h>
 
 #include <math.h>
-#include <chrono>
 #include <stdlib.h>
 #include <string.h>
 
@@ -938,7 +937,6 @@ extern "C" int trpo_dev_policy_gradient(trpo_dev *d, double *b_host, double *adv
 }
 
 static int enqueue_surrogate(trpo_dev *d, const double *fs, int k0, int nk, double *host_out = nullptr);
-static int wait_host_flags(hipStream_t st, const unsigned *flags, int nf, unsigned seq, long query_after_us);
 // export_solve_kernel's grid and the offset of its flag words in the update's pinned buffer
 static int export_blocks(int P, int H) {
     const int m = P > H ? P : H;
@@ -997,7 +995,7 @@ extern "C" int trpo_dev_update_solve(trpo_dev *d, size_t maxiter, double resth, 
     if (rc) return rc;
     if (trpo_dev_has_collective(d)) {
         DSYNC(d);                               // bounded wait, and the collective's own error
-    } else if (const int wrc = wait_host_flags(v.stream, (const unsigned *)(u->hst + export_flags_at(P, H)),
+    } else if (const int wrc = trpo_wait_host_flags(v.stream, (const unsigned *)(u->hst + export_flags_at(P, H)),
                                                export_blocks(P, H), u->seq, 2000)) {
         return wrc;
     }
@@ -1475,27 +1473,6 @@ extern "C" int trpo_bdev_set_data(trpo_bdev *b, const double *obs, const double 
     return 0;
 }
 
-// Waits until the nf flag words in pinned host memory read seq.  Spinning answers ~4.7 us sooner than
-// hipStreamSynchronize for one small launch (tools/micro/host_wait: 6.9 vs 11.6 us round trip); after
-// the first query_after_us the stream is queried between spins, so a launch that failed returns its error
-// instead of spinning (and one that completed without its flags is an error too).
-static int wait_host_flags(hipStream_t st, const unsigned *flags, int nf, unsigned seq, long query_after_us) {
-    const auto t0 = std::chrono::steady_clock::now();
-    int k = 0;                                   // flags[0 .. k) already read seq
-    for (unsigned long i = 1;; ++i) {
-        while (k < nf && __atomic_load_n(flags + k, __ATOMIC_ACQUIRE) == seq) ++k;
-        if (k == nf) return 0;
-        if ((i & 63) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(query_after_us)) {
-            const hipError_t e = hipStreamQuery(st);
-            if (e == hipSuccess) {
-                while (k < nf && __atomic_load_n(flags + k, __ATOMIC_ACQUIRE) == seq) ++k;
-                return k == nf ? 0 : -2;
-            }
-            if (e != hipErrorNotReady) return -2;
-        }
-        __builtin_ia32_pause();
-    }
-}
 
 // theta: natural [W, B per layer] (P - A values); gsum[P + 1]: gradient sums (P - A entries),
 // then sum (y - t)^2 at P - A; pred (n, may be NULL) receives the predictions
@@ -1570,7 +1547,7 @@ extern "C" int trpo_bdev_eval_finish(trpo_bdev *b, double *gsum, double *pred) {
     const int P = net.P;
     if (b->lane_ok && P - net.A <= BL_PA_MAX) {
         const size_t foff = (size_t)P + 1 + b->n + (size_t)(P - net.A);
-        if (const int rc = wait_host_flags(b->stream, (const unsigned *)(b->hst + foff), cdiv(P + 1, 16), b->seq, 100))
+        if (const int rc = trpo_wait_host_flags(b->stream, (const unsigned *)(b->hst + foff), cdiv(P + 1, 16), b->seq, 100))
             return rc;
     } else {
         HCHK(hipStreamSynchronize(b->stream));
