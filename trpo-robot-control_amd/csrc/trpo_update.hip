@@ -54,6 +54,7 @@ struct UpdState {
     double *hst = nullptr, *hst_dev = nullptr;
     size_t hst_cap = 0;
     unsigned seq = 0;                       // export_solve_kernel's flags: the last update's sequence number
+    size_t flag_at = 0;                     // where they were zeroed last (they move with maxiter)
     unsigned roll_gen = 0;                 // bumped by every rollout upload
 };
 
@@ -966,6 +967,10 @@ static int enqueue_update_device(trpo_dev *d, size_t maxiter, double resth, doub
         if (rc) return rc;
     }
     if (++u->seq == 0) u->seq = 1;
+    if (export_flags_at(P, H) != u->flag_at) {     // a new layout: no stale word may read as this seq
+        memset(u->hst + export_flags_at(P, H), 0, sizeof(double) * cdiv(export_blocks(P, H), 2));
+        u->flag_at = export_flags_at(P, H);
+    }
     hipLaunchKernelGGL(export_solve_kernel, dim3(export_blocks(P, H)), dim3(256), 0, v.stream, v.vec_b, v.vec_x,
                        v.vec_z, adv_dev, v.cg_iter, v.cg_hist, P, H, v.cg_stats, u->hst_dev,
                        (unsigned *)(u->hst_dev + export_flags_at(P, H)), u->seq);
@@ -1350,6 +1355,7 @@ struct trpo_bdev {
     size_t hst_cap = 0;
     unsigned seq = 0;                            // the lane path's host hand-off: the last call's sequence number
     int started = 0, want_pred = 0;              // an eval_start without its eval_finish yet; with predictions
+    size_t flag_at = 0;                          // where the flag words were zeroed last (they move with n)
 };
 
 static int act_code64(char a) {
@@ -1505,6 +1511,10 @@ extern "C" int trpo_bdev_eval_start(trpo_bdev *b, const double *theta, int want_
         memcpy(th.v, theta, sizeof(double) * (P - net.A));
         if (++b->seq == 0) b->seq = 1;
         const size_t foff = (size_t)P + 1 + b->n + (size_t)(P - net.A);
+        if (foff != b->flag_at) {                  // a new layout: no stale word may read as this seq
+            memset(b->hst + foff, 0, sizeof(double) * cdiv(nfl, 2));
+            b->flag_at = foff;
+        }
         hipLaunchKernelGGL(baseline_lane_kernel, dim3(b->Gl), dim3(256), 0, b->stream, net, th, (const double *)b->obs,
                            (const double *)b->target, (int)b->n, b->slabs, want_pred ? b->hst_dev + P + 1 : nullptr);
         hipLaunchKernelGGL(sum_slabs64_host_kernel, dim3(nfl), dim3(256), 0, b->stream, (const double *)b->slabs, b->Gl,
