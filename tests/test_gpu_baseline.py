@@ -144,3 +144,25 @@ def test_evaluate_sees_arrays_rewritten_in_place():
         assert abs(f - fr) <= 1e-13 * abs(fr), change
         assert cases.rel_l2(g, gr) <= 1e-12, change
         assert cases.rel_l2(p.predict, pr) <= 1e-12, change
+
+
+def test_evaluate_after_set_data_shrinks():
+    """Round 6: the lane path's flag words sit behind the predictions, so they move when set_data changes
+    the sample count; evaluations after a larger and then a smaller batch on one context equal a fresh
+    context's, bit for bit."""
+    L, acf = [16, 16, 16, 1], "lttl"
+    big = trpo_amd.synth.make_baseline_problem(L, 20, 150)
+    small = trpo_amd.synth.make_baseline_problem(L, 7, 111)
+    with trpo_amd.Baseline(L, acf) as b:
+        got = []
+        for x, obs, tgt, ne, el in ((*big, 20, 150), (*small, 7, 111), (*big, 20, 150)):
+            b.set_data(obs, tgt, ne, el)
+            got.append((b.evaluate(x, want_predict=True), b.evaluate(x)))
+    for (x, obs, tgt, ne, el), (r, r2) in zip(((*big, 20, 150), (*small, 7, 111), (*big, 20, 150)), got):
+        with trpo_amd.Baseline(L, acf) as f:
+            f.set_data(obs, tgt, ne, el)
+            e = f.evaluate(x, want_predict=True)
+        assert r[0] == e[0] and r2[0] == e[0]
+        np.testing.assert_array_equal(r[1], e[1])
+        np.testing.assert_array_equal(r2[1], e[1])
+        np.testing.assert_array_equal(r[2], e[2])

@@ -216,3 +216,24 @@ def test_fvp_of_v_after_replayed_solves(solves, monkeypatch):
         ctx.synchronize()
         z = ctx.download_z()
     assert cases.rel_l2(z, z_ref) <= 1e-6
+
+
+def test_updates_with_changing_max_iter():
+    """Round 6: an update's results come back through pinned memory behind per-block flag words whose
+    offset moves with max_iter (the history's length).  Updates on one context with max_iter 10, 4, 12, 10
+    each equal the same update on a fresh context, bit for bit."""
+    from trpo_amd import synth
+    layers, n = [15, 16, 16, 3], 3000
+    th, obs = synth.make_theta(layers), synth.make_obs(n, layers[0])
+    std = np.ones(layers[-1])
+    mean, action, adv = synth.make_rollout(layers, "lttl", th, obs, std)
+    with trpo_amd.Context(layers, "lttl", th, obs, std, 0.1) as ctx:
+        ctx.set_rollout(mean, action, adv)
+        got = [(m, ctx.update(max_iter=m)) for m in (10, 4, 12, 10)]
+    for m, r in got:
+        with trpo_amd.Context(layers, "lttl", th, obs, std, 0.1) as fresh:
+            fresh.set_rollout(mean, action, adv)
+            f = fresh.update(max_iter=m)
+        for key in ("theta", "x", "b"):
+            np.testing.assert_array_equal(r[key], f[key], err_msg="max_iter %d %s" % (m, key))
+        assert r["accepted"] == f["accepted"] and r["shs"] == f["shs"]
