@@ -292,6 +292,16 @@ def test_peer_missing_rank_times_out(proto, monkeypatch, capfd):
     assert "peer exchange timed out: rank 0 of 2" in err, err
     assert "exchange 1: after 0.5 s no data from rank 1" in err, err
     assert ("tag 0, expected 1; form %s" % proto) in err, err
+    assert "rank 0 of 2 polls its window at" in err, err
+    if proto == "4":
+        # the pushing side (round 6): rank 0's pusher to rank 1 reports exchange 1 and where it went --
+        # inside the window of rank 1 as attached in this process
+        import re
+        m = re.search(r"last pushed exchange 1 \((\d+) elements\) to rank 1 at (0x[0-9a-f]+) "
+                      r"\(that window as attached here: (0x[0-9a-f]+)\)", err)
+        assert m, err
+        addr, base = int(m.group(2), 16), int(m.group(3), 16)
+        assert base <= addr < base + (1 << 26), err
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])

@@ -91,6 +91,15 @@ __device__ void peer_report(PeerErr *err, int rank, int wg, unsigned e, int slot
     st_sys_i(&err->code, 2);
 }
 
+// The pushing side's record (round 6, after the in-process timeout of DESIGN §6.2): every pushing workgroup
+// of the granule forms leaves, in device memory, the exchange number and the address it pushed its first
+// element to; a report prints them beside the pollers' records, so a push that "never arrived" shows
+// whether it went to the window the peer polls.  One 32-byte store per pushing workgroup and exchange.
+struct PeerPush {
+    unsigned long long e, addr;
+    int rank, to, count, pad;
+};
+
 struct trpo_peer {
     int device;
     size_t S;                        // slot length (fp64)
@@ -100,6 +109,7 @@ struct trpo_peer {
     void *opened[PEER_WMAX];         // IPC-opened peer windows (closed at destroy)
     unsigned long long *cnt;         // [PEER_WMAX] per-workgroup exchange counters
     PeerErr *err_h, *err_d;          // pinned host error record and its device view
+    PeerPush *push_d;                // [2 PEER_WMAX] the pushing workgroups' last pushes (device)
     unsigned long long wait_ticks;   // a poll's bound (TRPO_PEER_WAIT_MS, default 3 s)
     int reported;                    // the records were printed
     int *zero_d;                     // a device word that stays 0 (the granule forms' `done` when none is given)
@@ -253,7 +263,7 @@ template <int W, bool SPLIT = false>
 __global__ void __launch_bounds__(PEER_T)
 peer_granule_w_kernel(const double *__restrict__ in, int R, int Rstride, int count, PeerWins<W> wins, int rank,
                       int S, double *__restrict__ out, unsigned long long *cnt, PeerErr *err, const int *done,
-                      size_t goff, unsigned long long wticks) {
+                      size_t goff, unsigned long long wticks, PeerPush *push) {
     const int t = blockIdx.x, tid = threadIdx.x;
     const bool pusher = !SPLIT || t < W, poller = !SPLIT || t >= W;   // grid-uniform per workgroup
     const int ts = SPLIT ? t - W : t;                                 // the slice this workgroup sums
@@ -291,6 +301,7 @@ peer_granule_w_kernel(const double *__restrict__ in, int R, int Rstride, int cou
                     st_sys64(dst + 2 * i + 1, tag | (b >> 32));
                 }
             }
+            if (i0 == 0 && tid == 0) push[t] = PeerPush{e, (unsigned long long)(size_t)dst, rank, t, count, 0};
         }
         if (!poller) {                                 // SPLIT pusher: done once its stores are issued
             if (tid == 0) cnt[t] = e;
@@ -484,6 +495,7 @@ static void peer_free(trpo_peer *p) {
     if (p->dwins) hipFree(p->dwins);
     if (p->cnt) hipFree(p->cnt);
     if (p->zero_d) hipFree(p->zero_d);
+    if (p->push_d) hipFree(p->push_d);
     if (p->err_h) hipHostFree(p->err_h);
     free(p);
 }
@@ -522,6 +534,8 @@ trpo_peer *trpo_peer_create(int device, size_t S) {
               hipMemset(p->cnt, 0, sizeof(unsigned long long) * 2 * PEER_WMAX) == hipSuccess &&
               trpo_malloc((void **)&p->zero_d, sizeof(int)) == hipSuccess &&
               hipMemset(p->zero_d, 0, sizeof(int)) == hipSuccess &&
+              trpo_malloc((void **)&p->push_d, sizeof(PeerPush) * 2 * PEER_WMAX) == hipSuccess &&
+              hipMemset(p->push_d, 0, sizeof(PeerPush) * 2 * PEER_WMAX) == hipSuccess &&
               hipHostMalloc((void **)&p->err_h, sizeof(PeerErr), TRPO_HOST_COHERENT) == hipSuccess;
     if (ok) {
         memset(p->err_h, 0, sizeof(PeerErr));
@@ -614,10 +628,10 @@ int trpo_peer_allreduce(trpo_peer *p, hipStream_t st, const double *in, int R, i
         for (int r = 0; r < W; ++r) pw.w[r] = p->hwins[r];                                                           \
         if (split)                                                                                                   \
             hipLaunchKernelGGL((peer_granule_w_kernel<W, true>), dim3(2 * W), dim3(PEER_T), 0, st, in, R, Rstride,    \
-                               count, pw, p->rank, (int)p->S, out, p->cnt, p->err_d, dz, go, p->wait_ticks);        \
+                               count, pw, p->rank, (int)p->S, out, p->cnt, p->err_d, dz, go, p->wait_ticks, p->push_d);\
         else                                                                                                         \
             hipLaunchKernelGGL((peer_granule_w_kernel<W, false>), dim3(W), dim3(PEER_T), 0, st, in, R, Rstride,       \
-                               count, pw, p->rank, (int)p->S, out, p->cnt, p->err_d, dz, go, p->wait_ticks);        \
+                               count, pw, p->rank, (int)p->S, out, p->cnt, p->err_d, dz, go, p->wait_ticks, p->push_d);\
         break;                                                                                                       \
     }
         switch (p->world) {
@@ -659,6 +673,19 @@ void trpo_peer_report(trpo_peer *p) {
                 p->world, e->code);
     else if (shown > 8)
         fprintf(stderr, "[trpo_mi355x] ... %d timed-out waves in all\n", shown);
+    // the pushing side of this rank (granule forms): where its last pushes went, beside its own window
+    PeerPush pu[2 * PEER_WMAX];
+    if (p->push_d && hipMemcpy(pu, p->push_d, sizeof pu, hipMemcpyDeviceToHost) == hipSuccess) {
+        fprintf(stderr, "[trpo_mi355x] rank %d of %d polls its window at %p\n", p->rank, p->world, (void *)p->win);
+        for (int i = 0; i < 2 * PEER_WMAX; ++i)
+            if (pu[i].e)
+                fprintf(stderr, "[trpo_mi355x] rank %d, pushing workgroup %d: last pushed exchange %llu (%d elements) "
+                                "to rank %d at %p (that window as attached here: %p)\n",
+                        pu[i].rank, i, pu[i].e, pu[i].count, pu[i].to, (void *)(size_t)pu[i].addr,
+                        pu[i].to < PEER_WMAX ? (void *)p->hwins[pu[i].to] : NULL);
+    } else {
+        (void)hipGetLastError();
+    }
 }
 size_t trpo_peer_slot(const trpo_peer *p) { return p ? p->S : 0; }
 int trpo_peer_proto(const trpo_peer *p) { return p ? p->proto : 0; }
