@@ -91,11 +91,11 @@ def test_lbfgs_fit_matches_oracle_fit():
 
 
 @pytest.mark.parametrize("num_ep,ep_len", [(1, 20), (5, 106), (20, 150), (40, 300)])
-def test_lane_kernel_in_launch_sum_and_handoff(num_ep, ep_len, monkeypatch):
-    """Round 6: the lane kernel sums its block slabs in the same launch (groups of 16 blocks, then the
-    groups) and hands the result over through pinned memory.  Grids of 1, 17 (a last group of one
-    block), 94 and 256 blocks (16 full groups) against the one-lane kernel, and repeated calls -- with
-    and without predictions, on changing parameters -- bit-identical to a fresh context's."""
+def test_lane_kernel_grids_and_handoff(num_ep, ep_len, monkeypatch):
+    """Round 6: the lane kernel takes theta by value and its slab sum hands the result over through pinned
+    memory (per-block flag words the host spins on).  Batches giving grids of 2, 34, 188 and 256 blocks
+    (one sample per 16-lane group, at most 256 blocks) against the one-lane kernel, and repeated calls --
+    with and without predictions, on changing parameters -- bit-identical to a fresh context's."""
     L, acf = [16, 16, 16, 1], "lttl"
     x, obs, tgt = trpo_amd.synth.make_baseline_problem(L, num_ep, ep_len)
     xs = [x, x * 0.9 + 0.01, x]
