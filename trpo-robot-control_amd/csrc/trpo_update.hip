@@ -466,6 +466,36 @@ __global__ void pg_finish2_kernel(const double *__restrict__ wsum, const double 
     if (q < P) b[q] = (q < P - A ? wsum[q] : lsum[q - (P - A)]) / n_total;
 }
 
+// Without a collective (round 6): the LogStd / Adv slab sums and the policy-gradient vector in ONE launch
+// instead of sum_slabs64_kernel + pg_finish2_kernel -- blocks [0, nb) write b's weight / bias entries
+// (wsum / N), block nb sums the A + 1 LogStd / Adv columns exactly as sum_slabs64_kernel's single block
+// does (same partial order, same bits; A + 1 <= 16), keeps them in lsum (sum(Adv) at A) and writes b's
+// LogStd entries.
+__global__ void pg_sum_finish2_kernel(const double *__restrict__ wsum, const double *__restrict__ slabs, int G, int A,
+                                      double n_total, int P, double *__restrict__ lsum, double *__restrict__ b) {
+    const int nb = (int)gridDim.x - 1;
+    if ((int)blockIdx.x < nb) {
+        const int q = blockIdx.x * blockDim.x + threadIdx.x;
+        if (q < P - A) b[q] = wsum[q] / n_total;
+        return;
+    }
+    __shared__ double part[16][17];
+    const int tq = threadIdx.x & 15, tj = threadIdx.x >> 4, len = A + 1;
+    double s = 0.0;
+    if (tq < len) {
+#pragma unroll 8
+        for (int bb = tj; bb < G; bb += 16) s += slabs[(long)bb * len + tq];
+    }
+    part[tj][tq] = s;
+    __syncthreads();
+    if (tj == 0 && tq < len) {
+        double t = 0.0;
+        for (int j = 0; j < 16; ++j) t += part[j][tq];
+        lsum[tq] = t;
+        if (tq < A) b[P - A + tq] = t / n_total;
+    }
+}
+
 // LogStd part of the policy gradient and sum(Adv), fp64: block b writes
 // slabs[b][i] = sum over its samples of Adv ((Action - Mean)^2 / sigma^2 - 1)  (i < A),
 // slabs[b][A] = sum of Adv  (src/TRPO_Update.c:297-303, :372)
@@ -898,6 +928,13 @@ static int enqueue_policy_gradient(trpo_dev *d, const double **adv_dev) {
         // weights / biases by the MFMA tile kernel (fp32 per sample, fp64 sums); LogStd + Adv in fp64
         const int A = net.A;
         hipLaunchKernelGGL(pg_logstd_kernel, dim3(G), dim3(UT), 0, v.stream, v.theta64, P, A, u->roll, n, u->slabs);
+        if (A + 1 <= 16 && !trpo_dev_has_collective(d)) {
+            hipLaunchKernelGGL(pg_sum_finish2_kernel, dim3(cdiv(P - A, 256) + 1), dim3(256), 0, v.stream, wsum,
+                               (const double *)u->slabs, G, A, v.n_total, P, u->sum, v.vec_b);
+            HCHK(hipGetLastError());
+            *adv_dev = u->sum + A;
+            return 0;
+        }
         hipLaunchKernelGGL(sum_slabs64_kernel, dim3(cdiv(A + 1, 16)), dim3(256), 0, v.stream, u->slabs, G, A + 1,
                            u->sum);
         HCHK(hipGetLastError());
